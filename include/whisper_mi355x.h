@@ -1,0 +1,174 @@
+/*
+ * whisper_mi355x.h — C ABI of the MI355X-native Whisper hot path.
+ *
+ * This is the drop-in boundary for szuwgh/whisper.rs (snapshot 2024-08-07).
+ * Every entry point below names the reference item it replaces
+ * (file:line into /root/reference/src/main.rs).  A Rust caller binds this
+ * header with a thin `extern "C"` block; the Python mirror
+ * whisper.rs_amd/wmi.py binds it with ctypes.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Every array passed in or out is a HOST
+ *    array owned by the caller; results are copied out.  Device memory is
+ *    owned by the context.
+ *  - Every call returns an int status (enum wmi_status).  Nothing aborts.
+ *    wmi_last_error() gives the detailed message (tensor name, sizes, ...),
+ *    mirroring the formatted WsError variants (main.rs:51-72).
+ *  - One context per host thread per GPU; calls are stream-ordered on the
+ *    context's HIP stream and synchronous at return (main.rs takes
+ *    `&mut WhisperContext`, so the reference is single-caller too).
+ *  - Layouts are the reference's: mel [n_mel][n_len] f32 (main.rs:1633),
+ *    encoder output [n_ctx][n_state] f32 (ggml ne [n_state, n_ctx]),
+ *    cross K/V [n_text_layer][n_ctx][n_state] f16 (main.rs:2018-2030).
+ */
+#ifndef WHISPER_MI355X_H
+#define WHISPER_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* WsError (main.rs:51-72) mapped 1:1, plus device-side codes. */
+enum wmi_status {
+    WMI_OK = 0,
+    WMI_E_IO = 1,             /* WsError::UnexpectIO        main.rs:54-55 */
+    WMI_E_BAD_MAGIC = 2,      /* WsError::BadMagic          main.rs:56-57 */
+    WMI_E_NO_SPACE = 3,       /* WsError::NotEnoughSpace    main.rs:58-59 */
+    WMI_E_UNKNOWN_TENSOR = 4, /* WsError::UnknownTensor     main.rs:60-61 */
+    WMI_E_BAD_REF_TENSOR = 5, /* WsError::BadRefTensor      main.rs:62-63 */
+    WMI_E_WRONG_SIZE = 6,     /* WsError::WrongSizeTensor   main.rs:64-65 */
+    WMI_E_WRONG_SHAPE = 7,    /* WsError::WrongShapeTensor  main.rs:66-67 */
+    WMI_E_WRONG_BYTES = 8,    /* WsError::WrongBytesTensor  main.rs:68-69 */
+    WMI_E_OP = 9,             /* WsError::WrongGTensor      main.rs:70-71 */
+    WMI_E_UNEXPECTED = 10,    /* WsError::Unexpected        main.rs:52-53 */
+    WMI_E_HIP = 11,           /* HIP runtime / kernel launch failure */
+    WMI_E_RCCL = 12,          /* RCCL failure */
+    WMI_E_UNSUPPORTED = 13,   /* valid file, feature not built (e.g. f32 matrices) */
+    WMI_E_INVALID_ARG = 14    /* bad pointer / size / state order */
+};
+
+/* WhisperHparams (main.rs:607-619), same field order as the file. */
+typedef struct wmi_hparams {
+    int32_t n_vocab;
+    int32_t n_audio_ctx;
+    int32_t n_audio_state;
+    int32_t n_audio_head;
+    int32_t n_audio_layer;
+    int32_t n_text_ctx;
+    int32_t n_text_state;
+    int32_t n_text_head;
+    int32_t n_text_layer;
+    int32_t n_mels;
+    int32_t f16;
+} wmi_hparams;
+
+/* WhisperVocab special ids after the multilingual shift (main.rs:557-575, 433-440). */
+typedef struct wmi_special_tokens {
+    int32_t eot, sot, prev, solm, not_, beg, translate, transcribe;
+    int32_t is_multilingual;
+} wmi_special_tokens;
+
+/* Per-stage device times of the last pipeline call, milliseconds (hipEvents).
+ * Replaces the never-written t_*_us fields of WhisperContext (main.rs:334-339). */
+typedef struct wmi_timings {
+    float mel_ms;
+    float encode_ms;     /* conv stem -> ln_post */
+    float cross_kv_ms;   /* cross-attention K/V precompute */
+    float decode_ms;     /* prompt + generated tokens */
+    int32_t n_decode_steps;
+} wmi_timings;
+
+typedef struct wmi_context wmi_context;
+
+/* ---- lifecycle ------------------------------------------------------ */
+
+/* WhisperContext::new(fname) (main.rs:366-503): open, magic, hparams,
+ * filters, vocab (+extra tokens), weights; then upload to `device`.
+ * max_clips sizes the device workspace for batched calls (>= 1). */
+int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context **out);
+void wmi_free(wmi_context *ctx);
+const char *wmi_strerror(int status);
+const char *wmi_last_error(const wmi_context *ctx);
+/* Library-level last error (for failures before a context exists). */
+const char *wmi_last_error_global(void);
+
+int wmi_get_hparams(const wmi_context *ctx, wmi_hparams *out);
+int wmi_get_special_tokens(const wmi_context *ctx, wmi_special_tokens *out);
+/* WhisperContext.exp_n_audio_ctx (main.rs:362, 1803-1807): 0 = n_audio_ctx. */
+int wmi_set_audio_ctx(wmi_context *ctx, int n_audio_ctx);
+/* id_to_token (main.rs:578-592, 442-467): copies the token bytes (not NUL
+ * terminated) into buf, *len = byte count; WMI_E_NO_SPACE if cap too small. */
+int wmi_token_to_bytes(const wmi_context *ctx, int32_t id, char *buf, size_t cap, size_t *len);
+
+/* ---- pipeline (reference entry points) ------------------------------ */
+
+/* whisper_pcm_to_mel (main.rs:1681-1707): f32 PCM (s16/32768) -> log-mel. */
+int wmi_pcm_to_mel(wmi_context *ctx, const float *pcm, size_t n_samples);
+/* Batched form: n_clips independent clips (each <= max_clips). */
+int wmi_pcm_to_mel_batch(wmi_context *ctx, int n_clips, const float *const *pcm, const size_t *n_samples);
+
+/* whisper_encode (main.rs:1799-2063): mel window at mel_offset -> conv stem
+ * -> encoder blocks -> ln_post -> cross-attention K/V for every decoder
+ * layer.  n_threads is accepted and ignored, as in the reference (:1799).
+ * Runs on every clip loaded by the last pcm_to_mel call. */
+int wmi_encode(wmi_context *ctx, int n_threads, int mel_offset);
+
+/* Greedy decode (the reference declares the decoder but has
+ * no forward pass).  Prompt = [SOT] (.en) or [SOT, lang(en), transcribe],
+ * then NOT.  Generates up to max_tokens ids per clip; stops a clip at EOT
+ * unless suppress_eot != 0 (then exactly max_tokens).  tokens is
+ * [n_clips][max_tokens]; n_tokens[c] = ids written for clip c. */
+int wmi_decode_greedy(wmi_context *ctx, int max_tokens, int suppress_eot,
+                      int32_t *tokens, int32_t *n_tokens);
+
+/* Teacher-forced decoder logits for clip `clip`: feeds tokens[0..n) one at a
+ * time from position 0 and writes logits[n][n_vocab] (f32). */
+int wmi_decode_logits(wmi_context *ctx, int clip, const int32_t *tokens, int n_tokens, float *logits);
+
+/* Transcribe: pcm_to_mel -> encode -> decode_greedy for one clip. */
+int wmi_full(wmi_context *ctx, const float *pcm, size_t n_samples, int max_tokens,
+             int32_t *tokens, int32_t *n_tokens);
+
+/* ---- device-resident benchmark path --------------------------------- */
+
+/* Upload n_clips PCM clips to HBM once (untimed). */
+int wmi_stage_pcm(wmi_context *ctx, int n_clips, const float *const *pcm, const size_t *n_samples);
+/* mel -> encode -> cross-KV -> decode (n_decode tokens, EOT suppressed) on
+ * the staged clips; token ids stay on the device until wmi_get_tokens. */
+int wmi_run_staged(wmi_context *ctx, int mel_offset, int n_decode);
+int wmi_get_tokens(const wmi_context *ctx, int32_t *tokens, size_t cap, int32_t *n_per_clip);
+int wmi_get_timings(const wmi_context *ctx, wmi_timings *out);
+/* Block until all work queued on the context's stream is done. */
+int wmi_sync(wmi_context *ctx);
+
+/* ---- parity getters (copy device results into caller-owned buffers) --- */
+
+/* ctx.mel (main.rs:1574-1578): [n_mel][n_len] f32. */
+int wmi_get_mel(const wmi_context *ctx, int clip, float *out, size_t cap, int32_t *n_mel, int32_t *n_len);
+/* ln_post output (main.rs:1977-1986): [n_ctx][n_audio_state] f32. */
+int wmi_get_encoder_out(const wmi_context *ctx, int clip, float *out, size_t cap);
+/* memory_cross_k / memory_cross_v (main.rs:2018-2030): f16 bit patterns,
+ * [n_text_layer][n_ctx][n_text_state] each. */
+int wmi_get_cross_kv(const wmi_context *ctx, int clip, uint16_t *k, uint16_t *v, size_t cap);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ------------------ */
+
+/* Size of the opaque RCCL unique id blob (ncclUniqueId). */
+size_t wmi_dist_id_size(void);
+/* Rank 0 creates the id; every rank passes the same bytes to init. */
+int wmi_dist_make_id(void *id_out);
+int wmi_dist_init(wmi_context *ctx, int rank, int world, const void *id);
+/* Gather every rank's token block ([n_clips][n_decode] int32 + counts) to
+ * root 0 over RCCL; out (root only) is [world][n_clips][n_decode]. */
+int wmi_dist_gather_tokens(wmi_context *ctx, int32_t *out, size_t cap);
+/* Device-side barrier over the communicator (an RCCL all-reduce of one int). */
+int wmi_dist_barrier(wmi_context *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WHISPER_MI355X_H */

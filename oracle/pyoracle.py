@@ -1,0 +1,142 @@
+"""ctypes binding of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+(as the checker / CPU baseline).  The product path never imports this file.
+PARITY UNPINNED: see oracle/README.md.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        vp, i32, sz = C.c_void_p, C.c_int32, C.c_size_t
+        fp = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+        hp_ = np.ctypeslib.ndpointer(np.uint16, flags="C_CONTIGUOUS")
+        ip = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+        L.or_load.argtypes = [C.c_char_p, C.POINTER(vp), C.c_char_p, sz]
+        L.or_free.argtypes = [vp]
+        L.or_get_hparams.argtypes = [vp, ip]
+        L.or_special_tokens.argtypes = [vp, ip]
+        L.or_prompt.argtypes = [vp, ip]
+        L.or_tables.argtypes = [hp_, hp_]
+        L.or_set_dot_mode.argtypes = [C.c_int]
+        L.or_mel.argtypes = [vp, fp, sz, C.c_int, C.c_void_p, C.POINTER(i32)]
+        L.or_encode.argtypes = [vp, fp, i32, C.c_int, C.c_int, C.c_int, fp, hp_, hp_, C.c_void_p]
+        L.or_decode_logits.argtypes = [vp, hp_, hp_, C.c_int, ip, C.c_int, C.c_int, fp]
+        L.or_decode_greedy.argtypes = [vp, hp_, hp_, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.POINTER(i32), fp]
+        _lib = L
+    return _lib
+
+
+HP_NAMES = ("n_vocab", "n_audio_ctx", "n_audio_state", "n_audio_head", "n_audio_layer", "n_text_ctx",
+            "n_text_state", "n_text_head", "n_text_layer", "n_mels", "f16")
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def set_dot_mode(exact_double: bool) -> None:
+    """Switch dot-product accumulation (noise-floor measurement only)."""
+    lib().or_set_dot_mode(int(exact_double))
+
+
+def tables():
+    g = np.zeros(65536, np.uint16)
+    e = np.zeros(65536, np.uint16)
+    lib().or_tables(g, e)
+    return g, e
+
+
+class OracleModel:
+    def __init__(self, path: str):
+        L = lib()
+        h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        rc = L.or_load(path.encode(), C.byref(h), err, 512)
+        if rc != 0:
+            raise OracleError(rc, err.value.decode())
+        self.h = h
+        hp = np.zeros(11, np.int32)
+        L.or_get_hparams(h, hp)
+        self.hp = dict(zip(HP_NAMES, (int(x) for x in hp)))
+        sp = np.zeros(9, np.int32)
+        L.or_special_tokens(h, sp)
+        self.special = dict(zip(("eot", "sot", "prev", "solm", "not", "beg", "translate", "transcribe",
+                                 "multilingual"), (int(x) for x in sp)))
+
+    def close(self):
+        if self.h:
+            lib().or_free(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def prompt(self):
+        out = np.zeros(8, np.int32)
+        n = lib().or_prompt(self.h, out)
+        return out[:n].tolist()
+
+    def mel(self, pcm: np.ndarray, n_threads: int = 4) -> np.ndarray:
+        pcm = np.ascontiguousarray(pcm, np.float32)
+        n_len = C.c_int32()
+        lib().or_mel(self.h, pcm, pcm.size, n_threads, None, C.byref(n_len))
+        out = np.zeros((self.hp["n_mels"], n_len.value), np.float32)
+        rc = lib().or_mel(self.h, pcm, pcm.size, n_threads, out.ctypes.data, C.byref(n_len))
+        if rc:
+            raise OracleError(rc, "mel")
+        return out
+
+    def encode(self, mel: np.ndarray, n_ctx: int = 0, mel_offset: int = 0, n_threads: int = 8, probe: bool = False):
+        hp = self.hp
+        n_ctx = n_ctx or hp["n_audio_ctx"]
+        n = hp["n_audio_state"]
+        mel = np.ascontiguousarray(mel, np.float32)
+        enc = np.zeros((n_ctx, n), np.float32)
+        ck = np.zeros((hp["n_text_layer"], n_ctx, hp["n_text_state"]), np.uint16)
+        cv = np.zeros_like(ck)
+        pr = np.zeros((hp["n_audio_layer"] + 1, n_ctx, n), np.float32) if probe else None
+        rc = lib().or_encode(self.h, mel, mel.shape[1], mel_offset, n_ctx, n_threads, enc, ck, cv,
+                             pr.ctypes.data if probe else None)
+        if rc:
+            raise OracleError(rc, "encode")
+        return (enc, ck, cv, pr) if probe else (enc, ck, cv)
+
+    def decode_logits(self, ck, cv, tokens, n_threads: int = 8) -> np.ndarray:
+        tokens = np.ascontiguousarray(tokens, np.int32)
+        out = np.zeros((tokens.size, self.hp["n_vocab"]), np.float32)
+        rc = lib().or_decode_logits(self.h, ck, cv, ck.shape[1], tokens, tokens.size, n_threads, out)
+        if rc:
+            raise OracleError(rc, "decode_logits")
+        return out
+
+    def decode_greedy(self, ck, cv, max_tokens: int, suppress_eot: bool = False, n_threads: int = 8):
+        toks = np.zeros(max_tokens, np.int32)
+        margins = np.zeros(max_tokens, np.float32)
+        n = C.c_int32()
+        rc = lib().or_decode_greedy(self.h, ck, cv, ck.shape[1], max_tokens, int(suppress_eot), n_threads, toks,
+                                    C.byref(n), margins)
+        if rc:
+            raise OracleError(rc, "decode_greedy")
+        return toks[:n.value], margins[:n.value]

@@ -1,0 +1,1350 @@
+// wmi_api.cpp — C ABI of the MI355X Whisper hot path (include/whisper_mi355x.h).
+//
+// Host side of the drop-in boundary for szuwgh/whisper.rs:
+//   WhisperContext::new          main.rs:366-503   -> wmi_init_from_file
+//   whisper_pcm_to_mel           main.rs:1681-1707 -> wmi_pcm_to_mel[_batch]
+//   whisper_encode               main.rs:1799-2063 -> wmi_encode
+//   (decoder: declared only in the reference, main.rs:694-731) -> wmi_decode_*
+// The file parser reproduces the reference loader's checks and error order
+// (main.rs:1384-1475); weights are then packed once for the kernels and
+// uploaded into one device arena, replacing the reference's four fixed-size
+// byte arenas (main.rs:402-418) with a workspace planned from the hparams.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/whisper_mi355x.h"
+#include "wmi_internal.h"
+
+#pragma clang fp contract(off)
+
+using namespace wmi;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+// ---------------------------------------------------------------------------
+// host f16 helpers (round to nearest even, as F16C / v_cvt_f16_f32)
+// ---------------------------------------------------------------------------
+uint16_t f32_to_f16(float f) {
+    uint32_t x;
+    memcpy(&x, &f, 4);
+    const uint32_t sign = (x >> 16) & 0x8000u;
+    uint32_t mant = x & 0x7fffffu;
+    const int exp = (int)((x >> 23) & 0xffu);
+    if (exp == 0xff) return (uint16_t)(sign | 0x7c00u | (mant ? 0x200u : 0u));
+    const int e = exp - 127 + 15;
+    if (e >= 31) return (uint16_t)(sign | 0x7c00u);
+    if (e <= 0) {
+        if (e < -10) return (uint16_t)sign;
+        mant |= 0x800000u;
+        const int shift = 14 - e;
+        uint32_t h = mant >> shift;
+        const uint32_t rem = mant & ((1u << shift) - 1u), halfway = 1u << (shift - 1);
+        if (rem > halfway || (rem == halfway && (h & 1u))) ++h;
+        return (uint16_t)(sign | h);
+    }
+    uint32_t h = sign | ((uint32_t)e << 10) | (mant >> 13);
+    const uint32_t rem = mant & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+    return (uint16_t)h;
+}
+
+float f16_to_f32(uint16_t h) {
+    const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+    const uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+    uint32_t x;
+    if (e == 0) {
+        if (m == 0) x = sign;
+        else {
+            int ee = -1;
+            uint32_t mm = m;
+            do { ++ee; mm <<= 1; } while (!(mm & 0x400u));
+            x = sign | ((uint32_t)(127 - 15 - ee) << 23) | ((mm & 0x3ffu) << 13);
+        }
+    } else if (e == 31) {
+        x = sign | 0x7f800000u | (m << 13);
+    } else {
+        x = sign | ((e - 15 + 127) << 23) | (m << 13);
+    }
+    float f;
+    memcpy(&f, &x, 4);
+    return f;
+}
+
+// ggml_init tables (ggml-1.0.3): GELU and exp over every f16 value
+void build_tables(std::vector<uint16_t> &gelu, std::vector<uint16_t> &expt) {
+    const float GELU_COEF_A = 0.044715f;
+    const float SQRT_2_OVER_PI = 0.79788456080286535587989211986876f;
+    gelu.resize(65536);
+    expt.resize(65536);
+    for (int i = 0; i < 65536; ++i) {
+        const float f = f16_to_f32((uint16_t)i);
+        gelu[i] = f32_to_f16(0.5f * f * (1.0f + tanhf(SQRT_2_OVER_PI * f * (1.0f + GELU_COEF_A * f * f))));
+        expt[i] = f32_to_f16((float)exp((double)f));
+    }
+}
+
+// main.rs:1567-1569, 1495, 1537: the reference's exact f32 expressions
+void build_mel_tables(MelTables &t) {
+    const float PI_F = 3.14159265358979323846264338327950288f;
+    for (int i = 0; i < 400; ++i) t.hann[i] = 0.5f * (1.0f - cosf((2.0f * PI_F * (float)i) / 400.0f));
+    for (int k = 0; k < 200; ++k) { float a = 2.0f * PI_F * (float)k / 400.0f; t.c400[k] = cosf(a); t.s400[k] = sinf(a); }
+    for (int k = 0; k < 100; ++k) { float a = 2.0f * PI_F * (float)k / 200.0f; t.c200[k] = cosf(a); t.s200[k] = sinf(a); }
+    for (int k = 0; k < 50; ++k) { float a = 2.0f * PI_F * (float)k / 100.0f; t.c100[k] = cosf(a); t.s100[k] = sinf(a); }
+    for (int k = 0; k < 25; ++k) { float a = 2.0f * PI_F * (float)k / 50.0f; t.c50[k] = cosf(a); t.s50[k] = sinf(a); }
+    for (int p = 0; p < 625; ++p) { float a = 2.0f * PI_F * (float)p / 25.0f; t.dc[p] = cosf(a); t.ds[p] = sinf(a); }
+}
+
+struct HostTensor {
+    int dtype = 0;  // 0 f32, 1 f16
+    int n_dims = 0;
+    int64_t ne[3] = {1, 1, 1};
+    std::vector<uint8_t> data;
+    int64_t nel() const { return ne[0] * ne[1] * ne[2]; }
+    const float *f32() const { return (const float *)data.data(); }
+    const uint16_t *f16() const { return (const uint16_t *)data.data(); }
+};
+
+struct EncLayerDev {
+    float *ln1_w, *ln1_b;
+    uint16_t *wqkv; float *bqkv;
+    uint16_t *wo; float *bo;
+    float *ln2_w, *ln2_b;
+    uint16_t *w0; float *b0;
+    uint16_t *w1; float *b1;
+};
+
+struct DecLayerDev {
+    float *ln1_w, *ln1_b;
+    uint16_t *wqkv; float *bqkv;
+    uint16_t *wo; float *bo;
+    float *lnc_w, *lnc_b;
+    uint16_t *wcq; float *bcq;
+    uint16_t *wco; float *bco;
+    float *ln2_w, *ln2_b;
+    uint16_t *w0; float *b0;
+    uint16_t *w1; float *b1;
+};
+
+int64_t up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct wmi_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    wmi_hparams hp{};
+    wmi_special_tokens sp{};
+    std::vector<std::string> vocab;
+    std::string last_error;
+    int Cp1 = 0, n_exp = 0;
+    // device model arena
+    void *d_model = nullptr;
+    size_t model_bytes = 0;
+    MelTables *meltabs = nullptr;
+    float *filt_t = nullptr;
+    uint16_t *gelu_tab = nullptr, *exp_tab = nullptr;
+    uint16_t *conv1_w = nullptr, *conv2_w = nullptr;
+    float *conv1_b = nullptr, *conv2_b = nullptr, *e_pe = nullptr, *lnp_w = nullptr, *lnp_b = nullptr;
+    std::vector<EncLayerDev> enc;
+    uint16_t *wckv = nullptr;
+    float *bckv = nullptr;
+    uint16_t *te = nullptr;
+    float *d_pe = nullptr, *dln_w = nullptr, *dln_b = nullptr;
+    std::vector<DecLayerDev> dec;
+    // workspace
+    int max_clips = 1;
+    void *d_ws = nullptr;
+    size_t ws_bytes = 0;
+    uint16_t *xconv = nullptr, *g1 = nullptr, *xln = nullptr, *q = nullptr, *k = nullptr, *vt = nullptr;
+    uint16_t *att = nullptr, *hid = nullptr, *enc16 = nullptr, *ck = nullptr, *cv = nullptr;
+    uint16_t *kcache = nullptr, *vcache = nullptr;
+    float *h = nullptr, *enc32 = nullptr;
+    // decoder small state
+    float *dx = nullptr, *dlogits = nullptr;
+    uint16_t *dq16 = nullptr, *datt16 = nullptr, *dhid16 = nullptr;
+    unsigned long long *damax = nullptr;
+    DecState *dstate = nullptr;
+    int32_t *dfeed = nullptr;
+    int feed_cap = 0;
+    int32_t *dtokens = nullptr;
+    size_t tokens_cap = 0;
+    // mel / pcm
+    std::vector<float *> pcm_dev;
+    std::vector<size_t> pcm_cap;
+    float **d_pcm_ptrs = nullptr;
+    int64_t *d_nsamp = nullptr, *d_nlen = nullptr;
+    uint32_t *d_melmax = nullptr;
+    float *d_mel = nullptr;
+    size_t mel_cap = 0;
+    int64_t mel_stride = 0, max_len = 0;
+    std::vector<int64_t> n_len_host, n_samp_host;
+    int n_clips = 0;   // clips loaded by the last pcm_to_mel / stage
+    int enc_T = 0;     // n_ctx of the last encode (0 = none)
+    int enc_clips = 0;
+    int layout_T = -1; // T the q/k/vt padded layout was last zeroed for
+    int cur_ctx = 0;   // exp_n_audio_ctx
+    // staged decode results
+    int staged_n_decode = 0;
+    // timings
+    hipEvent_t ev[8] = {};
+    wmi_timings timings{};
+    // decode graph cache
+    hipGraphExec_t g_exec = nullptr;
+    hipGraph_t g_graph = nullptr;
+    std::string g_key;
+    bool use_graph = true;
+    // dist
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1;
+    int32_t *d_gather = nullptr;
+    size_t gather_cap = 0;
+};
+
+namespace {
+
+int set_err(wmi_context *ctx, int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->last_error = buf;
+    g_last_error = buf;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                        \
+    do {                                                                                         \
+        hipError_t _e = (expr);                                                                  \
+        if (_e != hipSuccess)                                                                    \
+            return set_err((ctx), WMI_E_HIP, "HIP error %s at %s:%d: %s", hipGetErrorName(_e),    \
+                           __FILE__, __LINE__, #expr);                                           \
+    } while (0)
+
+#define RCCLCHK(ctx, expr)                                                                       \
+    do {                                                                                         \
+        ncclResult_t _r = (expr);                                                                \
+        if (_r != ncclSuccess)                                                                   \
+            return set_err((ctx), WMI_E_RCCL, "RCCL error %s at %s:%d", ncclGetErrorString(_r),    \
+                           __FILE__, __LINE__);                                                  \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// ggml-v1 file parser: WhisperContext::new + WhisperModel::load
+// ---------------------------------------------------------------------------
+struct Expected {
+    int dtype;
+    int n_dims;
+    int64_t ne[3];
+};
+
+struct ParsedModel {
+    wmi_hparams hp{};
+    int32_t n_filt_mel = 0, n_filt_ff = 0;
+    std::vector<float> filters;
+    std::vector<std::string> vocab;
+    std::map<std::string, HostTensor> tensors;
+};
+
+int parse_file(const char *path, ParsedModel &pm, std::string &err) {
+    FILE *f = fopen(path, "rb");
+    if (!f) { err = std::string("Unexpected IO: cannot open '") + path + "'"; return WMI_E_IO; }
+    std::unique_ptr<FILE, int (*)(FILE *)> guard(f, fclose);
+    fseek(f, 0, SEEK_END);
+    const long fsize = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    auto rd = [&](void *p, size_t n) { return fread(p, 1, n, f) == n; };
+    uint32_t magic = 0;
+    if (!rd(&magic, 4)) { err = "Unexpected IO: short read (magic)"; return WMI_E_IO; }
+    if (magic != 0x67676d6cu) { err = std::string("invalid model file '") + path + "' (bad magic)"; return WMI_E_BAD_MAGIC; }
+    int32_t hpv[11];
+    if (!rd(hpv, 44)) { err = "Unexpected IO: short read (hparams)"; return WMI_E_IO; }
+    memcpy(&pm.hp, hpv, 44);
+    const wmi_hparams &hp = pm.hp;
+    for (int i = 0; i < 10; ++i)
+        if (hpv[i] <= 0) { err = "Unexpected: non-positive hparam"; return WMI_E_UNEXPECTED; }
+    if (hp.n_audio_state % hp.n_audio_head || hp.n_text_state % hp.n_text_head) {
+        err = "Unexpected: state not divisible by heads";
+        return WMI_E_UNEXPECTED;
+    }
+    // filters (main.rs:513-535)
+    if (!rd(&pm.n_filt_mel, 4) || !rd(&pm.n_filt_ff, 4)) { err = "Unexpected IO: short read (filters)"; return WMI_E_IO; }
+    if (pm.n_filt_mel <= 0 || pm.n_filt_ff <= 0 || (int64_t)pm.n_filt_mel * pm.n_filt_ff > (1 << 24)) {
+        err = "Unexpected: bad filter dims";
+        return WMI_E_UNEXPECTED;
+    }
+    pm.filters.resize((size_t)pm.n_filt_mel * pm.n_filt_ff);
+    if (!rd(pm.filters.data(), pm.filters.size() * 4)) { err = "Unexpected IO: short read (filters)"; return WMI_E_IO; }
+    // vocab (main.rs:430, 578-592)
+    int32_t nv = 0;
+    if (!rd(&nv, 4) || nv < 0) { err = "Unexpected IO: vocab"; return WMI_E_IO; }
+    pm.vocab.resize(nv);
+    for (int32_t i = 0; i < nv; ++i) {
+        uint32_t len = 0;
+        if (!rd(&len, 4) || len > (1u << 20)) { err = "Unexpected IO: vocab"; return WMI_E_IO; }
+        pm.vocab[i].resize(len);
+        if (len && !rd(&pm.vocab[i][0], len)) { err = "Unexpected IO: vocab"; return WMI_E_IO; }
+    }
+    // expected tensors (main.rs:947-1334)
+    std::map<std::string, Expected> exp;
+    const int64_t n = hp.n_audio_state, nt = hp.n_text_state;
+    const int W = hp.f16 == 1 ? 1 : 0;
+    exp["encoder.positional_embedding"] = {0, 2, {n, hp.n_audio_ctx, 1}};
+    exp["encoder.conv1.weight"] = {W, 3, {3, hp.n_mels, n}};
+    exp["encoder.conv1.bias"] = {0, 2, {1, n, 1}};
+    exp["encoder.conv2.weight"] = {W, 3, {3, n, n}};
+    exp["encoder.conv2.bias"] = {0, 2, {1, n, 1}};
+    exp["encoder.ln_post.weight"] = {0, 1, {n, 1, 1}};
+    exp["encoder.ln_post.bias"] = {0, 1, {n, 1, 1}};
+    char nm[128];
+    for (int i = 0; i < hp.n_audio_layer; ++i) {
+        auto E = [&](const char *s, int dt, int nd, int64_t a, int64_t b) {
+            snprintf(nm, sizeof nm, "encoder.blocks.%d.%s", i, s);
+            exp[nm] = {dt, nd, {a, b, 1}};
+        };
+        E("mlp_ln.weight", 0, 1, n, 1); E("mlp_ln.bias", 0, 1, n, 1);
+        E("mlp.0.weight", W, 2, n, 4 * n); E("mlp.0.bias", 0, 1, 4 * n, 1);
+        E("mlp.2.weight", W, 2, 4 * n, n); E("mlp.2.bias", 0, 1, n, 1);
+        E("attn_ln.weight", 0, 1, n, 1); E("attn_ln.bias", 0, 1, n, 1);
+        E("attn.query.weight", W, 2, n, n); E("attn.query.bias", 0, 1, n, 1);
+        E("attn.key.weight", W, 2, n, n);
+        E("attn.value.weight", W, 2, n, n); E("attn.value.bias", 0, 1, n, 1);
+        E("attn.out.weight", W, 2, n, n); E("attn.out.bias", 0, 1, n, 1);
+    }
+    exp["decoder.positional_embedding"] = {0, 2, {nt, hp.n_text_ctx, 1}};
+    exp["decoder.token_embedding.weight"] = {W, 2, {nt, hp.n_vocab, 1}};
+    exp["decoder.ln.weight"] = {0, 1, {nt, 1, 1}};
+    exp["decoder.ln.bias"] = {0, 1, {nt, 1, 1}};
+    for (int i = 0; i < hp.n_text_layer; ++i) {
+        auto E = [&](const char *s, int dt, int nd, int64_t a, int64_t b) {
+            snprintf(nm, sizeof nm, "decoder.blocks.%d.%s", i, s);
+            exp[nm] = {dt, nd, {a, b, 1}};
+        };
+        E("mlp_ln.weight", 0, 1, nt, 1); E("mlp_ln.bias", 0, 1, nt, 1);
+        E("mlp.0.weight", W, 2, nt, 4 * nt); E("mlp.0.bias", 0, 1, 4 * nt, 1);
+        E("mlp.2.weight", W, 2, 4 * nt, nt); E("mlp.2.bias", 0, 1, nt, 1);
+        for (const char *a : {"attn", "cross_attn"}) {
+            char s[64];
+            snprintf(s, sizeof s, "%s_ln.weight", a); E(s, 0, 1, nt, 1);
+            snprintf(s, sizeof s, "%s_ln.bias", a); E(s, 0, 1, nt, 1);
+            snprintf(s, sizeof s, "%s.query.weight", a); E(s, W, 2, nt, nt);
+            snprintf(s, sizeof s, "%s.query.bias", a); E(s, 0, 1, nt, 1);
+            snprintf(s, sizeof s, "%s.key.weight", a); E(s, W, 2, nt, nt);
+            snprintf(s, sizeof s, "%s.value.weight", a); E(s, W, 2, nt, nt);
+            snprintf(s, sizeof s, "%s.value.bias", a); E(s, 0, 1, nt, 1);
+            snprintf(s, sizeof s, "%s.out.weight", a); E(s, W, 2, nt, nt);
+            snprintf(s, sizeof s, "%s.out.bias", a); E(s, 0, 1, nt, 1);
+        }
+    }
+    // every expected tensor exists, zero-filled, like the reference arena
+    for (auto &kv : exp) {
+        HostTensor t;
+        t.dtype = kv.second.dtype;
+        t.n_dims = kv.second.n_dims;
+        for (int i = 0; i < 3; ++i) t.ne[i] = kv.second.ne[i];
+        t.data.assign((size_t)t.nel() * (t.dtype ? 2 : 4), 0);
+        pm.tensors[kv.first] = std::move(t);
+    }
+    // record loop (main.rs:1384-1475): until fewer than 12 bytes remain
+    for (;;) {
+        const long pos = ftell(f);
+        if (fsize - pos < 12) break;
+        int32_t hdr[3];
+        if (!rd(hdr, 12)) { err = "Unexpected IO: short read (tensor header)"; return WMI_E_IO; }
+        const int32_t n_dims = hdr[0], len = hdr[1], ftype = hdr[2];
+        if (n_dims < 1 || n_dims > 3 || len <= 0 || len > 255) {
+            char b[128];
+            snprintf(b, sizeof b, "Unexpected: bad tensor header (n_dims %d, name_len %d)", n_dims, len);
+            err = b;
+            return WMI_E_UNEXPECTED;
+        }
+        int64_t ne[3] = {1, 1, 1}, nel = 1;
+        for (int i = 0; i < n_dims; ++i) {
+            int32_t v;
+            if (!rd(&v, 4)) { err = "Unexpected IO: short read (dims)"; return WMI_E_IO; }
+            ne[i] = v;
+            nel *= v;
+        }
+        std::string name(len, '\0');
+        if (!rd(&name[0], len)) { err = "Unexpected IO: short read (name)"; return WMI_E_IO; }
+        auto it = pm.tensors.find(name);
+        char b[512];
+        if (it == pm.tensors.end()) {
+            snprintf(b, sizeof b, "unknown tensor '%s' in model file", name.c_str());
+            err = b;
+            return WMI_E_UNKNOWN_TENSOR;
+        }
+        HostTensor &t = it->second;
+        if (t.nel() != nel) {
+            snprintf(b, sizeof b, "tensor %s has wrong size in model file, got:%lld, expected:%lld", name.c_str(),
+                     (long long)t.nel(), (long long)nel);
+            err = b;
+            return WMI_E_WRONG_SIZE;
+        }
+        for (int i = 0; i < t.n_dims; ++i)
+            if (t.ne[i] != ne[i]) {
+                snprintf(b, sizeof b, "tensor %s has wrong shape in model file, got:[%lld, %lld, %lld], expected:[%lld, %lld, %lld]",
+                         name.c_str(), (long long)t.ne[0], (long long)t.ne[1], (long long)t.ne[2], (long long)ne[0],
+                         (long long)ne[1], (long long)ne[2]);
+                err = b;
+                return WMI_E_WRONG_SHAPE;
+            }
+        const int64_t bpe = ftype == 0 ? 4 : 2;
+        if (nel * bpe != (int64_t)t.data.size()) {
+            snprintf(b, sizeof b, "tensor %s has wrong bytes in model file, got:%lld, expected:%lld", name.c_str(),
+                     (long long)t.data.size(), (long long)(nel * bpe));
+            err = b;
+            return WMI_E_WRONG_BYTES;
+        }
+        if (!rd(t.data.data(), t.data.size())) { err = "Unexpected IO: short read (tensor data)"; return WMI_E_IO; }
+    }
+    if (hp.f16 != 1) {
+        err = "f32 matrices (hparams.f16 != 1) are not supported by this build";
+        return WMI_E_UNSUPPORTED;
+    }
+    return WMI_OK;
+}
+
+// special ids: main.rs:557-575 + multilingual shift main.rs:433-440 (large-v3:
+// later whisper.cpp's variable-language shift)
+void init_specials(int32_t n_vocab, wmi_special_tokens &sp) {
+    int32_t eot = 50256, sot = 50257, prev = 50360, solm = 50361, not_ = 50362, beg = 50363;
+    int32_t translate = 50358, transcribe = 50359;
+    const int multilingual = n_vocab >= 51865;
+    if (multilingual) {
+        const int dt = (n_vocab - 51765 - 1) - 98;
+        const int extra = dt > 1 ? dt - 1 : 0;
+        eot += 1; sot += 1;
+        prev += 1 + extra; solm += 1 + extra; not_ += 1 + extra; beg += 1 + extra;
+        translate += extra; transcribe += extra;
+    }
+    sp = {eot, sot, prev, solm, not_, beg, translate, transcribe, multilingual};
+}
+
+int prompt_tokens(const wmi_context *ctx, int32_t *out) {
+    int n = 0;
+    out[n++] = ctx->sp.sot;
+    if (ctx->sp.is_multilingual) {
+        out[n++] = ctx->sp.sot + 1;  // <|en|>
+        out[n++] = ctx->sp.transcribe;
+    }
+    out[n++] = ctx->sp.not_;
+    return n;
+}
+
+// ---------------------------------------------------------------------------
+// device arena planning
+// ---------------------------------------------------------------------------
+struct Arena {
+    size_t off = 0;
+    std::vector<std::pair<size_t, size_t>> dummy;
+    size_t take(size_t bytes) {
+        const size_t o = off;
+        off = up(off + bytes, 256);
+        return o;
+    }
+};
+
+int upload_model(wmi_context *ctx, ParsedModel &pm) {
+    const wmi_hparams &hp = ctx->hp;
+    const int64_t n = hp.n_audio_state, nt = hp.n_text_state;
+    const int La = hp.n_audio_layer, Lt = hp.n_text_layer;
+    const int C = hp.n_mels;
+    ctx->Cp1 = (int)up(C, 32);
+    const int Cp1 = ctx->Cp1;
+    std::vector<uint16_t> gelu, expt;
+    build_tables(gelu, expt);
+    // negative-half exp table: entries beyond the last non-zero (up to -inf) are 0
+    int n_exp = 0;
+    for (int j = 0; j <= 0x7c00; ++j)
+        if (expt[0x8000 | j] != 0) n_exp = j + 1;
+    ctx->n_exp = n_exp;
+    // plan
+    Arena A;
+    struct Piece { size_t off; std::vector<uint8_t> bytes; };
+    std::vector<Piece> pieces;
+    auto add = [&](const void *src, size_t bytes) -> size_t {
+        const size_t o = A.take(bytes);
+        Piece p{o, std::vector<uint8_t>((const uint8_t *)src, (const uint8_t *)src + bytes)};
+        pieces.push_back(std::move(p));
+        return o;
+    };
+    auto T = [&](const std::string &name) -> HostTensor & { return pm.tensors.at(name); };
+    MelTables mt;
+    build_mel_tables(mt);
+    const size_t o_mt = add(&mt, sizeof(mt));
+    std::vector<float> filt_t((size_t)201 * C, 0.0f);
+    if ((int64_t)pm.n_filt_mel * pm.n_filt_ff < (int64_t)C * 201)
+        return set_err(ctx, WMI_E_UNEXPECTED, "filterbank too small: %d x %d for %d mels", pm.n_filt_mel, pm.n_filt_ff, C);
+    for (int m = 0; m < C; ++m)
+        for (int k = 0; k < 201; ++k) filt_t[(size_t)k * C + m] = pm.filters[(size_t)m * 201 + k];  // main.rs:1624
+    const size_t o_filt = add(filt_t.data(), filt_t.size() * 4);
+    const size_t o_gelu = add(gelu.data(), gelu.size() * 2);
+    std::vector<uint16_t> expneg(expt.begin() + 0x8000, expt.begin() + 0x8000 + n_exp);
+    const size_t o_exp = add(expneg.data(), expneg.size() * 2);
+    // conv weights -> [o][tap][Cp] (implicit-GEMM B operand)
+    auto pack_conv = [&](const HostTensor &w, int Cin, int Cp) {
+        std::vector<uint16_t> p((size_t)n * 3 * Cp, 0);
+        const uint16_t *s = w.f16();
+        for (int64_t o = 0; o < n; ++o)
+            for (int c = 0; c < Cin; ++c)
+                for (int k = 0; k < 3; ++k) p[((size_t)o * 3 + k) * Cp + c] = s[((size_t)o * Cin + c) * 3 + k];
+        return add(p.data(), p.size() * 2);
+    };
+    const size_t o_c1w = pack_conv(T("encoder.conv1.weight"), C, Cp1);
+    const size_t o_c1b = add(T("encoder.conv1.bias").f32(), n * 4);
+    const size_t o_c2w = pack_conv(T("encoder.conv2.weight"), (int)n, (int)n);
+    const size_t o_c2b = add(T("encoder.conv2.bias").f32(), n * 4);
+    const size_t o_epe = add(T("encoder.positional_embedding").f32(), (size_t)hp.n_audio_ctx * n * 4);
+    const size_t o_lnpw = add(T("encoder.ln_post.weight").f32(), n * 4);
+    const size_t o_lnpb = add(T("encoder.ln_post.bias").f32(), n * 4);
+    auto cat3 = [&](const std::string &p, int64_t dim) {
+        std::vector<uint16_t> w((size_t)3 * dim * dim);
+        memcpy(&w[0], T(p + "query.weight").f16(), dim * dim * 2);
+        memcpy(&w[dim * dim], T(p + "key.weight").f16(), dim * dim * 2);
+        memcpy(&w[2 * dim * dim], T(p + "value.weight").f16(), dim * dim * 2);
+        std::vector<float> b((size_t)3 * dim, 0.0f);
+        memcpy(&b[0], T(p + "query.bias").f32(), dim * 4);
+        memcpy(&b[2 * dim], T(p + "value.bias").f32(), dim * 4);
+        return std::make_pair(add(w.data(), w.size() * 2), add(b.data(), b.size() * 4));
+    };
+    struct EncOff { size_t l1w, l1b, wqkv, bqkv, wo, bo, l2w, l2b, w0, b0, w1, b1; };
+    std::vector<EncOff> eo(La);
+    char nm[128];
+    for (int i = 0; i < La; ++i) {
+        snprintf(nm, sizeof nm, "encoder.blocks.%d.", i);
+        const std::string p(nm);
+        EncOff &e = eo[i];
+        e.l1w = add(T(p + "attn_ln.weight").f32(), n * 4);
+        e.l1b = add(T(p + "attn_ln.bias").f32(), n * 4);
+        auto qkv = cat3(p + "attn.", n);
+        e.wqkv = qkv.first; e.bqkv = qkv.second;
+        e.wo = add(T(p + "attn.out.weight").f16(), n * n * 2);
+        e.bo = add(T(p + "attn.out.bias").f32(), n * 4);
+        e.l2w = add(T(p + "mlp_ln.weight").f32(), n * 4);
+        e.l2b = add(T(p + "mlp_ln.bias").f32(), n * 4);
+        e.w0 = add(T(p + "mlp.0.weight").f16(), 4 * n * n * 2);
+        e.b0 = add(T(p + "mlp.0.bias").f32(), 4 * n * 4);
+        e.w1 = add(T(p + "mlp.2.weight").f16(), 4 * n * n * 2);
+        e.b1 = add(T(p + "mlp.2.bias").f32(), n * 4);
+    }
+    // cross-attention K/V of every decoder layer as ONE [Lt*2*nt][n] matrix
+    size_t o_wckv, o_bckv;
+    {
+        std::vector<uint16_t> w((size_t)Lt * 2 * nt * n);
+        std::vector<float> b((size_t)Lt * 2 * nt, 0.0f);
+        for (int l = 0; l < Lt; ++l) {
+            snprintf(nm, sizeof nm, "decoder.blocks.%d.cross_attn.", l);
+            const std::string p(nm);
+            memcpy(&w[(size_t)(2 * l) * nt * n], T(p + "key.weight").f16(), nt * n * 2);
+            memcpy(&w[(size_t)(2 * l + 1) * nt * n], T(p + "value.weight").f16(), nt * n * 2);
+            memcpy(&b[(size_t)(2 * l + 1) * nt], T(p + "value.bias").f32(), nt * 4);
+        }
+        o_wckv = add(w.data(), w.size() * 2);
+        o_bckv = add(b.data(), b.size() * 4);
+    }
+    const size_t o_te = add(T("decoder.token_embedding.weight").f16(), (size_t)hp.n_vocab * nt * 2);
+    const size_t o_dpe = add(T("decoder.positional_embedding").f32(), (size_t)hp.n_text_ctx * nt * 4);
+    const size_t o_dlnw = add(T("decoder.ln.weight").f32(), nt * 4);
+    const size_t o_dlnb = add(T("decoder.ln.bias").f32(), nt * 4);
+    struct DecOff { size_t l1w, l1b, wqkv, bqkv, wo, bo, lcw, lcb, wcq, bcq, wco, bco, l2w, l2b, w0, b0, w1, b1; };
+    std::vector<DecOff> dof(Lt);
+    for (int i = 0; i < Lt; ++i) {
+        snprintf(nm, sizeof nm, "decoder.blocks.%d.", i);
+        const std::string p(nm);
+        DecOff &d = dof[i];
+        d.l1w = add(T(p + "attn_ln.weight").f32(), nt * 4);
+        d.l1b = add(T(p + "attn_ln.bias").f32(), nt * 4);
+        auto qkv = cat3(p + "attn.", nt);
+        d.wqkv = qkv.first; d.bqkv = qkv.second;
+        d.wo = add(T(p + "attn.out.weight").f16(), nt * nt * 2);
+        d.bo = add(T(p + "attn.out.bias").f32(), nt * 4);
+        d.lcw = add(T(p + "cross_attn_ln.weight").f32(), nt * 4);
+        d.lcb = add(T(p + "cross_attn_ln.bias").f32(), nt * 4);
+        d.wcq = add(T(p + "cross_attn.query.weight").f16(), nt * nt * 2);
+        d.bcq = add(T(p + "cross_attn.query.bias").f32(), nt * 4);
+        d.wco = add(T(p + "cross_attn.out.weight").f16(), nt * nt * 2);
+        d.bco = add(T(p + "cross_attn.out.bias").f32(), nt * 4);
+        d.l2w = add(T(p + "mlp_ln.weight").f32(), nt * 4);
+        d.l2b = add(T(p + "mlp_ln.bias").f32(), nt * 4);
+        d.w0 = add(T(p + "mlp.0.weight").f16(), 4 * nt * nt * 2);
+        d.b0 = add(T(p + "mlp.0.bias").f32(), 4 * nt * 4);
+        d.w1 = add(T(p + "mlp.2.weight").f16(), 4 * nt * nt * 2);
+        d.b1 = add(T(p + "mlp.2.bias").f32(), nt * 4);
+    }
+    // upload everything in one copy
+    ctx->model_bytes = A.off;
+    HIPCHK(ctx, hipMalloc(&ctx->d_model, ctx->model_bytes));
+    {
+        std::vector<uint8_t> stage(ctx->model_bytes, 0);
+        for (auto &p : pieces) memcpy(&stage[p.off], p.bytes.data(), p.bytes.size());
+        pieces.clear();
+        HIPCHK(ctx, hipMemcpy(ctx->d_model, stage.data(), stage.size(), hipMemcpyHostToDevice));
+    }
+    uint8_t *base = (uint8_t *)ctx->d_model;
+    auto F = [&](size_t o) { return (float *)(base + o); };
+    auto H = [&](size_t o) { return (uint16_t *)(base + o); };
+    ctx->meltabs = (MelTables *)(base + o_mt);
+    ctx->filt_t = F(o_filt);
+    ctx->gelu_tab = H(o_gelu);
+    ctx->exp_tab = H(o_exp);
+    ctx->conv1_w = H(o_c1w); ctx->conv1_b = F(o_c1b);
+    ctx->conv2_w = H(o_c2w); ctx->conv2_b = F(o_c2b);
+    ctx->e_pe = F(o_epe); ctx->lnp_w = F(o_lnpw); ctx->lnp_b = F(o_lnpb);
+    ctx->enc.resize(La);
+    for (int i = 0; i < La; ++i) {
+        const EncOff &e = eo[i];
+        ctx->enc[i] = {F(e.l1w), F(e.l1b), H(e.wqkv), F(e.bqkv), H(e.wo), F(e.bo),
+                       F(e.l2w), F(e.l2b), H(e.w0), F(e.b0), H(e.w1), F(e.b1)};
+    }
+    ctx->wckv = H(o_wckv); ctx->bckv = F(o_bckv);
+    ctx->te = H(o_te); ctx->d_pe = F(o_dpe); ctx->dln_w = F(o_dlnw); ctx->dln_b = F(o_dlnb);
+    ctx->dec.resize(Lt);
+    for (int i = 0; i < Lt; ++i) {
+        const DecOff &d = dof[i];
+        ctx->dec[i] = {F(d.l1w), F(d.l1b), H(d.wqkv), F(d.bqkv), H(d.wo), F(d.bo), F(d.lcw), F(d.lcb),
+                       H(d.wcq), F(d.bcq), H(d.wco), F(d.bco), F(d.l2w), F(d.l2b), H(d.w0), F(d.b0), H(d.w1), F(d.b1)};
+    }
+    return WMI_OK;
+}
+
+// workspace for max_clips clips of up to n_audio_ctx frames
+int alloc_workspace(wmi_context *ctx) {
+    const wmi_hparams &hp = ctx->hp;
+    const int64_t B = ctx->max_clips, T = hp.n_audio_ctx, T2 = 2 * T, Tp = up(T, 64);
+    const int64_t n = hp.n_audio_state, nt = hp.n_text_state, H = hp.n_audio_head;
+    const int64_t Lt = hp.n_text_layer;
+    Arena A;
+    const size_t o_xconv = A.take(B * (T2 + 2) * ctx->Cp1 * 2);
+    const size_t o_g1 = A.take(B * (T2 + 2) * n * 2);
+    const size_t o_h = A.take(B * T * n * 4);
+    const size_t o_xln = A.take(B * T * n * 2);
+    const size_t o_q = A.take(B * H * Tp * 64 * 2);
+    const size_t o_k = A.take(B * H * Tp * 64 * 2);
+    const size_t o_vt = A.take(B * H * Tp * 64 * 2);
+    const size_t o_att = A.take(B * T * n * 2);
+    const size_t o_hid = A.take(B * T * 4 * n * 2);
+    const size_t o_enc32 = A.take(B * T * n * 4);
+    const size_t o_enc16 = A.take(B * T * n * 2);
+    const size_t o_ck = A.take(Lt * B * T * nt * 2);
+    const size_t o_cv = A.take(Lt * B * T * nt * 2);
+    const size_t o_kc = A.take(Lt * B * hp.n_text_ctx * nt * 2);
+    const size_t o_vc = A.take(Lt * B * hp.n_text_ctx * nt * 2);
+    const size_t o_dx = A.take(B * nt * 4);
+    const size_t o_dq = A.take(B * nt * 2);
+    const size_t o_datt = A.take(B * nt * 2);
+    const size_t o_dhid = A.take(B * 4 * nt * 2);
+    const size_t o_dlog = A.take(B * (int64_t)hp.n_vocab * 4);
+    const size_t o_amax = A.take(B * 8);
+    const size_t o_st = A.take(sizeof(DecState));
+    const size_t o_ptrs = A.take(B * sizeof(float *));
+    const size_t o_ns = A.take(B * 8);
+    const size_t o_nl = A.take(B * 8);
+    const size_t o_mm = A.take(B * 4);
+    ctx->ws_bytes = A.off;
+    HIPCHK(ctx, hipMalloc(&ctx->d_ws, ctx->ws_bytes));
+    HIPCHK(ctx, hipMemset(ctx->d_ws, 0, ctx->ws_bytes));
+    uint8_t *b = (uint8_t *)ctx->d_ws;
+    ctx->xconv = (uint16_t *)(b + o_xconv);
+    ctx->g1 = (uint16_t *)(b + o_g1);
+    ctx->h = (float *)(b + o_h);
+    ctx->xln = (uint16_t *)(b + o_xln);
+    ctx->q = (uint16_t *)(b + o_q);
+    ctx->k = (uint16_t *)(b + o_k);
+    ctx->vt = (uint16_t *)(b + o_vt);
+    ctx->att = (uint16_t *)(b + o_att);
+    ctx->hid = (uint16_t *)(b + o_hid);
+    ctx->enc32 = (float *)(b + o_enc32);
+    ctx->enc16 = (uint16_t *)(b + o_enc16);
+    ctx->ck = (uint16_t *)(b + o_ck);
+    ctx->cv = (uint16_t *)(b + o_cv);
+    ctx->kcache = (uint16_t *)(b + o_kc);
+    ctx->vcache = (uint16_t *)(b + o_vc);
+    ctx->dx = (float *)(b + o_dx);
+    ctx->dq16 = (uint16_t *)(b + o_dq);
+    ctx->datt16 = (uint16_t *)(b + o_datt);
+    ctx->dhid16 = (uint16_t *)(b + o_dhid);
+    ctx->dlogits = (float *)(b + o_dlog);
+    ctx->damax = (unsigned long long *)(b + o_amax);
+    ctx->dstate = (DecState *)(b + o_st);
+    ctx->d_pcm_ptrs = (float **)(b + o_ptrs);
+    ctx->d_nsamp = (int64_t *)(b + o_ns);
+    ctx->d_nlen = (int64_t *)(b + o_nl);
+    ctx->d_melmax = (uint32_t *)(b + o_mm);
+    for (int i = 0; i < 8; ++i) HIPCHK(ctx, hipEventCreate(&ctx->ev[i]));
+    return WMI_OK;
+}
+
+// ---------------------------------------------------------------------------
+// pipeline stages
+// ---------------------------------------------------------------------------
+int stage_pcm(wmi_context *ctx, int n_clips, const float *const *pcm, const size_t *n_samples) {
+    if (n_clips < 1 || n_clips > ctx->max_clips || !pcm || !n_samples)
+        return set_err(ctx, WMI_E_INVALID_ARG, "n_clips %d outside [1, max_clips=%d]", n_clips, ctx->max_clips);
+    ctx->pcm_dev.resize(ctx->max_clips, nullptr);
+    ctx->pcm_cap.resize(ctx->max_clips, 0);
+    std::vector<float *> ptrs(n_clips);
+    ctx->n_len_host.assign(n_clips, 0);
+    ctx->n_samp_host.assign(n_clips, 0);
+    int64_t max_len = 0;
+    for (int c = 0; c < n_clips; ++c) {
+        const size_t ns = n_samples[c];
+        if (ns > 0 && !pcm[c]) return set_err(ctx, WMI_E_INVALID_ARG, "null pcm for clip %d", c);
+        if (ns + 64 > ctx->pcm_cap[c]) {
+            if (ctx->pcm_dev[c]) HIPCHK(ctx, hipFree(ctx->pcm_dev[c]));
+            ctx->pcm_cap[c] = ns + 64;
+            HIPCHK(ctx, hipMalloc(&ctx->pcm_dev[c], ctx->pcm_cap[c] * 4));
+        }
+        if (ns) HIPCHK(ctx, hipMemcpyAsync(ctx->pcm_dev[c], pcm[c], ns * 4, hipMemcpyHostToDevice, ctx->stream));
+        ptrs[c] = ctx->pcm_dev[c];
+        ctx->n_samp_host[c] = (int64_t)ns;
+        ctx->n_len_host[c] = (int64_t)(ns / 160);  // main.rs:1575
+        if (ctx->n_len_host[c] > max_len) max_len = ctx->n_len_host[c];
+    }
+    const int64_t n_mel = ctx->hp.n_mels;
+    const size_t need = (size_t)n_clips * n_mel * (max_len > 0 ? max_len : 1);
+    if (need > ctx->mel_cap) {
+        if (ctx->d_mel) HIPCHK(ctx, hipFree(ctx->d_mel));
+        const size_t cap = (size_t)ctx->max_clips * n_mel * (max_len > 0 ? max_len : 1);
+        HIPCHK(ctx, hipMalloc(&ctx->d_mel, cap * 4));
+        ctx->mel_cap = cap;
+    }
+    ctx->mel_stride = n_mel * (max_len > 0 ? max_len : 1);
+    ctx->max_len = max_len;
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_pcm_ptrs, ptrs.data(), n_clips * sizeof(float *), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_nsamp, ctx->n_samp_host.data(), n_clips * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_nlen, ctx->n_len_host.data(), n_clips * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->n_clips = n_clips;
+    ctx->enc_T = 0;
+    return WMI_OK;
+}
+
+int run_mel(wmi_context *ctx) {
+    const int B = ctx->n_clips;
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_melmax, 0, B * 4, ctx->stream));
+    HIPCHK(ctx, launch_mel_frames(ctx->stream, ctx->meltabs, ctx->filt_t, ctx->hp.n_mels,
+                                  (const float *const *)ctx->d_pcm_ptrs, ctx->d_nsamp, ctx->d_mel, ctx->mel_stride,
+                                  ctx->d_nlen, ctx->max_len, ctx->d_melmax, B));
+    HIPCHK(ctx, launch_mel_norm(ctx->stream, ctx->d_mel, ctx->mel_stride, ctx->hp.n_mels, ctx->d_nlen, ctx->max_len,
+                                ctx->d_melmax, B));
+    return WMI_OK;
+}
+
+int run_encode(wmi_context *ctx, int mel_offset) {
+    const wmi_hparams &hp = ctx->hp;
+    const int B = ctx->n_clips;
+    const int T = ctx->cur_ctx > 0 ? ctx->cur_ctx : hp.n_audio_ctx, T2 = 2 * T;
+    const int Tp = (int)up(T, 64);
+    const int n = hp.n_audio_state, H = hp.n_audio_head, nt = hp.n_text_state;
+    if (B < 1) return set_err(ctx, WMI_E_INVALID_ARG, "encode before pcm_to_mel");
+    if (mel_offset < 0) return set_err(ctx, WMI_E_INVALID_ARG, "negative mel_offset");
+    if (nt != n) return set_err(ctx, WMI_E_UNSUPPORTED, "n_text_state != n_audio_state");
+    if (n / H != 64) return set_err(ctx, WMI_E_UNSUPPORTED, "head dim %d != 64", n / H);
+    hipStream_t s = ctx->stream;
+    if (ctx->layout_T != T) {
+        const size_t qkv_bytes = (size_t)ctx->max_clips * H * up(hp.n_audio_ctx, 64) * 64 * 2;
+        HIPCHK(ctx, hipMemsetAsync(ctx->q, 0, qkv_bytes, s));
+        HIPCHK(ctx, hipMemsetAsync(ctx->k, 0, qkv_bytes, s));
+        HIPCHK(ctx, hipMemsetAsync(ctx->vt, 0, qkv_bytes, s));
+        ctx->layout_T = T;
+    }
+    // mel window -> conv1 input (main.rs:1816-1833)
+    HIPCHK(ctx, launch_mel_window(s, ctx->d_mel, ctx->mel_stride, hp.n_mels, ctx->d_nlen, mel_offset, T2, ctx->Cp1,
+                                  ctx->xconv, B));
+    HIPCHK(ctx, hipMemsetAsync(ctx->g1, 0, (size_t)B * (T2 + 2) * n * 2, s));
+    GemmArgs g{};
+    // conv1 + bias + GELU (main.rs:1834-1855)
+    g.A = ctx->xconv; g.B = ctx->conv1_w; g.bias = ctx->conv1_b;
+    g.M = B * T2; g.N = n; g.K = 3 * ctx->Cp1;
+    g.conv = 1; g.conv_stride = 1; g.conv_tin = T2; g.conv_cp = ctx->Cp1; g.conv_tout = T2;
+    g.out16 = ctx->g1; g.ldo = n; g.gelu_tab = ctx->gelu_tab; g.T = T2;
+    HIPCHK(ctx, launch_gemm(s, EPI_CONV1, g));
+    // conv2 + bias + GELU + positional embedding (main.rs:1856-1875)
+    g = GemmArgs{};
+    g.A = ctx->g1; g.B = ctx->conv2_w; g.bias = ctx->conv2_b;
+    g.M = B * T; g.N = n; g.K = 3 * n;
+    g.conv = 1; g.conv_stride = 2; g.conv_tin = T2; g.conv_cp = n; g.conv_tout = T;
+    g.out32 = ctx->h; g.ldo = n; g.gelu_tab = ctx->gelu_tab; g.pe = ctx->e_pe; g.T = T;
+    HIPCHK(ctx, launch_gemm(s, EPI_CONV2PE, g));
+    const int M = B * T;
+    for (int l = 0; l < hp.n_audio_layer; ++l) {
+        const EncLayerDev &e = ctx->enc[l];
+        HIPCHK(ctx, launch_layernorm(s, ctx->h, M, n, e.ln1_w, e.ln1_b, ctx->xln, nullptr));
+        g = GemmArgs{};
+        g.A = ctx->xln; g.lda = n; g.B = e.wqkv; g.bias = e.bqkv; g.M = M; g.N = 3 * n; g.K = n;
+        g.q = ctx->q; g.k = ctx->k; g.vt = ctx->vt; g.T = T; g.Tp = Tp; g.n_state = n;
+        HIPCHK(ctx, launch_gemm(s, EPI_QKV, g));
+        AttnArgs at{};
+        at.q = ctx->q; at.k = ctx->k; at.vt = ctx->vt; at.out = ctx->att; at.exp_tab = ctx->exp_tab;
+        at.n_exp = ctx->n_exp; at.T = T; at.Tp = Tp; at.H = H; at.n_state = n; at.n_clips = B;
+        at.scale = (float)(1.0 / sqrt(64.0));
+        HIPCHK(ctx, launch_attn_enc(s, at));
+        g = GemmArgs{};
+        g.A = ctx->att; g.lda = n; g.B = e.wo; g.bias = e.bo; g.M = M; g.N = n; g.K = n;
+        g.out32 = ctx->h; g.ldo = n;
+        HIPCHK(ctx, launch_gemm(s, EPI_RESID, g));
+        HIPCHK(ctx, launch_layernorm(s, ctx->h, M, n, e.ln2_w, e.ln2_b, ctx->xln, nullptr));
+        g = GemmArgs{};
+        g.A = ctx->xln; g.lda = n; g.B = e.w0; g.bias = e.b0; g.M = M; g.N = 4 * n; g.K = n;
+        g.out16 = ctx->hid; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
+        HIPCHK(ctx, launch_gemm(s, EPI_GELU16, g));
+        g = GemmArgs{};
+        g.A = ctx->hid; g.lda = 4 * n; g.B = e.w1; g.bias = e.b1; g.M = M; g.N = n; g.K = 4 * n;
+        g.out32 = ctx->h; g.ldo = n;
+        HIPCHK(ctx, launch_gemm(s, EPI_RESID, g));
+    }
+    // ln_post (main.rs:1977-1986)
+    HIPCHK(ctx, launch_layernorm(s, ctx->h, M, n, ctx->lnp_w, ctx->lnp_b, ctx->enc16, ctx->enc32));
+    HIPCHK(ctx, hipEventRecord(ctx->ev[2], s));
+    // cross-attention K/V for every decoder layer in one GEMM (main.rs:1990-2060)
+    g = GemmArgs{};
+    g.A = ctx->enc16; g.lda = n; g.B = ctx->wckv; g.bias = ctx->bckv; g.M = M; g.N = hp.n_text_layer * 2 * nt; g.K = n;
+    g.ck = ctx->ck; g.cv = ctx->cv; g.T = T; g.n_state = nt; g.n_clips = B;
+    g.kscale = powf((float)n / (float)H, -0.25f);  // main.rs:1994
+    HIPCHK(ctx, launch_gemm(s, EPI_CROSSKV, g));
+    ctx->enc_T = T;
+    ctx->enc_clips = B;
+    return WMI_OK;
+}
+
+// one decoder step for clips [b0, b0 + B) of the encoded batch
+int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride, int suppress_eot, int out_stride) {
+    const wmi_hparams &hp = ctx->hp;
+    const int n = hp.n_text_state, H = hp.n_text_head, T = ctx->enc_T, Bt = ctx->enc_clips;
+    hipStream_t s = ctx->stream;
+    const float qs = powf((float)n / (float)H, -0.25f);
+    DecEmbedArgs em{};
+    em.te = ctx->te; em.pe = ctx->d_pe; em.x = ctx->dx; em.feed = ctx->dfeed; em.feed_len = feed_len;
+    em.feed_stride = feed_stride; em.amax = ctx->damax; em.tokens_out = ctx->dtokens + (size_t)b0 * out_stride;
+    em.out_stride = out_stride; em.st = ctx->dstate; em.n = n; em.B = B; em.record_only = 0;
+    HIPCHK(ctx, launch_dec_embed(s, em));
+    for (int l = 0; l < hp.n_text_layer; ++l) {
+        const DecLayerDev &d = ctx->dec[l];
+        uint16_t *kc = ctx->kcache + (size_t)l * ctx->max_clips * hp.n_text_ctx * n;
+        uint16_t *vc = ctx->vcache + (size_t)l * ctx->max_clips * hp.n_text_ctx * n;
+        DecGemvArgs g{};
+        g.x = ctx->dx; g.ln_w = d.ln1_w; g.ln_b = d.ln1_b; g.W = d.wqkv; g.bias = d.bqkv; g.N = 3 * n; g.K = n; g.B = B;
+        g.qscale = qs; g.out16 = ctx->dq16; g.ldo = n; g.kcache = kc; g.vcache = vc; g.n_text_ctx = hp.n_text_ctx;
+        g.st = ctx->dstate;
+        HIPCHK(ctx, launch_dec_gemv(s, DEC_QKV, g));
+        DecAttnArgs at{};
+        at.q = ctx->dq16; at.K = kc; at.V = vc; at.clip_stride = (int64_t)hp.n_text_ctx * n; at.M_fixed = 0;
+        at.st = ctx->dstate; at.out = ctx->datt16; at.exp_tab = ctx->exp_tab; at.n_exp = ctx->n_exp; at.H = H; at.n = n;
+        at.B = B;
+        HIPCHK(ctx, launch_dec_attn(s, at));
+        g = DecGemvArgs{};
+        g.xin16 = ctx->datt16; g.W = d.wo; g.bias = d.bo; g.N = n; g.K = n; g.B = B; g.out32 = ctx->dx;
+        HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
+        g = DecGemvArgs{};
+        g.x = ctx->dx; g.ln_w = d.lnc_w; g.ln_b = d.lnc_b; g.W = d.wcq; g.bias = d.bcq; g.N = n; g.K = n; g.B = B;
+        g.qscale = qs; g.out16 = ctx->dq16; g.ldo = n;
+        HIPCHK(ctx, launch_dec_gemv(s, DEC_Q, g));
+        at = DecAttnArgs{};
+        at.q = ctx->dq16;
+        at.K = ctx->ck + ((size_t)l * Bt + b0) * T * n;
+        at.V = ctx->cv + ((size_t)l * Bt + b0) * T * n;
+        at.clip_stride = (int64_t)T * n; at.M_fixed = T; at.st = ctx->dstate; at.out = ctx->datt16;
+        at.exp_tab = ctx->exp_tab; at.n_exp = ctx->n_exp; at.H = H; at.n = n; at.B = B;
+        HIPCHK(ctx, launch_dec_attn(s, at));
+        g = DecGemvArgs{};
+        g.xin16 = ctx->datt16; g.W = d.wco; g.bias = d.bco; g.N = n; g.K = n; g.B = B; g.out32 = ctx->dx;
+        HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
+        g = DecGemvArgs{};
+        g.x = ctx->dx; g.ln_w = d.ln2_w; g.ln_b = d.ln2_b; g.W = d.w0; g.bias = d.b0; g.N = 4 * n; g.K = n; g.B = B;
+        g.out16 = ctx->dhid16; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
+        HIPCHK(ctx, launch_dec_gemv(s, DEC_GELU, g));
+        g = DecGemvArgs{};
+        g.xin16 = ctx->dhid16; g.W = d.w1; g.bias = d.b1; g.N = n; g.K = 4 * n; g.B = B; g.out32 = ctx->dx;
+        HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
+    }
+    DecGemvArgs g{};
+    g.x = ctx->dx; g.ln_w = ctx->dln_w; g.ln_b = ctx->dln_b; g.W = ctx->te; g.N = hp.n_vocab; g.K = n; g.B = B;
+    g.out32 = ctx->dlogits; g.amax = ctx->damax; g.suppress_id = suppress_eot ? ctx->sp.eot : -1;
+    g.st_advance = ctx->dstate;
+    HIPCHK(ctx, launch_dec_gemv(s, DEC_LOGITS, g));
+    return WMI_OK;
+}
+
+int ensure_decode_buffers(wmi_context *ctx, int feed_elems, size_t token_elems) {
+    if (feed_elems > ctx->feed_cap) {
+        if (ctx->dfeed) HIPCHK(ctx, hipFree(ctx->dfeed));
+        HIPCHK(ctx, hipMalloc(&ctx->dfeed, (size_t)feed_elems * 4));
+        ctx->feed_cap = feed_elems;
+        ctx->g_key.clear();
+    }
+    if (token_elems > ctx->tokens_cap) {
+        if (ctx->dtokens) HIPCHK(ctx, hipFree(ctx->dtokens));
+        HIPCHK(ctx, hipMalloc(&ctx->dtokens, token_elems * 4));
+        HIPCHK(ctx, hipMemset(ctx->dtokens, 0, token_elems * 4));
+        ctx->tokens_cap = token_elems;
+        ctx->g_key.clear();
+    }
+    return WMI_OK;
+}
+
+// run `steps` decoder steps for clips [b0, b0+B), via a captured hipGraph
+int run_dec_steps(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride, int suppress_eot, int out_stride,
+                  int steps) {
+    if (!ctx->use_graph) {
+        for (int i = 0; i < steps; ++i) {
+            int rc = enqueue_dec_step(ctx, b0, B, feed_len, feed_stride, suppress_eot, out_stride);
+            if (rc) return rc;
+        }
+        return WMI_OK;
+    }
+    char key[160];
+    snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%p/%p", b0, B, feed_len, feed_stride, suppress_eot, out_stride,
+             ctx->enc_T, ctx->enc_clips, (void *)ctx->dfeed, (void *)ctx->dtokens);
+    if (ctx->g_key != key) {
+        if (ctx->g_exec) { (void)hipGraphExecDestroy(ctx->g_exec); ctx->g_exec = nullptr; }
+        if (ctx->g_graph) { (void)hipGraphDestroy(ctx->g_graph); ctx->g_graph = nullptr; }
+        HIPCHK(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+        int rc = enqueue_dec_step(ctx, b0, B, feed_len, feed_stride, suppress_eot, out_stride);
+        hipGraph_t graph = nullptr;
+        hipError_t ce = hipStreamEndCapture(ctx->stream, &graph);
+        if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
+        HIPCHK(ctx, ce);
+        ctx->g_graph = graph;
+        HIPCHK(ctx, hipGraphInstantiate(&ctx->g_exec, graph, nullptr, nullptr, 0));
+        ctx->g_key = key;
+    }
+    for (int i = 0; i < steps; ++i) HIPCHK(ctx, hipGraphLaunch(ctx->g_exec, ctx->stream));
+    return WMI_OK;
+}
+
+// greedy decode of every encoded clip; tokens stay in ctx->dtokens
+// ([enc_clips][n_gen]); returns after enqueueing (no sync) unless early stop.
+int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, std::vector<int32_t> *host_tokens,
+               std::vector<int32_t> *host_counts) {
+    const int Bt = ctx->enc_clips;
+    if (ctx->enc_T <= 0 || Bt < 1) return set_err(ctx, WMI_E_INVALID_ARG, "decode before encode");
+    int32_t prompt[8];
+    const int np = prompt_tokens(ctx, prompt);
+    if (n_gen < 1 || np + n_gen > ctx->hp.n_text_ctx)
+        return set_err(ctx, WMI_E_INVALID_ARG, "max_tokens %d: prompt %d + tokens must fit n_text_ctx %d", n_gen, np,
+                       ctx->hp.n_text_ctx);
+    int rc = ensure_decode_buffers(ctx, 8 * np, (size_t)Bt * n_gen);
+    if (rc) return rc;
+    std::vector<int32_t> feed(8 * np);
+    for (int b = 0; b < 8; ++b)
+        for (int i = 0; i < np; ++i) feed[b * np + i] = prompt[i];
+    HIPCHK(ctx, hipMemcpyAsync(ctx->dfeed, feed.data(), feed.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    if (host_tokens) host_tokens->assign((size_t)Bt * n_gen, 0);
+    if (host_counts) host_counts->assign(Bt, n_gen);
+    for (int b0 = 0; b0 < Bt; b0 += 8) {
+        const int B = Bt - b0 < 8 ? Bt - b0 : 8;
+        HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
+        HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * 8, ctx->stream));
+        const int total_steps = np + n_gen - 1;
+        int done_steps = 0;
+        while (done_steps < total_steps) {
+            int chunk = total_steps - done_steps;
+            if (early_stop && chunk > 32) chunk = 32;
+            rc = run_dec_steps(ctx, b0, B, np, np, suppress_eot, n_gen, chunk);
+            if (rc) return rc;
+            done_steps += chunk;
+            if (early_stop && done_steps < total_steps && done_steps >= np) {
+                // tokens generated so far: done_steps - np + 1 (last one still in amax)
+                const int have = done_steps - np;
+                std::vector<int32_t> tk((size_t)B * n_gen);
+                HIPCHK(ctx, hipMemcpyAsync(tk.data(), ctx->dtokens + (size_t)b0 * n_gen, tk.size() * 4,
+                                           hipMemcpyDeviceToHost, ctx->stream));
+                HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+                bool all = true;
+                for (int b = 0; b < B && all; ++b) {
+                    bool found = false;
+                    for (int i = 0; i < have; ++i)
+                        if (tk[(size_t)b * n_gen + i] == ctx->sp.eot) { found = true; break; }
+                    all = found;
+                }
+                if (all) break;
+            }
+        }
+        // record the last argmax (embed kernel in record-only mode)
+        DecEmbedArgs em{};
+        em.te = ctx->te; em.pe = ctx->d_pe; em.x = ctx->dx; em.feed = ctx->dfeed; em.feed_len = np; em.feed_stride = np;
+        em.amax = ctx->damax; em.tokens_out = ctx->dtokens + (size_t)b0 * n_gen; em.out_stride = n_gen;
+        em.st = ctx->dstate; em.n = ctx->hp.n_text_state; em.B = B; em.record_only = 1;
+        HIPCHK(ctx, launch_dec_embed(ctx->stream, em));
+    }
+    if (host_tokens) {
+        HIPCHK(ctx, hipMemcpyAsync(host_tokens->data(), ctx->dtokens, host_tokens->size() * 4, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        for (int b = 0; b < Bt; ++b) {
+            int cnt = n_gen;
+            if (!suppress_eot)
+                for (int i = 0; i < n_gen; ++i)
+                    if ((*host_tokens)[(size_t)b * n_gen + i] == ctx->sp.eot) { cnt = i + 1; break; }
+            (*host_counts)[b] = cnt;
+        }
+    }
+    return WMI_OK;
+}
+
+bool valid(const wmi_context *ctx) { return ctx != nullptr && ctx->d_model != nullptr; }
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+const char *wmi_strerror(int status) {
+    switch (status) {
+        case WMI_OK: return "ok";
+        case WMI_E_IO: return "Unexpected IO";
+        case WMI_E_BAD_MAGIC: return "invalid model file (bad magic)";
+        case WMI_E_NO_SPACE: return "not enough space";
+        case WMI_E_UNKNOWN_TENSOR: return "unknown tensor in model file";
+        case WMI_E_BAD_REF_TENSOR: return "invalid ref tensor";
+        case WMI_E_WRONG_SIZE: return "tensor has wrong size in model file";
+        case WMI_E_WRONG_SHAPE: return "tensor has wrong shape in model file";
+        case WMI_E_WRONG_BYTES: return "tensor has wrong bytes in model file";
+        case WMI_E_OP: return "tensor op error";
+        case WMI_E_UNEXPECTED: return "Unexpected";
+        case WMI_E_HIP: return "HIP error";
+        case WMI_E_RCCL: return "RCCL error";
+        case WMI_E_UNSUPPORTED: return "unsupported";
+        case WMI_E_INVALID_ARG: return "invalid argument";
+        default: return "unknown status";
+    }
+}
+
+const char *wmi_last_error(const wmi_context *ctx) { return ctx ? ctx->last_error.c_str() : g_last_error.c_str(); }
+const char *wmi_last_error_global(void) { return g_last_error.c_str(); }
+
+int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context **out) {
+    if (!out || !path) return set_err(nullptr, WMI_E_INVALID_ARG, "null argument");
+    *out = nullptr;
+    if (max_clips < 1) return set_err(nullptr, WMI_E_INVALID_ARG, "max_clips must be >= 1");
+    ParsedModel pm;
+    std::string err;
+    int rc = parse_file(path, pm, err);
+    if (rc) return set_err(nullptr, rc, "%s", err.c_str());
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return set_err(nullptr, WMI_E_HIP, "no HIP device available (the MI355X path has no CPU fallback)");
+    if (device < 0 || device >= ndev) return set_err(nullptr, WMI_E_INVALID_ARG, "device %d of %d", device, ndev);
+    std::unique_ptr<wmi_context> ctx(new wmi_context());
+    ctx->device = device;
+    ctx->max_clips = max_clips;
+    ctx->hp = pm.hp;
+    init_specials(pm.hp.n_vocab, ctx->sp);
+    // id_to_token incl. extra-token names (main.rs:442-467)
+    ctx->vocab = std::move(pm.vocab);
+    for (int32_t i = (int32_t)ctx->vocab.size(); i < pm.hp.n_vocab; ++i) {
+        char b[64];
+        if (i > ctx->sp.beg) snprintf(b, sizeof b, "[_TT_%d]", i - ctx->sp.beg);
+        else if (i == ctx->sp.eot) snprintf(b, sizeof b, "[_EOT_]");
+        else if (i == ctx->sp.sot) snprintf(b, sizeof b, "[_SOT_]");
+        else if (i == ctx->sp.prev) snprintf(b, sizeof b, "[_PREV_]");
+        else if (i == ctx->sp.not_) snprintf(b, sizeof b, "[_NOT_]");
+        else if (i == ctx->sp.beg) snprintf(b, sizeof b, "[_BEG_]");
+        else snprintf(b, sizeof b, "[_extra_token_%d]", i);
+        ctx->vocab.push_back(b);
+    }
+    HIPCHK(ctx.get(), hipSetDevice(device));
+    HIPCHK(ctx.get(), hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    rc = upload_model(ctx.get(), pm);
+    if (rc) { g_last_error = ctx->last_error; wmi_free(ctx.release()); return rc; }
+    pm.tensors.clear();
+    rc = alloc_workspace(ctx.get());
+    if (rc) { g_last_error = ctx->last_error; wmi_free(ctx.release()); return rc; }
+    if (getenv("WMI_NO_GRAPH")) ctx->use_graph = false;
+    *out = ctx.release();
+    return WMI_OK;
+}
+
+void wmi_free(wmi_context *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    if (ctx->g_exec) (void)hipGraphExecDestroy(ctx->g_exec);
+    if (ctx->g_graph) (void)hipGraphDestroy(ctx->g_graph);
+    for (float *p : ctx->pcm_dev) if (p) (void)hipFree(p);
+    if (ctx->d_mel) (void)hipFree(ctx->d_mel);
+    if (ctx->dfeed) (void)hipFree(ctx->dfeed);
+    if (ctx->dtokens) (void)hipFree(ctx->dtokens);
+    if (ctx->d_gather) (void)hipFree(ctx->d_gather);
+    if (ctx->d_ws) (void)hipFree(ctx->d_ws);
+    if (ctx->d_model) (void)hipFree(ctx->d_model);
+    for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int wmi_get_hparams(const wmi_context *ctx, wmi_hparams *out) {
+    if (!ctx || !out) return WMI_E_INVALID_ARG;
+    *out = ctx->hp;
+    return WMI_OK;
+}
+
+int wmi_get_special_tokens(const wmi_context *ctx, wmi_special_tokens *out) {
+    if (!ctx || !out) return WMI_E_INVALID_ARG;
+    *out = ctx->sp;
+    return WMI_OK;
+}
+
+int wmi_set_audio_ctx(wmi_context *ctx, int n_audio_ctx) {
+    if (!ctx) return WMI_E_INVALID_ARG;
+    if (n_audio_ctx < 0 || n_audio_ctx > ctx->hp.n_audio_ctx)
+        return set_err(ctx, WMI_E_INVALID_ARG, "audio ctx %d outside [0, %d]", n_audio_ctx, ctx->hp.n_audio_ctx);
+    ctx->cur_ctx = n_audio_ctx;
+    return WMI_OK;
+}
+
+int wmi_token_to_bytes(const wmi_context *ctx, int32_t id, char *buf, size_t cap, size_t *len) {
+    if (!ctx || !len) return WMI_E_INVALID_ARG;
+    if (id < 0 || id >= (int32_t)ctx->vocab.size()) return WMI_E_INVALID_ARG;
+    const std::string &s = ctx->vocab[id];
+    *len = s.size();
+    if (!buf || cap < s.size()) return WMI_E_NO_SPACE;
+    memcpy(buf, s.data(), s.size());
+    return WMI_OK;
+}
+
+int wmi_pcm_to_mel_batch(wmi_context *ctx, int n_clips, const float *const *pcm, const size_t *n_samples) {
+    if (!valid(ctx)) return WMI_E_INVALID_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc = stage_pcm(ctx, n_clips, pcm, n_samples);
+    if (rc) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+    rc = run_mel(ctx);
+    if (rc) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
+    ctx->timings.mel_ms = ms;
+    return WMI_OK;
+}
+
+int wmi_pcm_to_mel(wmi_context *ctx, const float *pcm, size_t n_samples) {
+    return wmi_pcm_to_mel_batch(ctx, 1, &pcm, &n_samples);
+}
+
+int wmi_encode(wmi_context *ctx, int n_threads, int mel_offset) {
+    (void)n_threads;  // ignored, as in the reference (main.rs:1799)
+    if (!valid(ctx)) return WMI_E_INVALID_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+    int rc = run_encode(ctx, mel_offset);
+    if (rc) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    float a = 0, b = 0;
+    (void)hipEventElapsedTime(&a, ctx->ev[1], ctx->ev[2]);
+    (void)hipEventElapsedTime(&b, ctx->ev[2], ctx->ev[3]);
+    ctx->timings.encode_ms = a;
+    ctx->timings.cross_kv_ms = b;
+    return WMI_OK;
+}
+
+int wmi_decode_greedy(wmi_context *ctx, int max_tokens, int suppress_eot, int32_t *tokens, int32_t *n_tokens) {
+    if (!valid(ctx) || !tokens || !n_tokens) return WMI_E_INVALID_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    std::vector<int32_t> tk, cnt;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+    int rc = run_greedy(ctx, max_tokens, suppress_eot, !suppress_eot, &tk, &cnt);
+    if (rc) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, ctx->ev[4], ctx->ev[5]);
+    ctx->timings.decode_ms = ms;
+    memcpy(tokens, tk.data(), tk.size() * 4);
+    memcpy(n_tokens, cnt.data(), cnt.size() * 4);
+    return WMI_OK;
+}
+
+int wmi_decode_logits(wmi_context *ctx, int clip, const int32_t *tokens, int n_tokens, float *logits) {
+    if (!valid(ctx) || !tokens || !logits || n_tokens < 1) return WMI_E_INVALID_ARG;
+    if (ctx->enc_T <= 0) return set_err(ctx, WMI_E_INVALID_ARG, "decode before encode");
+    if (clip < 0 || clip >= ctx->enc_clips) return set_err(ctx, WMI_E_INVALID_ARG, "clip %d", clip);
+    if (n_tokens > ctx->hp.n_text_ctx) return set_err(ctx, WMI_E_INVALID_ARG, "too many tokens");
+    for (int i = 0; i < n_tokens; ++i)
+        if (tokens[i] < 0 || tokens[i] >= ctx->hp.n_vocab) return set_err(ctx, WMI_E_INVALID_ARG, "token id %d", tokens[i]);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc = ensure_decode_buffers(ctx, n_tokens, 1);
+    if (rc) return rc;
+    HIPCHK(ctx, hipMemcpyAsync(ctx->dfeed, tokens, (size_t)n_tokens * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * 8, ctx->stream));
+    const size_t V = ctx->hp.n_vocab;
+    for (int i = 0; i < n_tokens; ++i) {
+        rc = run_dec_steps(ctx, clip, 1, n_tokens, n_tokens, 0, 1, 1);
+        if (rc) return rc;
+        HIPCHK(ctx, hipMemcpyAsync(logits + (size_t)i * V, ctx->dlogits, V * 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return WMI_OK;
+}
+
+int wmi_full(wmi_context *ctx, const float *pcm, size_t n_samples, int max_tokens, int32_t *tokens, int32_t *n_tokens) {
+    int rc = wmi_pcm_to_mel(ctx, pcm, n_samples);
+    if (rc) return rc;
+    rc = wmi_encode(ctx, 1, 0);
+    if (rc) return rc;
+    return wmi_decode_greedy(ctx, max_tokens, 0, tokens, n_tokens);
+}
+
+int wmi_stage_pcm(wmi_context *ctx, int n_clips, const float *const *pcm, const size_t *n_samples) {
+    if (!valid(ctx)) return WMI_E_INVALID_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    return stage_pcm(ctx, n_clips, pcm, n_samples);
+}
+
+int wmi_run_staged(wmi_context *ctx, int mel_offset, int n_decode) {
+    if (!valid(ctx)) return WMI_E_INVALID_ARG;
+    if (ctx->n_clips < 1) return set_err(ctx, WMI_E_INVALID_ARG, "nothing staged");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+    int rc = run_mel(ctx);
+    if (rc) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+    rc = run_encode(ctx, mel_offset);
+    if (rc) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    rc = run_greedy(ctx, n_decode, 1, false, nullptr, nullptr);
+    if (rc) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->staged_n_decode = n_decode;
+    float a = 0, b = 0, c = 0, d = 0;
+    (void)hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]);
+    (void)hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]);
+    (void)hipEventElapsedTime(&c, ctx->ev[2], ctx->ev[3]);
+    (void)hipEventElapsedTime(&d, ctx->ev[3], ctx->ev[5]);
+    int32_t prompt[8];
+    ctx->timings = {a, b, c, d, prompt_tokens(ctx, prompt) + n_decode - 1};
+    return WMI_OK;
+}
+
+int wmi_get_tokens(const wmi_context *ctx, int32_t *tokens, size_t cap, int32_t *n_per_clip) {
+    if (!ctx || !tokens) return WMI_E_INVALID_ARG;
+    const size_t need = (size_t)ctx->enc_clips * ctx->staged_n_decode;
+    if (cap < need) return WMI_E_NO_SPACE;
+    if (hipMemcpy(tokens, ctx->dtokens, need * 4, hipMemcpyDeviceToHost) != hipSuccess) return WMI_E_HIP;
+    if (n_per_clip)
+        for (int b = 0; b < ctx->enc_clips; ++b) n_per_clip[b] = ctx->staged_n_decode;
+    return WMI_OK;
+}
+
+int wmi_get_timings(const wmi_context *ctx, wmi_timings *out) {
+    if (!ctx || !out) return WMI_E_INVALID_ARG;
+    *out = ctx->timings;
+    return WMI_OK;
+}
+
+int wmi_sync(wmi_context *ctx) {
+    if (!ctx) return WMI_E_INVALID_ARG;
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return WMI_OK;
+}
+
+int wmi_get_mel(const wmi_context *ctx, int clip, float *out, size_t cap, int32_t *n_mel, int32_t *n_len) {
+    if (!ctx || clip < 0 || clip >= ctx->n_clips) return WMI_E_INVALID_ARG;
+    const int64_t nl = ctx->n_len_host[clip];
+    if (n_mel) *n_mel = ctx->hp.n_mels;
+    if (n_len) *n_len = (int32_t)nl;
+    const size_t need = (size_t)ctx->hp.n_mels * nl;
+    if (!out) return WMI_OK;
+    if (cap < need) return WMI_E_NO_SPACE;
+    if (need && hipMemcpy(out, ctx->d_mel + (size_t)clip * ctx->mel_stride, need * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return WMI_E_HIP;
+    return WMI_OK;
+}
+
+int wmi_get_encoder_out(const wmi_context *ctx, int clip, float *out, size_t cap) {
+    if (!ctx || !out || clip < 0 || clip >= ctx->enc_clips || ctx->enc_T <= 0) return WMI_E_INVALID_ARG;
+    const size_t need = (size_t)ctx->enc_T * ctx->hp.n_audio_state;
+    if (cap < need) return WMI_E_NO_SPACE;
+    if (hipMemcpy(out, ctx->enc32 + (size_t)clip * need, need * 4, hipMemcpyDeviceToHost) != hipSuccess) return WMI_E_HIP;
+    return WMI_OK;
+}
+
+int wmi_get_cross_kv(const wmi_context *ctx, int clip, uint16_t *k, uint16_t *v, size_t cap) {
+    if (!ctx || !k || !v || clip < 0 || clip >= ctx->enc_clips || ctx->enc_T <= 0) return WMI_E_INVALID_ARG;
+    const size_t per = (size_t)ctx->enc_T * ctx->hp.n_text_state;
+    const size_t need = per * ctx->hp.n_text_layer;
+    if (cap < need) return WMI_E_NO_SPACE;
+    for (int l = 0; l < ctx->hp.n_text_layer; ++l) {
+        const size_t off = ((size_t)l * ctx->enc_clips + clip) * per;
+        if (hipMemcpy(k + l * per, ctx->ck + off, per * 2, hipMemcpyDeviceToHost) != hipSuccess) return WMI_E_HIP;
+        if (hipMemcpy(v + l * per, ctx->cv + off, per * 2, hipMemcpyDeviceToHost) != hipSuccess) return WMI_E_HIP;
+    }
+    return WMI_OK;
+}
+
+size_t wmi_dist_id_size(void) { return sizeof(ncclUniqueId); }
+
+int wmi_dist_make_id(void *id_out) {
+    if (!id_out) return WMI_E_INVALID_ARG;
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return set_err(nullptr, WMI_E_RCCL, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+    memcpy(id_out, &id, sizeof(id));
+    return WMI_OK;
+}
+
+int wmi_dist_init(wmi_context *ctx, int rank, int world, const void *id) {
+    if (!valid(ctx) || !id || world < 1 || rank < 0 || rank >= world) return WMI_E_INVALID_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof(uid));
+    RCCLCHK(ctx, ncclCommInitRank(&ctx->comm, world, uid, rank));
+    ctx->rank = rank;
+    ctx->world = world;
+    return WMI_OK;
+}
+
+int wmi_dist_gather_tokens(wmi_context *ctx, int32_t *out, size_t cap) {
+    if (!valid(ctx) || !ctx->comm) return WMI_E_INVALID_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const size_t count = (size_t)ctx->enc_clips * ctx->staged_n_decode;
+    const size_t total = count * ctx->world;
+    if (total > ctx->gather_cap) {
+        if (ctx->d_gather) HIPCHK(ctx, hipFree(ctx->d_gather));
+        HIPCHK(ctx, hipMalloc(&ctx->d_gather, total * 4));
+        ctx->gather_cap = total;
+    }
+    RCCLCHK(ctx, ncclGather(ctx->dtokens, ctx->d_gather, count, ncclInt32, 0, ctx->comm, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->rank == 0 && out) {
+        if (cap < total) return WMI_E_NO_SPACE;
+        HIPCHK(ctx, hipMemcpy(out, ctx->d_gather, total * 4, hipMemcpyDeviceToHost));
+    }
+    return WMI_OK;
+}
+
+int wmi_dist_barrier(wmi_context *ctx) {
+    if (!valid(ctx) || !ctx->comm) return WMI_E_INVALID_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (ctx->gather_cap < 1) {
+        if (ctx->d_gather) HIPCHK(ctx, hipFree(ctx->d_gather));
+        HIPCHK(ctx, hipMalloc(&ctx->d_gather, 4 * 4));
+        ctx->gather_cap = 4;
+    }
+    RCCLCHK(ctx, ncclAllReduce(ctx->d_gather, ctx->d_gather, 1, ncclInt32, ncclSum, ctx->comm, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return WMI_OK;
+}
+
+}  // extern "C"

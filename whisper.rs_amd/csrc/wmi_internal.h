@@ -1,0 +1,140 @@
+// wmi_internal.h — launch interface between the C-ABI host layer
+// (wmi_api.cpp) and the gfx950 kernels (wmi_kernels.hip).
+//
+// Every launcher enqueues on the given stream and returns hipError_t; no
+// launcher allocates, copies or synchronises, so a caller may capture any
+// sequence of them into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wmi {
+
+// ---- mel frontend (main.rs:1486-1671) ---------------------------------------
+// Constant tables built on the host with the reference's exact f32 formulas
+// (main.rs:1495, 1537, 1568), uploaded once.
+struct MelTables {
+    float hann[400];
+    float c400[200], s400[200], c200[100], s200[100], c100[50], s100[50], c50[25], s50[25];
+    float dc[625], ds[625];
+};
+
+// frames -> raw log10 mel [n_mel][n_len] + per-clip ordered-uint max.
+// pcm: n_clips pointers (device) with n_samples each (device arrays).
+hipError_t launch_mel_frames(hipStream_t s, const MelTables *tabs, const float *filt_t /*[201][n_mel]*/, int n_mel,
+                             const float *const *pcm, const int64_t *n_samples, float *mel, int64_t mel_stride,
+                             const int64_t *n_len, int64_t max_len, uint32_t *mel_max, int n_clips);
+// clamp_and_normalize in place on mel.
+hipError_t launch_mel_norm(hipStream_t s, float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
+                           int64_t max_len, const uint32_t *mel_max, int n_clips);
+// mel window (main.rs:1816-1833) -> conv1 input, f16 time-major, zero-padded
+// by one frame at each end and to Cp channels: X[b][T2 + 2][Cp].
+hipError_t launch_mel_window(hipStream_t s, const float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
+                             int mel_offset, int T2, int Cp, uint16_t *xconv, int n_clips);
+
+// ---- LayerNorm (ggml norm + mul(repeat(w)) + add(repeat(b))) ----------------
+hipError_t launch_layernorm(hipStream_t s, const float *x, int rows, int n, const float *w, const float *b,
+                            uint16_t *y16, float *y32);
+
+// ---- MFMA GEMM: C[M][N] = A[M][K] * B[N][K]^T, f16 in, f32 accumulate -------
+enum GemmEpi {
+    EPI_F32 = 0,        // out32[m][n] = acc + bias
+    EPI_RESID = 1,      // out32[m][n] = (acc + bias) + out32[m][n]
+    EPI_GELU16 = 2,     // out16[m][n] = gelu_tab[f16(acc + bias)]
+    EPI_QKV = 3,        // q/k [b][h][Tp][64], vt [b][h][64][Tp]   (acc + bias) -> f16
+    EPI_CONV1 = 4,      // out16[b][t + 1][n] = gelu_tab[f16(acc + bias)]  (padded time-major)
+    EPI_CONV2PE = 5,    // out32[b*T + t][n] = pe[t][n] + gelu_tab[f16(acc + bias)]
+    EPI_CROSSKV = 6,    // K: f16(acc * kscale), V: f16(acc + bias) -> [l][b][T][ns]
+};
+
+struct GemmArgs {
+    const uint16_t *A;  // plain: [M][lda]; conv: X[b][Tin + 2][Cp]
+    const uint16_t *B;  // [N][K]
+    const float *bias;  // [N] or null
+    int M, N, K, lda;
+    // implicit-GEMM conv: row m -> (b = m / Tout, t = m % Tout); k -> (tap, c)
+    int conv, conv_stride, conv_tin, conv_cp, conv_tout;
+    float *out32;
+    uint16_t *out16;
+    int ldo;
+    const uint16_t *gelu_tab;
+    const float *pe;    // EPI_CONV2PE: [T][N]
+    int T;              // rows per clip (for b/t split)
+    // EPI_QKV
+    uint16_t *q, *k, *vt;
+    int Tp, n_state;
+    // EPI_CROSSKV
+    uint16_t *ck, *cv;
+    int n_clips;
+    float kscale;
+};
+hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a);
+
+// ---- encoder self-attention (ggml flash_attn_f16 semantics, exact softmax) --
+struct AttnArgs {
+    const uint16_t *q, *k, *vt;  // [b][h][Tp][64], vt [b][h][64][Tp]
+    uint16_t *out;               // [b*T + t][n_state]
+    const uint16_t *exp_tab;     // f16 exp table, negative half
+    int n_exp;                   // entries in exp_tab
+    int T, Tp, H, n_state, n_clips;
+    float scale;
+};
+hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a);
+
+// ---- decoder step -----------------------------------------
+struct DecState {          // device-resident, advanced by the kernels
+    int32_t pos;           // position of the token being processed
+    int32_t pad[3];
+};
+
+enum DecEpi { DEC_QKV = 0, DEC_Q = 1, DEC_GELU = 2, DEC_RESID = 3, DEC_LOGITS = 4 };
+
+struct DecGemvArgs {
+    const float *x;          // LN input [B][K] f32 (ln != null)
+    const float *ln_w, *ln_b;
+    const uint16_t *xin16;   // non-LN input [B][K] f16
+    const uint16_t *W;       // [N][K]
+    const float *bias;       // [N] (null for logits)
+    int N, K, B;
+    float qscale;            // (n/h)^-0.25
+    // outputs
+    uint16_t *out16;         // DEC_Q / DEC_GELU / DEC_QKV(q): [B][ldo]
+    float *out32;            // DEC_RESID: x [B][N]; DEC_LOGITS: logits [B][N]
+    int ldo;
+    uint16_t *kcache, *vcache;  // DEC_QKV: [B][n_text_ctx][n]
+    int n_text_ctx;
+    const DecState *st;
+    const uint16_t *gelu_tab;
+    unsigned long long *amax;   // DEC_LOGITS: per-clip packed argmax
+    int suppress_id;            // DEC_LOGITS: id excluded from argmax (-1 none)
+    DecState *st_advance;       // DEC_LOGITS: pos += 1 (block 0)
+};
+hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a);
+
+struct DecAttnArgs {
+    const uint16_t *q;       // [B][n]
+    const uint16_t *K, *V;   // [B][ldkv_clip] rows of n
+    int64_t clip_stride;     // elements between clips in K/V
+    int M_fixed;             // >0: fixed key count (cross); 0: pos + 1 (self)
+    const DecState *st;
+    uint16_t *out;           // [B][n]
+    const uint16_t *exp_tab;
+    int n_exp, H, n, B;
+};
+hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a);
+
+struct DecEmbedArgs {
+    const uint16_t *te;      // [V][n]
+    const float *pe;         // [n_text_ctx][n]
+    float *x;                // [B][n]
+    const int32_t *feed;     // [B][feed_stride] tokens fed while pos < feed_len
+    int feed_len, feed_stride;
+    unsigned long long *amax;
+    int32_t *tokens_out;     // [B][out_stride]
+    int out_stride;
+    const DecState *st;
+    int n, B, record_only;
+};
+hipError_t launch_dec_embed(hipStream_t s, const DecEmbedArgs &a);
+
+}  // namespace wmi

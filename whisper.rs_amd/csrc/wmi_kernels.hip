@@ -1,0 +1,904 @@
+// wmi_kernels.hip — gfx950 (CDNA4) kernels for the Whisper hot path.
+//
+// Numerics follow the restated reference path (oracle/wmi_oracle.c):
+//   * mel: main.rs:1486-1671 operation for operation (f32, unfused), so the
+//     frontend matches the CPU restatement bit for bit except where the
+//     device log10f differs from glibc's by an ulp;
+//   * tensor ops: ggml-1.0.3 rounding points — activations
+//     rounded to f16 before every matmul/conv (free: MFMA takes f16),
+//     f32 accumulation, f16 GELU/exp lookup tables (uploaded from the host,
+//     so the device uses the exact table values), double-accumulated norm,
+//     and the flash-attn softmax computed EXACTLY as ggml does (true row max,
+//     table exp of f16(s - max), normalise, round to f16, then P·V), which
+//     takes three passes over the keys instead of an online softmax.
+//
+// f32 multiply/add stay separately rounded (no FMA contraction) everywhere a
+// reference operation is restated; MFMA and the dot-product accumulations
+// are the only places where the summation order differs from the CPU.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "wmi_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace wmi {
+
+typedef _Float16 f16;
+typedef f16 half8 __attribute__((ext_vector_type(8)));
+typedef f16 half4 __attribute__((ext_vector_type(4)));
+typedef f16 half2v __attribute__((ext_vector_type(2)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint16_t f2h_bits(float x) { return __builtin_bit_cast(uint16_t, (f16)x); }
+__device__ __forceinline__ float h2f_bits(uint16_t b) { return (float)__builtin_bit_cast(f16, b); }
+__device__ __forceinline__ uint32_t ord_f32(float v) {
+    const uint32_t u = __float_as_uint(v);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f32(uint32_t o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float gelu_lookup(const uint16_t *tab, float x) { return h2f_bits(tab[f2h_bits(x)]); }
+
+static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// dynamic LDS above 64 KiB must be opted into per kernel (gfx950 has 160 KiB)
+template <typename K>
+static hipError_t allow_lds(K *kern, size_t bytes) {
+    if (bytes <= 65536) return hipSuccess;
+    return hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+// ============================================================================
+// mel frontend
+// ============================================================================
+constexpr int MEL_WAVES = 4;
+constexpr int MEL_FPW = 2;  // frames per wave
+constexpr int MEL_SCRATCH = 2000;  // floats per wave: fin[400], A[800], B[800]
+
+struct cpx {
+    float re, im;
+};
+
+// one radix-2 combine level of fft (main.rs:1536-1550) for all sub-arrays:
+// out sub-array s (size n) = combine(E = in[s], O = in[s + nsub]) where the
+// input holds 2*nsub sub-arrays of size n/2.
+__device__ __forceinline__ void fft_level(const cpx *in, cpx *out, int n, int nsub, const float *cs, const float *sn,
+                                          int lane) {
+    const int half = n / 2;
+    for (int task = lane; task < nsub * half; task += 64) {
+        const int s = task / half, k = task - s * half;
+        const cpx E = in[s * half + k], O = in[(s + nsub) * half + k];
+        const float re = cs[k], im = -sn[k];
+        cpx a, b;
+        a.re = E.re + re * O.re - im * O.im;
+        a.im = E.im + re * O.im + im * O.re;
+        b.re = E.re - re * O.re + im * O.im;
+        b.im = E.im - re * O.im - im * O.re;
+        out[s * n + k] = a;
+        out[s * n + k + half] = b;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mel_frames(const MelTables *__restrict__ tabs_g, const float *__restrict__ filt_t,
+                                                    int n_mel, const float *const *pcm, const int64_t *n_samples,
+                                                    float *mel, int64_t mel_stride, const int64_t *n_len,
+                                                    uint32_t *mel_max) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int b = blockIdx.y;
+    const int64_t nl = n_len[b];
+    const int64_t frame0 = (int64_t)blockIdx.x * (MEL_WAVES * MEL_FPW);
+    if (frame0 >= nl) return;
+    MelTables *tabs = (MelTables *)sm;
+    float *F = sm + sizeof(MelTables) / 4;
+    float *scratch = F + 201 * n_mel;
+    {
+        const float *src = (const float *)tabs_g;
+        float *dst = (float *)tabs;
+        for (int i = threadIdx.x; i < (int)(sizeof(MelTables) / 4); i += 256) dst[i] = src[i];
+        for (int i = threadIdx.x; i < 201 * n_mel; i += 256) F[i] = filt_t[i];
+    }
+    __syncthreads();
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float *fin = scratch + w * MEL_SCRATCH;
+    cpx *A = (cpx *)(fin + 400);
+    cpx *Bf = (cpx *)(fin + 1200);
+    const float *x = pcm[b];
+    const int64_t ns = n_samples[b];
+    float lmax = -INFINITY;
+    float *melb = mel + (int64_t)b * mel_stride;
+    for (int f = 0; f < MEL_FPW; ++f) {
+        const int64_t i = frame0 + w * MEL_FPW + f;
+        if (i >= nl) break;
+        const int64_t off = i * 160;
+        // window, zero past the end (main.rs:1594-1601)
+        for (int j = lane; j < 400; j += 64) fin[j] = (off + j < ns) ? tabs->hann[j] * x[off + j] : 0.0f;
+        wave_sync();
+        // 16 DFT-25 leaves: residue r = in[r + 16 j] (main.rs:1487-1502)
+        for (int task = lane; task < 400; task += 64) {
+            const int r = task / 25, k = task - r * 25;
+            float re = 0.0f, im = 0.0f;
+            for (int j = 0; j < 25; ++j) {
+                const float v = fin[r + 16 * j];
+                re = re + v * tabs->dc[k * j];
+                im = im - v * tabs->ds[k * j];
+            }
+            A[r * 25 + k] = cpx{re, im};
+        }
+        wave_sync();
+        fft_level(A, Bf, 50, 8, tabs->c50, tabs->s50, lane);
+        wave_sync();
+        fft_level(Bf, A, 100, 4, tabs->c100, tabs->s100, lane);
+        wave_sync();
+        fft_level(A, Bf, 200, 2, tabs->c200, tabs->s200, lane);
+        wave_sync();
+        fft_level(Bf, A, 400, 1, tabs->c400, tabs->s400, lane);
+        wave_sync();
+        // power (main.rs:1603-1606), fold (main.rs:1608-1610)
+        for (int j = lane; j < 400; j += 64) fin[j] = A[j].re * A[j].re + A[j].im * A[j].im;
+        wave_sync();
+        float fold[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = lane + 64 * q;
+            fold[q] = (j >= 1 && j < 200) ? fin[j] + fin[400 - j] : 0.0f;
+        }
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = lane + 64 * q;
+            if (j >= 1 && j < 200) fin[j] = fold[q];
+        }
+        wave_sync();
+        // filterbank, clamp, log10 (main.rs:1620-1634)
+        for (int m = lane; m < n_mel; m += 64) {
+            float sum = 0.0f;
+            for (int k = 0; k < 201; ++k) sum = sum + fin[k] * F[k * n_mel + m];
+            if (sum < 1e-10f) sum = 1e-10f;
+            // glibc's log10f (what Rust's f32::log10 calls) is within an ulp of
+            // the correctly rounded result; the double path lands on the same
+            // float for ~96% of inputs, the device log10f for far fewer.
+            const float v = (float)log10((double)sum);
+            melb[(int64_t)m * nl + i] = v;
+            lmax = fmaxf(lmax, v);
+        }
+        wave_sync();
+    }
+    lmax = wave_max(lmax);
+    if (lane == 0 && lmax > -INFINITY) atomicMax(&mel_max[b], ord_f32(lmax));
+}
+
+__global__ void k_mel_norm(float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len, const uint32_t *mel_max) {
+    const int b = blockIdx.y;
+    const int64_t tot = (int64_t)n_mel * n_len[b];
+    const double mmax = (double)unord_f32(mel_max[b]) - 8.0;  // clamp_and_normalize, main.rs:1654-1671
+    float *p = mel + (int64_t)b * mel_stride;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (int64_t)gridDim.x * blockDim.x) {
+        float v = p[i];
+        if ((double)v < mmax) v = (float)mmax;
+        p[i] = (v + 4.0f) / 4.0f;
+    }
+}
+
+__global__ void k_mel_window(const float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len, int mel_offset,
+                             int T2, int Cp, uint16_t *xconv) {
+    const int b = blockIdx.y;
+    const int64_t nl = n_len[b];
+    const int64_t tot = (int64_t)(T2 + 2) * Cp;
+    const int64_t i0 = mel_offset < nl ? mel_offset : nl;
+    const int64_t i1 = (int64_t)mel_offset + T2 < nl ? (int64_t)mel_offset + T2 : nl;
+    const float *p = mel + (int64_t)b * mel_stride;
+    uint16_t *o = xconv + (int64_t)b * tot;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = idx / Cp;
+        const int c = (int)(idx - row * Cp);
+        const int64_t t = row - 1;
+        float v = 0.0f;
+        if (t >= 0 && t < T2 && c < n_mel && i0 + t < i1) v = p[(int64_t)c * nl + i0 + t];
+        o[idx] = f2h_bits(v);
+    }
+}
+
+hipError_t launch_mel_frames(hipStream_t s, const MelTables *tabs, const float *filt_t, int n_mel,
+                             const float *const *pcm, const int64_t *n_samples, float *mel, int64_t mel_stride,
+                             const int64_t *n_len, int64_t max_len, uint32_t *mel_max, int n_clips) {
+    const size_t lds = sizeof(MelTables) + sizeof(float) * (201 * n_mel + MEL_WAVES * MEL_SCRATCH);
+    dim3 grid(cdiv(max_len, MEL_WAVES * MEL_FPW), n_clips);
+    if (max_len <= 0) return hipSuccess;
+    hipError_t e = allow_lds(k_mel_frames, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_mel_frames, grid, dim3(256), lds, s, tabs, filt_t, n_mel, pcm, n_samples, mel, mel_stride,
+                       n_len, mel_max);
+    return hipGetLastError();
+}
+
+hipError_t launch_mel_norm(hipStream_t s, float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
+                           int64_t max_len, const uint32_t *mel_max, int n_clips) {
+    if (max_len <= 0) return hipSuccess;
+    dim3 grid(cdiv((int64_t)n_mel * max_len, 1024) < 512 ? cdiv((int64_t)n_mel * max_len, 1024) : 512, n_clips);
+    hipLaunchKernelGGL(k_mel_norm, grid, dim3(256), 0, s, mel, mel_stride, n_mel, n_len, mel_max);
+    return hipGetLastError();
+}
+
+hipError_t launch_mel_window(hipStream_t s, const float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
+                             int mel_offset, int T2, int Cp, uint16_t *xconv, int n_clips) {
+    const int64_t tot = (int64_t)(T2 + 2) * Cp;
+    dim3 grid(cdiv(tot, 1024) < 512 ? cdiv(tot, 1024) : 512, n_clips);
+    hipLaunchKernelGGL(k_mel_window, grid, dim3(256), 0, s, mel, mel_stride, n_mel, n_len, mel_offset, T2, Cp, xconv);
+    return hipGetLastError();
+}
+
+// ============================================================================
+// LayerNorm: ggml_compute_forward_norm_f32 (double mean / variance, eps 1e-5)
+// followed by mul(repeat(w)) and add(repeat(b)) (main.rs:1881-1886)
+// ============================================================================
+__device__ __forceinline__ void layernorm_wave(const float *x, int n, const float *w, const float *b, uint16_t *y16,
+                                               float *y32, int lane) {
+    double s = 0.0;
+    for (int i = lane; i < n; i += 64) s += (double)x[i];
+    s = wave_sum(s);
+    const double mean = s / n;
+    double s2 = 0.0;
+    for (int i = lane; i < n; i += 64) {
+        const double v = (double)x[i] - mean;
+        s2 += v * v;
+    }
+    s2 = wave_sum(s2);
+    const float scale = (float)(1.0 / sqrt(s2 / n + (double)1e-5f));
+    for (int i = lane; i < n; i += 64) {
+        const float yv = (float)((double)x[i] - mean);
+        const float t = yv * scale;
+        const float o = b[i] + w[i] * t;
+        if (y16) y16[i] = f2h_bits(o);
+        if (y32) y32[i] = o;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_layernorm(const float *x, int rows, int n, const float *w, const float *b,
+                                                   uint16_t *y16, float *y32) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    layernorm_wave(x + (int64_t)row * n, n, w, b, y16 ? y16 + (int64_t)row * n : nullptr,
+                   y32 ? y32 + (int64_t)row * n : nullptr, threadIdx.x & 63);
+}
+
+hipError_t launch_layernorm(hipStream_t s, const float *x, int rows, int n, const float *w, const float *b,
+                            uint16_t *y16, float *y32) {
+    hipLaunchKernelGGL(k_layernorm, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, rows, n, w, b, y16, y32);
+    return hipGetLastError();
+}
+
+// ============================================================================
+// MFMA GEMM  C[M][N] = A[M][K] * B[N][K]^T   (f16 x f16 -> f32)
+// 256 threads = 2x2 waves; each wave owns (BM/2)x(BN/2) built from
+// v_mfma_f32_32x32x16_f16 tiles; BK = 32, register-staged double-buffered
+// LDS with 80-byte rows (conflict-free ds_read_b128 fragment reads).
+// ============================================================================
+constexpr int GBK = 32;
+constexpr int GLDS = 40;  // halfs per LDS row (32 + 8 pad)
+
+template <bool CONV>
+__device__ __forceinline__ uint4 gemm_load_a(const GemmArgs &a, int m, int k) {
+    if (m >= a.M) return make_uint4(0, 0, 0, 0);
+    const uint16_t *p;
+    if (CONV) {
+        const int b = m / a.conv_tout;
+        const int t = m - b * a.conv_tout;
+        const int tap = k / a.conv_cp;
+        const int c = k - tap * a.conv_cp;
+        p = a.A + ((int64_t)b * (a.conv_tin + 2) + (int64_t)t * a.conv_stride + tap) * a.conv_cp + c;
+    } else {
+        p = a.A + (int64_t)m * a.lda + k;
+    }
+    return *(const uint4 *)p;
+}
+
+template <int EPI>
+__device__ __forceinline__ void gemm_epi4(const GemmArgs &a, int m, int n, const float *v) {
+    // v[0..3] = rows m..m+3 of column n
+    if (n >= a.N) return;
+    const float bias = a.bias ? a.bias[n] : 0.0f;
+    if (EPI == EPI_QKV) {
+        const int ns = a.n_state;
+        const int which = n / ns, c = n - which * ns, h = c >> 6, d = c & 63;
+        const int H = ns >> 6;
+        if (which < 2) {
+            uint16_t *dst = which == 0 ? a.q : a.k;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int mm = m + r;
+                if (mm >= a.M) break;
+                const int b = mm / a.T, t = mm - b * a.T;
+                dst[(((int64_t)b * H + h) * a.Tp + t) * 64 + d] = f2h_bits(v[r] + bias);
+            }
+        } else {
+            const int b0 = m / a.T, t0 = m - b0 * a.T;
+            if (m + 3 < a.M && t0 + 3 < a.T && (t0 & 3) == 0) {
+                half4 hv;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) hv[r] = (f16)(v[r] + bias);
+                *(half4 *)(a.vt + (((int64_t)b0 * H + h) * 64 + d) * a.Tp + t0) = hv;
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int mm = m + r;
+                    if (mm >= a.M) break;
+                    const int b = mm / a.T, t = mm - b * a.T;
+                    a.vt[(((int64_t)b * H + h) * 64 + d) * a.Tp + t] = f2h_bits(v[r] + bias);
+                }
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int mm = m + r;
+        if (mm >= a.M) break;
+        if (EPI == EPI_F32) {
+            a.out32[(int64_t)mm * a.ldo + n] = v[r] + bias;
+        } else if (EPI == EPI_RESID) {
+            float *p = a.out32 + (int64_t)mm * a.ldo + n;
+            *p = (v[r] + bias) + *p;
+        } else if (EPI == EPI_GELU16) {
+            a.out16[(int64_t)mm * a.ldo + n] = a.gelu_tab[f2h_bits(v[r] + bias)];
+        } else if (EPI == EPI_CONV1) {
+            const int b = mm / a.T, t = mm - b * a.T;
+            a.out16[((int64_t)b * (a.T + 2) + t + 1) * a.ldo + n] = a.gelu_tab[f2h_bits(v[r] + bias)];
+        } else if (EPI == EPI_CONV2PE) {
+            const int b = mm / a.T, t = mm - b * a.T;
+            (void)b;
+            a.out32[(int64_t)mm * a.ldo + n] = a.pe[(int64_t)t * a.ldo + n] + gelu_lookup(a.gelu_tab, v[r] + bias);
+        } else if (EPI == EPI_CROSSKV) {
+            const int ns = a.n_state;
+            const int l = n / (2 * ns), rr = n - l * 2 * ns;
+            const int b = mm / a.T, t = mm - b * a.T;
+            const int64_t base = (((int64_t)l * a.n_clips + b) * a.T + t) * ns;
+            if (rr < ns) a.ck[base + rr] = f2h_bits(v[r] * a.kscale);
+            else a.cv[base + rr - ns] = f2h_bits(v[r] + bias);
+        }
+    }
+}
+
+template <int BM, int BN, int EPI, bool CONV>
+__global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
+    constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave (2x2 waves)
+    constexpr int ACH = BM / 64, BCH = BN / 64;  // 16-byte chunks per thread per k-tile
+    __shared__ __attribute__((aligned(16))) f16 smem[2 * (BM + BN) * GLDS];
+    f16 *As = smem;
+    f16 *Bs = smem + 2 * BM * GLDS;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // XCD-aware tile order: consecutive block ids land on different XCDs, so
+    // give each XCD a contiguous range of tiles (bijective remap).
+    const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
+    const int nwg = nbm * nbn;
+    int bid = blockIdx.x;
+    {
+        const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+    }
+    const int bn = bid % nbn, bm = bid / nbn;
+    const int m0 = bm * BM, n0 = bn * BN;
+    const int nk = a.K / GBK;
+
+    uint4 ra[ACH], rb[BCH];
+    auto gload = [&](int kt) {
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) {
+            const int c = tid + i * 256, row = c >> 2, col = (c & 3) * 8;
+            ra[i] = gemm_load_a<CONV>(a, m0 + row, kt * GBK + col);
+        }
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            const int c = tid + i * 256, row = c >> 2, col = (c & 3) * 8;
+            const int n = n0 + row;
+            rb[i] = n < a.N ? *(const uint4 *)(a.B + (int64_t)n * a.K + kt * GBK + col) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) {
+            const int c = tid + i * 256, row = c >> 2, col = (c & 3) * 8;
+            *(uint4 *)(As + buf * BM * GLDS + row * GLDS + col) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            const int c = tid + i * 256, row = c >> 2, col = (c & 3) * 8;
+            *(uint4 *)(Bs + buf * BN * GLDS + row * GLDS + col) = rb[i];
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    const int lr = lane & 31, lh = lane >> 5;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) gload(kt + 1);
+        const f16 *Ab = As + buf * BM * GLDS;
+        const f16 *Bb = Bs + buf * BN * GLDS;
+#pragma unroll
+        for (int ks = 0; ks < GBK / 16; ++ks) {
+            half8 af[TM], bf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                af[i] = *(const half8 *)(Ab + (wm * (BM / 2) + i * 32 + lr) * GLDS + ks * 16 + lh * 8);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                bf[j] = *(const half8 *)(Bb + (wn * (BN / 2) + j * 32 + lr) * GLDS + ks * 16 + lh * 8);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) sstore(buf ^ 1);
+        __syncthreads();
+    }
+    // epilogue: lane holds column n, rows (reg&3) + 8(reg>>2) + 4(lane>>5)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * (BN / 2) + j * 32 + lr;
+            const int mb = m0 + wm * (BM / 2) + i * 32 + 4 * lh;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                gemm_epi4<EPI>(a, mb + 8 * g, n, v);
+            }
+        }
+}
+
+template <int BM, int BN, bool CONV>
+static hipError_t gemm_dispatch_epi(hipStream_t s, int epi, const GemmArgs &a) {
+    const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+    dim3 grid(nwg), block(256);
+#define GEMM_CASE(E)                                                                  \
+    case E:                                                                          \
+        hipLaunchKernelGGL((k_gemm<BM, BN, E, CONV>), grid, block, 0, s, a);         \
+        break;
+    if constexpr (CONV) {
+        switch (epi) {
+            GEMM_CASE(EPI_CONV1)
+            GEMM_CASE(EPI_CONV2PE)
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (epi) {
+            GEMM_CASE(EPI_F32)
+            GEMM_CASE(EPI_RESID)
+            GEMM_CASE(EPI_GELU16)
+            GEMM_CASE(EPI_QKV)
+            GEMM_CASE(EPI_CROSSKV)
+            default: return hipErrorInvalidValue;
+        }
+    }
+#undef GEMM_CASE
+    return hipGetLastError();
+}
+
+hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a) {
+    if (a.M <= 0 || a.N <= 0) return hipSuccess;
+    if (a.K % GBK != 0 || a.K <= 0) return hipErrorInvalidValue;
+    if (a.conv && a.conv_cp % GBK != 0) return hipErrorInvalidValue;
+    const int64_t t128 = (int64_t)cdiv(a.M, 128) * cdiv(a.N, 128);
+    const int64_t t12864 = (int64_t)cdiv(a.M, 128) * cdiv(a.N, 64);
+    if (a.conv) {
+        if (t128 >= 240) return gemm_dispatch_epi<128, 128, true>(s, epi, a);
+        if (t12864 >= 240) return gemm_dispatch_epi<128, 64, true>(s, epi, a);
+        return gemm_dispatch_epi<64, 64, true>(s, epi, a);
+    }
+    if (t128 >= 240) return gemm_dispatch_epi<128, 128, false>(s, epi, a);
+    if (t12864 >= 240) return gemm_dispatch_epi<128, 64, false>(s, epi, a);
+    return gemm_dispatch_epi<64, 64, false>(s, epi, a);
+}
+
+// ============================================================================
+// Encoder self-attention, ggml flash_attn_f16 semantics (masked = false).
+// One workgroup = 32 queries of one (clip, head); its 4 waves split the keys
+// in 32-key tiles.  S^T = K Q^T per tile on MFMA (keys in registers, the
+// query on the lane), so row reductions are lane-local.
+//   pass 1: row max of scale*S            (exact, as ggml_vec_max_f32)
+//   pass 2: sum of exp_tab[f16(s - max)]  (double)
+//   pass 3: P16 = f16(p * (1/sum)); O += P16 V on MFMA (P16 used straight
+//           from the S^T accumulator registers as the A operand)
+// The f16 exp table's negative half lives in LDS.
+// ============================================================================
+constexpr int ATT_QB = 32;
+
+__global__ __launch_bounds__(256) void k_attn_enc(AttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+    uint16_t *tab = (uint16_t *)smraw;
+    const int tab_bytes = ((a.n_exp * 2 + 15) / 16) * 16;
+    float *red = (float *)(smraw + tab_bytes);          // [4][32] f32
+    double *redd = (double *)(red + 128);               // [4][32] f64
+    float *opart = (float *)(redd + 128);               // [3][32][64] f32
+    const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int lr = lane & 31, lh = lane >> 5;
+    for (int i = tid; i < a.n_exp; i += 256) tab[i] = a.exp_tab[i];
+    const int64_t bh = (int64_t)b * a.H + h;
+    const f16 *Q = (const f16 *)a.q + bh * a.Tp * 64;
+    const f16 *K = (const f16 *)a.k + bh * a.Tp * 64;
+    const f16 *Vt = (const f16 *)a.vt + bh * 64 * a.Tp;
+    const int q0 = qb * ATT_QB;
+    const int T = a.T;
+    const float scale = a.scale;
+    half8 qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *(const half8 *)(Q + (int64_t)(q0 + lr) * 64 + 16 * s + 8 * lh);
+    const int ntiles = (T + 31) / 32;
+    __syncthreads();
+
+    auto qk_tile = [&](int key0) {
+        floatx16 sacc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[r] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const half8 kf = *(const half8 *)(K + (int64_t)(key0 + lr) * 64 + 16 * s + 8 * lh);
+            sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], sacc, 0, 0, 0);
+        }
+        return sacc;
+    };
+
+    // pass 1: max
+    float mx = -INFINITY;
+    for (int kt = w; kt < ntiles; kt += 4) {
+        const int key0 = kt * 32;
+        const floatx16 sacc = qk_tile(key0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (key < T) mx = fmaxf(mx, sacc[r] * scale);
+        }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    if (lh == 0) red[w * 32 + lr] = mx;
+    __syncthreads();
+    const float mrow = fmaxf(fmaxf(red[lr], red[32 + lr]), fmaxf(red[64 + lr], red[96 + lr]));
+
+    auto pexp = [&](float sv) -> float {
+        const uint32_t i = f2h_bits(sv - mrow) & 0x7fffu;
+        return (int)i < a.n_exp ? h2f_bits(tab[i]) : 0.0f;
+    };
+    // pass 2: sum
+    double sum = 0.0;
+    for (int kt = w; kt < ntiles; kt += 4) {
+        const int key0 = kt * 32;
+        const floatx16 sacc = qk_tile(key0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (key < T) sum += (double)pexp(sacc[r] * scale);
+        }
+    }
+    sum += __shfl_xor(sum, 32);
+    if (lh == 0) redd[w * 32 + lr] = sum;
+    __syncthreads();
+    const float sumf = (float)(((redd[lr] + redd[32 + lr]) + redd[64 + lr]) + redd[96 + lr]);
+    const float inv = (float)(1.0 / (double)sumf);
+
+    // pass 3: O = P16 V
+    floatx16 o0, o1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] = 0.0f; o1[r] = 0.0f; }
+    for (int kt = w; kt < ntiles; kt += 4) {
+        const int key0 = kt * 32;
+        const floatx16 sacc = qk_tile(key0);
+        half8 pa[2];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            const float p = key < T ? pexp(sacc[r] * scale) * inv : 0.0f;
+            pa[r >> 3][r & 7] = (f16)p;
+        }
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            const f16 *vrow = Vt + (int64_t)(dt * 32 + lr) * a.Tp + key0;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const half4 v0 = *(const half4 *)(vrow + 16 * s + 4 * lh);
+                const half4 v1 = *(const half4 *)(vrow + 16 * s + 8 + 4 * lh);
+                half8 vb;
+                vb[0] = v0[0]; vb[1] = v0[1]; vb[2] = v0[2]; vb[3] = v0[3];
+                vb[4] = v1[0]; vb[5] = v1[1]; vb[6] = v1[2]; vb[7] = v1[3];
+                if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[s], vb, o0, 0, 0, 0);
+                else o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[s], vb, o1, 0, 0, 0);
+            }
+        }
+    }
+    // combine the 4 waves' partial O: ((w0 + w1) + w2) + w3
+    if (w > 0) {
+        float *op = opart + (w - 1) * 32 * 64;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int q = (r & 3) + 8 * (r >> 2) + 4 * lh;
+            op[q * 64 + lr] = o0[r];
+            op[q * 64 + 32 + lr] = o1[r];
+        }
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int q = (r & 3) + 8 * (r >> 2) + 4 * lh;
+            const int t = q0 + q;
+            float v0 = o0[r], v1 = o1[r];
+#pragma unroll
+            for (int ww = 0; ww < 3; ++ww) {
+                v0 = v0 + opart[ww * 2048 + q * 64 + lr];
+                v1 = v1 + opart[ww * 2048 + q * 64 + 32 + lr];
+            }
+            if (t < T) {
+                uint16_t *dst = a.out + ((int64_t)b * T + t) * a.n_state + h * 64;
+                dst[lr] = f2h_bits(v0);
+                dst[32 + lr] = f2h_bits(v1);
+            }
+        }
+    }
+}
+
+hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a) {
+    const size_t lds = ((a.n_exp * 2 + 15) / 16) * 16 + 128 * 4 + 128 * 8 + 3 * 32 * 64 * 4;
+    dim3 grid(cdiv(a.T, ATT_QB), a.H, a.n_clips);
+    hipError_t e = allow_lds(k_attn_enc, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_attn_enc, grid, dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
+// ============================================================================
+// decoder step kernels (batch B <= 8 clips)
+// ============================================================================
+constexpr int DG_RPW = 4;  // output rows per wave
+constexpr int DG_MAXB = 8;
+
+__device__ __forceinline__ float dot8(const half8 w, const half8 x, float acc) {
+    acc = __builtin_amdgcn_fdot2(half2v{w[0], w[1]}, half2v{x[0], x[1]}, acc, false);
+    acc = __builtin_amdgcn_fdot2(half2v{w[2], w[3]}, half2v{x[2], x[3]}, acc, false);
+    acc = __builtin_amdgcn_fdot2(half2v{w[4], w[5]}, half2v{x[4], x[5]}, acc, false);
+    acc = __builtin_amdgcn_fdot2(half2v{w[6], w[7]}, half2v{x[6], x[7]}, acc, false);
+    return acc;
+}
+
+template <int EPI, bool LN>
+__global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+    f16 *xs = (f16 *)smraw;  // [B][K]
+    __shared__ unsigned long long amax_s[DG_MAXB];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int K = a.K, B = a.B;
+    if (LN) {
+        for (int rb = w; rb < B; rb += 4)
+            layernorm_wave(a.x + (int64_t)rb * K, K, a.ln_w, a.ln_b, (uint16_t *)(xs + rb * K), nullptr, lane);
+    } else {
+        const uint4 *src = (const uint4 *)a.xin16;
+        uint4 *dst = (uint4 *)xs;
+        for (int i = tid; i < B * K / 8; i += 256) dst[i] = src[i];
+    }
+    if (EPI == DEC_LOGITS && tid < DG_MAXB) amax_s[tid] = 0ull;
+    __syncthreads();
+    const int row0 = (blockIdx.x * 4 + w) * DG_RPW;
+    float acc[DG_RPW][DG_MAXB];
+#pragma unroll
+    for (int r = 0; r < DG_RPW; ++r)
+#pragma unroll
+        for (int bb = 0; bb < DG_MAXB; ++bb) acc[r][bb] = 0.0f;
+    for (int kc = lane * 8; kc < K; kc += 512) {
+        half8 wv[DG_RPW];
+#pragma unroll
+        for (int r = 0; r < DG_RPW; ++r) {
+            const int o = row0 + r;
+            if (o < a.N) wv[r] = *(const half8 *)((const f16 *)a.W + (int64_t)o * K + kc);
+            else
+#pragma unroll
+                for (int e = 0; e < 8; ++e) wv[r][e] = (f16)0.0f;
+        }
+#pragma unroll
+        for (int bb = 0; bb < DG_MAXB; ++bb) {
+            if (bb < B) {
+                const half8 xv = *(const half8 *)(xs + bb * K + kc);
+#pragma unroll
+                for (int r = 0; r < DG_RPW; ++r) acc[r][bb] = dot8(wv[r], xv, acc[r][bb]);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < DG_RPW; ++r)
+#pragma unroll
+        for (int bb = 0; bb < DG_MAXB; ++bb)
+            if (bb < B) acc[r][bb] = wave_sum(acc[r][bb]);
+    // epilogue: lane (r * B + bb) owns value (r, bb)
+    const int pos = (EPI == DEC_QKV) ? a.st->pos : 0;
+#pragma unroll
+    for (int r = 0; r < DG_RPW; ++r)
+#pragma unroll
+        for (int bb = 0; bb < DG_MAXB; ++bb) {
+            if (bb >= B || lane != r * DG_MAXB + bb) continue;
+            const int o = row0 + r;
+            if (o >= a.N) continue;
+            const float v = acc[r][bb];
+            if (EPI == DEC_QKV) {
+                const int n = a.N / 3, which = o / n, c = o - which * n;
+                if (which == 0) a.out16[bb * a.ldo + c] = f2h_bits((v + a.bias[o]) * a.qscale);
+                else if (which == 1)
+                    a.kcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(v * a.qscale);
+                else a.vcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(a.bias[o] + v);
+            } else if (EPI == DEC_Q) {
+                a.out16[bb * a.ldo + o] = f2h_bits((v + a.bias[o]) * a.qscale);
+            } else if (EPI == DEC_GELU) {
+                a.out16[bb * a.ldo + o] = a.gelu_tab[f2h_bits(v + a.bias[o])];
+            } else if (EPI == DEC_RESID) {
+                float *p = a.out32 + (int64_t)bb * a.N + o;
+                *p = (v + a.bias[o]) + *p;
+            } else if (EPI == DEC_LOGITS) {
+                a.out32[(int64_t)bb * a.N + o] = v;
+                if (o != a.suppress_id) {
+                    const unsigned long long key =
+                        ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)o);
+                    atomicMax(&amax_s[bb], key);
+                }
+            }
+        }
+    if (EPI == DEC_LOGITS) {
+        __syncthreads();
+        if (tid < B && amax_s[tid]) atomicMax(&a.amax[tid], amax_s[tid]);
+        if (blockIdx.x == 0 && tid == 0) a.st_advance->pos += 1;
+    }
+}
+
+hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a) {
+    if (a.B < 1 || a.B > DG_MAXB || a.K % 8) return hipErrorInvalidValue;
+    dim3 grid(cdiv(a.N, 4 * DG_RPW)), block(256);
+    const size_t lds = (size_t)a.B * a.K * 2;
+    const bool ln = a.ln_w != nullptr;
+#define DG(E, L)                                                              \
+    do {                                                                      \
+        hipError_t e_ = allow_lds(k_dec_gemv<E, L>, lds);                     \
+        if (e_ != hipSuccess) return e_;                                      \
+        hipLaunchKernelGGL((k_dec_gemv<E, L>), grid, block, lds, s, a);       \
+    } while (0)
+    switch (epi) {
+        case DEC_QKV: if (ln) DG(DEC_QKV, true); else DG(DEC_QKV, false); break;
+        case DEC_Q: if (ln) DG(DEC_Q, true); else DG(DEC_Q, false); break;
+        case DEC_GELU: if (ln) DG(DEC_GELU, true); else DG(DEC_GELU, false); break;
+        case DEC_RESID: if (ln) DG(DEC_RESID, true); else DG(DEC_RESID, false); break;
+        case DEC_LOGITS: if (ln) DG(DEC_LOGITS, true); else DG(DEC_LOGITS, false); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef DG
+    return hipGetLastError();
+}
+
+// decoder attention for one (clip, head): scores over M keys (pre-scaled f16
+// K rows), softmax as ggml_compute_forward_soft_max_f32 (table exp, double
+// sum), P16 = f16(p * (1/sum)), out = sum_j P16_j V_j (f32) -> f16.
+constexpr int DA_THREADS = 512;
+__global__ __launch_bounds__(DA_THREADS) void k_dec_attn(DecAttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+    const int h = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int NW = DA_THREADS / 64;
+    const int M = a.M_fixed > 0 ? a.M_fixed : a.st->pos + 1;
+    const int n = a.n;
+    float *S = (float *)smraw;                         // [M]
+    uint16_t *P = (uint16_t *)(S + ((M + 3) & ~3));   // [M]
+    __shared__ float redf[NW];
+    __shared__ double redd[NW];
+    __shared__ float opart[NW][64];
+    const f16 *q = (const f16 *)a.q + (int64_t)b * n + h * 64;
+    const f16 *Kb = (const f16 *)a.K + (int64_t)b * a.clip_stride + h * 64;
+    const f16 *Vb = (const f16 *)a.V + (int64_t)b * a.clip_stride + h * 64;
+    half8 qv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qv[i] = *(const half8 *)(q + 8 * i);
+    float mx = -INFINITY;
+    for (int j = tid; j < M; j += DA_THREADS) {
+        const f16 *kr = Kb + (int64_t)j * n;
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s = dot8(*(const half8 *)(kr + 8 * i), qv[i], s);
+        S[j] = s;
+        mx = fmaxf(mx, s);
+    }
+    mx = wave_max(mx);
+    if (lane == 0) redf[w] = mx;
+    __syncthreads();
+    mx = redf[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) mx = fmaxf(mx, redf[i]);
+    double sum = 0.0;
+    for (int j = tid; j < M; j += DA_THREADS) {
+        const uint32_t i = f2h_bits(S[j] - mx) & 0x7fffu;
+        const float p = (int)i < a.n_exp ? h2f_bits(a.exp_tab[i]) : 0.0f;
+        S[j] = p;
+        sum += (double)p;
+    }
+    sum = wave_sum(sum);
+    if (lane == 0) redd[w] = sum;
+    __syncthreads();
+    double tot = 0.0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) tot += redd[i];
+    const float inv = (float)(1.0 / tot);
+    for (int j = tid; j < M; j += DA_THREADS) P[j] = f2h_bits(S[j] * inv);
+    __syncthreads();
+    float o = 0.0f;
+    for (int j = w; j < M; j += NW) o = o + h2f_bits(P[j]) * (float)Vb[(int64_t)j * n + lane];
+    opart[w][lane] = o;
+    __syncthreads();
+    if (w == 0) {
+        float v = opart[0][lane];
+#pragma unroll
+        for (int i = 1; i < NW; ++i) v = v + opart[i][lane];
+        a.out[(int64_t)b * n + h * 64 + lane] = f2h_bits(v);
+    }
+}
+
+hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
+    const int Mmax = a.M_fixed > 0 ? a.M_fixed : 4096;
+    const size_t lds = (size_t)((Mmax + 3) & ~3) * 4 + (size_t)Mmax * 2 + 16;
+    hipError_t e = allow_lds(k_dec_attn, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_dec_attn, dim3(a.H, a.B), dim3(DA_THREADS), lds, s, a);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_dec_embed(DecEmbedArgs a) {
+    __shared__ int32_t tok[DG_MAXB];
+    const int pos = a.st->pos;
+    const int tid = threadIdx.x;
+    if (tid < a.B) {
+        int32_t t;
+        if (pos < a.feed_len) {
+            t = a.feed[tid * a.feed_stride + pos];
+        } else {
+            const unsigned long long key = a.amax[tid];
+            t = (int32_t)(0xffffffffu - (uint32_t)(key & 0xffffffffull));
+            a.tokens_out[tid * a.out_stride + (pos - a.feed_len)] = t;
+        }
+        // the previous step's argmax is consumed (or, while feeding, unused):
+        // clear it before this step's logits kernel accumulates into it
+        a.amax[tid] = 0ull;
+        tok[tid] = t;
+    }
+    __syncthreads();
+    if (a.record_only) return;
+    for (int i = tid; i < a.B * a.n; i += 256) {
+        const int bb = i / a.n, c = i - bb * a.n;
+        a.x[i] = h2f_bits(a.te[(int64_t)tok[bb] * a.n + c]) + a.pe[(int64_t)pos * a.n + c];
+    }
+}
+
+hipError_t launch_dec_embed(hipStream_t s, const DecEmbedArgs &a) {
+    hipLaunchKernelGGL(k_dec_embed, dim3(1), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace wmi

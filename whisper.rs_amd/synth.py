@@ -1,0 +1,254 @@
+"""Synthetic inputs for the Whisper hot path: ggml-v1 model files and 30 s clips.
+
+Real ggml checkpoints and jfk.wav are not available offline, so
+benchmarks and parity tests run on synthetic files with the real
+hyper-parameters.  The file format is the one the reference loader reads:
+
+  magic u32 0x67676d6c                                    /root/reference/src/main.rs:46, 368-371
+  11 x i32 hparams                                        main.rs:623-633
+  filters: i32 n_mel, i32 n_ff, f32[n_mel*n_ff]           main.rs:514-524
+  vocab:   i32 n, n x (u32 len, bytes)                    main.rs:430, 579-583
+  tensors: i32 n_dims, i32 name_len, i32 ftype, i32 ne[n_dims], name, data
+                                                          main.rs:1385-1400, 1423-1437
+
+Tensor set and storage dtypes follow WhisperModel::load (main.rs:947-1334):
+matrices and conv kernels are f16 when hparams.f16 == 1; biases, LayerNorm
+parameters, conv biases ([1, n]) and both positional embeddings are f32.
+
+Value recipe: 2-D+ weights N(0, 0.02) f16, biases N(0, 0.01),
+LN gains 1 + N(0, 0.02), encoder PE sinusoidal, decoder PE N(0, 0.01),
+Slaney filterbank, seed = crc32(tensor name).  Audio: SURVEY.md §8d formula,
+quantised to int16 and read back as s16/32768 (main.rs:1673-1679).
+"""
+from __future__ import annotations
+
+import os
+import struct
+import zlib
+
+import numpy as np
+
+GGML_MAGIC = 0x67676D6C
+SAMPLE_RATE = 16000
+N_FFT = 400
+HOP = 160
+
+# name -> (n_vocab, n_audio_ctx, n_state, n_head, n_layer, n_text_ctx, n_mels)
+MODEL_DIMS = {
+    "micro":    dict(n_vocab=51864, n_audio_ctx=1500, n_audio_state=128,  n_audio_head=2,  n_audio_layer=2,
+                     n_text_ctx=448, n_text_state=128,  n_text_head=2,  n_text_layer=2,  n_mels=80),
+    "tiny.en":  dict(n_vocab=51864, n_audio_ctx=1500, n_audio_state=384,  n_audio_head=6,  n_audio_layer=4,
+                     n_text_ctx=448, n_text_state=384,  n_text_head=6,  n_text_layer=4,  n_mels=80),
+    "tiny":     dict(n_vocab=51865, n_audio_ctx=1500, n_audio_state=384,  n_audio_head=6,  n_audio_layer=4,
+                     n_text_ctx=448, n_text_state=384,  n_text_head=6,  n_text_layer=4,  n_mels=80),
+    "base":     dict(n_vocab=51865, n_audio_ctx=1500, n_audio_state=512,  n_audio_head=8,  n_audio_layer=6,
+                     n_text_ctx=448, n_text_state=512,  n_text_head=8,  n_text_layer=6,  n_mels=80),
+    "small":    dict(n_vocab=51865, n_audio_ctx=1500, n_audio_state=768,  n_audio_head=12, n_audio_layer=12,
+                     n_text_ctx=448, n_text_state=768,  n_text_head=12, n_text_layer=12, n_mels=80),
+    "medium":   dict(n_vocab=51865, n_audio_ctx=1500, n_audio_state=1024, n_audio_head=16, n_audio_layer=24,
+                     n_text_ctx=448, n_text_state=1024, n_text_head=16, n_text_layer=24, n_mels=80),
+    "large-v3": dict(n_vocab=51866, n_audio_ctx=1500, n_audio_state=1280, n_audio_head=20, n_audio_layer=32,
+                     n_text_ctx=448, n_text_state=1280, n_text_head=20, n_text_layer=32, n_mels=128),
+}
+
+HPARAM_ORDER = ("n_vocab", "n_audio_ctx", "n_audio_state", "n_audio_head", "n_audio_layer",
+                "n_text_ctx", "n_text_state", "n_text_head", "n_text_layer", "n_mels", "f16")
+
+
+# ----------------------------------------------------------------------------
+# Slaney mel filterbank (librosa.filters.mel(htk=False, norm="slaney") algorithm)
+# ----------------------------------------------------------------------------
+def _hz_to_mel(f):
+    f = np.asarray(f, dtype=np.float64)
+    f_sp = 200.0 / 3
+    mels = f / f_sp
+    min_log_hz = 1000.0
+    min_log_mel = min_log_hz / f_sp
+    logstep = np.log(6.4) / 27.0
+    return np.where(f >= min_log_hz, min_log_mel + np.log(np.maximum(f, 1e-10) / min_log_hz) / logstep, mels)
+
+
+def _mel_to_hz(m):
+    m = np.asarray(m, dtype=np.float64)
+    f_sp = 200.0 / 3
+    freqs = f_sp * m
+    min_log_hz = 1000.0
+    min_log_mel = min_log_hz / f_sp
+    logstep = np.log(6.4) / 27.0
+    return np.where(m >= min_log_mel, min_log_hz * np.exp(logstep * (m - min_log_mel)), freqs)
+
+
+def mel_filterbank(n_mels: int, n_fft: int = N_FFT, sr: int = SAMPLE_RATE) -> np.ndarray:
+    """[n_mels][1 + n_fft/2] float32, row-major as WhisperFilters::load reads it (main.rs:513-535)."""
+    n_freq = 1 + n_fft // 2
+    fftfreqs = np.linspace(0, sr / 2, n_freq)
+    mel_f = _mel_to_hz(np.linspace(_hz_to_mel(0.0), _hz_to_mel(sr / 2.0), n_mels + 2))
+    fdiff = np.diff(mel_f)
+    ramps = np.subtract.outer(mel_f, fftfreqs)
+    w = np.zeros((n_mels, n_freq), dtype=np.float64)
+    for i in range(n_mels):
+        lower = -ramps[i] / fdiff[i]
+        upper = ramps[i + 2] / fdiff[i + 1]
+        w[i] = np.maximum(0, np.minimum(lower, upper))
+    enorm = 2.0 / (mel_f[2:n_mels + 2] - mel_f[:n_mels])
+    w *= enorm[:, None]
+    return w.astype(np.float32)
+
+
+def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> np.ndarray:
+    """Whisper encoder positional embedding, [length][channels] float32."""
+    inc = np.log(max_timescale) / (channels // 2 - 1)
+    inv = np.exp(-inc * np.arange(channels // 2))
+    t = np.arange(length)[:, None] * inv[None, :]
+    return np.concatenate([np.sin(t), np.cos(t)], axis=1).astype(np.float32)
+
+
+# ----------------------------------------------------------------------------
+# tensor list (same names/shapes as WhisperModel::load, main.rs:947-1334)
+# ----------------------------------------------------------------------------
+def tensor_specs(hp: dict):
+    """Yield (name, torch_shape, kind) with kind in {w, b, g, lnb, epe, dpe}.
+
+    torch_shape is row-major (outermost first); the file stores ne reversed.
+    """
+    n = hp["n_audio_state"]
+    nt = hp["n_text_state"]
+    yield "encoder.positional_embedding", (hp["n_audio_ctx"], n), "epe"
+    yield "encoder.conv1.weight", (n, hp["n_mels"], 3), "w"
+    yield "encoder.conv1.bias", (n, 1), "b"
+    yield "encoder.conv2.weight", (n, n, 3), "w"
+    yield "encoder.conv2.bias", (n, 1), "b"
+    for i in range(hp["n_audio_layer"]):
+        p = f"encoder.blocks.{i}."
+        yield p + "attn_ln.weight", (n,), "g"
+        yield p + "attn_ln.bias", (n,), "lnb"
+        yield p + "attn.query.weight", (n, n), "w"
+        yield p + "attn.query.bias", (n,), "b"
+        yield p + "attn.key.weight", (n, n), "w"
+        yield p + "attn.value.weight", (n, n), "w"
+        yield p + "attn.value.bias", (n,), "b"
+        yield p + "attn.out.weight", (n, n), "w"
+        yield p + "attn.out.bias", (n,), "b"
+        yield p + "mlp_ln.weight", (n,), "g"
+        yield p + "mlp_ln.bias", (n,), "lnb"
+        yield p + "mlp.0.weight", (4 * n, n), "w"
+        yield p + "mlp.0.bias", (4 * n,), "b"
+        yield p + "mlp.2.weight", (n, 4 * n), "w"
+        yield p + "mlp.2.bias", (n,), "b"
+    yield "encoder.ln_post.weight", (n,), "g"
+    yield "encoder.ln_post.bias", (n,), "lnb"
+    yield "decoder.positional_embedding", (hp["n_text_ctx"], nt), "dpe"
+    yield "decoder.token_embedding.weight", (hp["n_vocab"], nt), "w"
+    for i in range(hp["n_text_layer"]):
+        p = f"decoder.blocks.{i}."
+        for a in ("attn", "cross_attn"):
+            yield p + f"{a}_ln.weight", (nt,), "g"
+            yield p + f"{a}_ln.bias", (nt,), "lnb"
+            yield p + f"{a}.query.weight", (nt, nt), "w"
+            yield p + f"{a}.query.bias", (nt,), "b"
+            yield p + f"{a}.key.weight", (nt, nt), "w"
+            yield p + f"{a}.value.weight", (nt, nt), "w"
+            yield p + f"{a}.value.bias", (nt,), "b"
+            yield p + f"{a}.out.weight", (nt, nt), "w"
+            yield p + f"{a}.out.bias", (nt,), "b"
+        yield p + "mlp_ln.weight", (nt,), "g"
+        yield p + "mlp_ln.bias", (nt,), "lnb"
+        yield p + "mlp.0.weight", (4 * nt, nt), "w"
+        yield p + "mlp.0.bias", (4 * nt,), "b"
+        yield p + "mlp.2.weight", (nt, 4 * nt), "w"
+        yield p + "mlp.2.bias", (nt,), "b"
+    yield "decoder.ln.weight", (nt,), "g"
+    yield "decoder.ln.bias", (nt,), "lnb"
+
+
+def tensor_value(name: str, shape, kind: str, hp: dict, wscale: float = 0.02) -> np.ndarray:
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    if kind == "w":
+        return (rng.standard_normal(shape, dtype=np.float32) * wscale).astype(np.float16)
+    if kind in ("b", "lnb"):
+        return (rng.standard_normal(shape, dtype=np.float32) * 0.01).astype(np.float32)
+    if kind == "g":
+        return (1.0 + rng.standard_normal(shape, dtype=np.float32) * 0.02).astype(np.float32)
+    if kind == "epe":
+        return sinusoids(shape[0], shape[1])
+    if kind == "dpe":
+        return (rng.standard_normal(shape, dtype=np.float32) * 0.01).astype(np.float32)
+    raise ValueError(kind)
+
+
+def _vocab_tokens(n: int):
+    for i in range(n):
+        yield (f" w{i}" if i < 50256 else f"<|special{i}|>").encode()
+
+
+def write_ggml(path: str, model: str = "base", hp_override: dict | None = None,
+               wscale: float = 0.02, n_vocab_file: int | None = None) -> dict:
+    """Write a synthetic ggml-v1 Whisper file; returns the hparams used."""
+    hp = dict(MODEL_DIMS[model])
+    hp["f16"] = 1
+    if hp_override:
+        hp.update(hp_override)
+    n_vocab_file = 50257 if n_vocab_file is None else n_vocab_file
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, "wb") as f:
+        f.write(struct.pack("<I", GGML_MAGIC))
+        f.write(struct.pack("<11i", *[hp[k] for k in HPARAM_ORDER]))
+        filt = mel_filterbank(hp["n_mels"])
+        f.write(struct.pack("<ii", filt.shape[0], filt.shape[1]))
+        f.write(filt.astype("<f4").tobytes())
+        f.write(struct.pack("<i", n_vocab_file))
+        for tok in _vocab_tokens(n_vocab_file):
+            f.write(struct.pack("<I", len(tok)))
+            f.write(tok)
+        for name, shape, kind in tensor_specs(hp):
+            arr = tensor_value(name, shape, kind, hp, wscale)
+            ftype = 1 if arr.dtype == np.float16 else 0
+            ne = tuple(reversed(shape))
+            nb = name.encode()
+            f.write(struct.pack("<iii", len(ne), len(nb), ftype))
+            f.write(struct.pack(f"<{len(ne)}i", *ne))
+            f.write(nb)
+            f.write(arr.astype("<f2" if ftype else "<f4").tobytes())
+    os.replace(tmp, path)
+    return hp
+
+
+def model_path(model: str, cache_dir: str | None = None) -> str:
+    """Generate (once) and return the path of a synthetic model file."""
+    cache_dir = cache_dir or os.environ.get("WMI_MODEL_CACHE", "/tmp/wmi_models")
+    os.makedirs(cache_dir, exist_ok=True)
+    p = os.path.join(cache_dir, f"ggml-synth-{model}.bin")
+    if not os.path.exists(p):
+        write_ggml(p, model)
+    return p
+
+
+# ----------------------------------------------------------------------------
+# synthetic audio
+# ----------------------------------------------------------------------------
+def synth_pcm_i16(seconds: float = 30.0, seed: int = 1234) -> np.ndarray:
+    n = int(round(seconds * SAMPLE_RATE))
+    t = np.arange(n, dtype=np.float64)
+    rng = np.random.default_rng(seed)
+    x = (0.4 * np.sin(2 * np.pi * 220 * t / SAMPLE_RATE) * (0.6 + 0.4 * np.sin(2 * np.pi * 0.5 * t / SAMPLE_RATE))
+         + 0.2 * np.sin(2 * np.pi * 1330 * t / SAMPLE_RATE) + 0.05 * rng.standard_normal(n))
+    x = np.clip(x, -1.0, 1.0)
+    return np.round(x * 32767).astype(np.int16)
+
+
+def pcm_i16_to_f32(s16: np.ndarray) -> np.ndarray:
+    """convert_integer_to_float_audio (main.rs:1673-1679): s / 32768.0 in f32."""
+    return (s16.astype(np.float32) / np.float32(32768.0)).astype(np.float32)
+
+
+def synth_pcm_f32(seconds: float = 30.0, seed: int = 1234) -> np.ndarray:
+    return pcm_i16_to_f32(synth_pcm_i16(seconds, seed))
+
+
+def write_wav(path: str, s16: np.ndarray, sr: int = SAMPLE_RATE) -> None:
+    """16-bit mono PCM WAV (what hound reads in main.rs:2067-2068)."""
+    data = s16.astype("<i2").tobytes()
+    with open(path, "wb") as f:
+        f.write(b"RIFF" + struct.pack("<I", 36 + len(data)) + b"WAVE")
+        f.write(b"fmt " + struct.pack("<IHHIIHH", 16, 1, 1, sr, sr * 2, 2, 16))
+        f.write(b"data" + struct.pack("<I", len(data)) + data)

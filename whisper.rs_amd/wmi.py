@@ -1,0 +1,312 @@
+"""Python mirror of the reference's pipeline interface over the C ABI.
+
+The reference (szuwgh/whisper.rs, src/main.rs) exposes
+
+    WhisperContext::new(fname) -> WsResult<WhisperContext>          main.rs:366
+    whisper_pcm_to_mel(&mut ctx, samples: Arc<Vec<f32>>)            main.rs:1681
+    whisper_encode(&mut ctx, n_threads, mel_offset)                 main.rs:1799
+    convert_integer_to_float_audio(&[i16]) -> Vec<f32>              main.rs:1673
+    WsError (BadMagic, UnknownTensor, WrongSizeTensor, ...)         main.rs:51-72
+
+This module keeps those names, argument meanings and error behaviour, and
+binds them with ctypes to libwhisper_mi355x.so (include/whisper_mi355x.h),
+whose work runs in hand-written gfx950 kernels.  There is no CPU fallback:
+if the shared library or a HIP device is missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libwhisper_mi355x.so")
+
+WMI_OK = 0
+
+
+class WsError(RuntimeError):
+    """WsError (main.rs:51-72); `code` is the wmi_status value."""
+    code = -1
+
+    def __init__(self, msg: str = "", code: int | None = None):
+        super().__init__(msg)
+        if code is not None:
+            self.code = code
+
+
+class UnexpectIO(WsError): code = 1
+class BadMagic(WsError): code = 2
+class NotEnoughSpace(WsError): code = 3
+class UnknownTensor(WsError): code = 4
+class BadRefTensor(WsError): code = 5
+class WrongSizeTensor(WsError): code = 6
+class WrongShapeTensor(WsError): code = 7
+class WrongBytesTensor(WsError): code = 8
+class WrongGTensor(WsError): code = 9
+class Unexpected(WsError): code = 10
+class HipError(WsError): code = 11
+class RcclError(WsError): code = 12
+class Unsupported(WsError): code = 13
+class InvalidArgument(WsError): code = 14
+
+
+_ERRORS = {c.code: c for c in (UnexpectIO, BadMagic, NotEnoughSpace, UnknownTensor, BadRefTensor, WrongSizeTensor,
+                               WrongShapeTensor, WrongBytesTensor, WrongGTensor, Unexpected, HipError, RcclError,
+                               Unsupported, InvalidArgument)}
+
+# exported symbols of include/whisper_mi355x.h
+EXPORTS = (
+    "wmi_init_from_file", "wmi_free", "wmi_strerror", "wmi_last_error", "wmi_last_error_global",
+    "wmi_get_hparams", "wmi_get_special_tokens", "wmi_set_audio_ctx", "wmi_token_to_bytes",
+    "wmi_pcm_to_mel", "wmi_pcm_to_mel_batch", "wmi_encode", "wmi_decode_greedy", "wmi_decode_logits", "wmi_full",
+    "wmi_stage_pcm", "wmi_run_staged", "wmi_get_tokens", "wmi_get_timings", "wmi_sync",
+    "wmi_get_mel", "wmi_get_encoder_out", "wmi_get_cross_kv",
+    "wmi_dist_id_size", "wmi_dist_make_id", "wmi_dist_init", "wmi_dist_gather_tokens", "wmi_dist_barrier",
+)
+
+
+class Hparams(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("n_vocab", "n_audio_ctx", "n_audio_state", "n_audio_head", "n_audio_layer",
+                                         "n_text_ctx", "n_text_state", "n_text_head", "n_text_layer", "n_mels", "f16")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class SpecialTokens(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("eot", "sot", "prev", "solm", "not_", "beg", "translate", "transcribe",
+                                         "is_multilingual")]
+
+
+class Timings(C.Structure):
+    _fields_ = [("mel_ms", C.c_float), ("encode_ms", C.c_float), ("cross_kv_ms", C.c_float),
+                ("decode_ms", C.c_float), ("n_decode_steps", C.c_int32)]
+
+
+_lib = None
+
+
+def lib():
+    """Load the HIP library (fails loudly: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} not built: run __graft_entry__.build() (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        vp, i32, sz = C.c_void_p, C.c_int32, C.c_size_t
+        L.wmi_init_from_file.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(vp)]
+        L.wmi_free.argtypes = [vp]
+        L.wmi_free.restype = None
+        L.wmi_strerror.restype = C.c_char_p
+        L.wmi_last_error.argtypes = [vp]
+        L.wmi_last_error.restype = C.c_char_p
+        L.wmi_last_error_global.restype = C.c_char_p
+        L.wmi_get_hparams.argtypes = [vp, C.POINTER(Hparams)]
+        L.wmi_get_special_tokens.argtypes = [vp, C.POINTER(SpecialTokens)]
+        L.wmi_set_audio_ctx.argtypes = [vp, C.c_int]
+        L.wmi_token_to_bytes.argtypes = [vp, i32, C.c_char_p, sz, C.POINTER(sz)]
+        L.wmi_pcm_to_mel.argtypes = [vp, vp, sz]
+        L.wmi_pcm_to_mel_batch.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(sz)]
+        L.wmi_stage_pcm.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(sz)]
+        L.wmi_encode.argtypes = [vp, C.c_int, C.c_int]
+        L.wmi_decode_greedy.argtypes = [vp, C.c_int, C.c_int, vp, vp]
+        L.wmi_decode_logits.argtypes = [vp, C.c_int, vp, C.c_int, vp]
+        L.wmi_full.argtypes = [vp, vp, sz, C.c_int, vp, vp]
+        L.wmi_run_staged.argtypes = [vp, C.c_int, C.c_int]
+        L.wmi_get_tokens.argtypes = [vp, vp, sz, vp]
+        L.wmi_get_timings.argtypes = [vp, C.POINTER(Timings)]
+        L.wmi_sync.argtypes = [vp]
+        L.wmi_get_mel.argtypes = [vp, C.c_int, vp, sz, C.POINTER(i32), C.POINTER(i32)]
+        L.wmi_get_encoder_out.argtypes = [vp, C.c_int, vp, sz]
+        L.wmi_get_cross_kv.argtypes = [vp, C.c_int, vp, vp, sz]
+        L.wmi_dist_id_size.restype = sz
+        L.wmi_dist_make_id.argtypes = [vp]
+        L.wmi_dist_init.argtypes = [vp, C.c_int, C.c_int, vp]
+        L.wmi_dist_gather_tokens.argtypes = [vp, vp, sz]
+        L.wmi_dist_barrier.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+def _raise(rc: int, ctx=None):
+    if rc == WMI_OK:
+        return
+    L = lib()
+    msg = (L.wmi_last_error(ctx) if ctx else L.wmi_last_error_global()) or b""
+    cls = _ERRORS.get(rc, WsError)
+    raise cls(f"{L.wmi_strerror(rc).decode()}: {msg.decode(errors='replace')}", rc)
+
+
+def convert_integer_to_float_audio(samples) -> np.ndarray:
+    """main.rs:1673-1679: s16 -> f32 / 32768.0."""
+    return (np.asarray(samples, dtype=np.int16).astype(np.float32) / np.float32(32768.0)).astype(np.float32)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class WhisperContext:
+    """WhisperContext (main.rs:333-363), device-resident."""
+
+    def __init__(self, handle, device: int, max_clips: int):
+        self._h = handle
+        self.device = device
+        self.max_clips = max_clips
+        hp = Hparams()
+        _raise(lib().wmi_get_hparams(self._h, C.byref(hp)), self._h)
+        self.hparams = hp.as_dict()
+        sp = SpecialTokens()
+        _raise(lib().wmi_get_special_tokens(self._h, C.byref(sp)), self._h)
+        self.special = {"eot": sp.eot, "sot": sp.sot, "prev": sp.prev, "solm": sp.solm, "not": sp.not_,
+                        "beg": sp.beg, "translate": sp.translate, "transcribe": sp.transcribe,
+                        "multilingual": sp.is_multilingual}
+        self.n_clips = 0
+        self.n_ctx = self.hparams["n_audio_ctx"]
+
+    @classmethod
+    def new(cls, fname: str, device: int = 0, max_clips: int = 1) -> "WhisperContext":
+        """WhisperContext::new (main.rs:366-503); raises the WsError variant."""
+        h = C.c_void_p()
+        rc = lib().wmi_init_from_file(os.fsencode(fname), device, max_clips, C.byref(h))
+        _raise(rc)
+        return cls(h, device, max_clips)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().wmi_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # --- knobs -------------------------------------------------------------
+    def set_audio_ctx(self, n: int) -> None:
+        """exp_n_audio_ctx (main.rs:362, 1803-1807); 0 restores n_audio_ctx."""
+        _raise(lib().wmi_set_audio_ctx(self._h, n), self._h)
+        self.n_ctx = n or self.hparams["n_audio_ctx"]
+
+    def token_to_str(self, tid: int) -> bytes:
+        """id_to_token (main.rs:578-592, 442-467)."""
+        n = C.c_size_t()
+        buf = C.create_string_buffer(512)
+        _raise(lib().wmi_token_to_bytes(self._h, tid, buf, 512, C.byref(n)), self._h)
+        return buf.raw[:n.value]
+
+    # --- pipeline ---------------------------------------------------------
+    def pcm_to_mel_batch(self, clips) -> None:
+        clips = [np.ascontiguousarray(c, dtype=np.float32) for c in clips]
+        ptrs = (C.c_void_p * len(clips))(*[c.ctypes.data for c in clips])
+        ns = (C.c_size_t * len(clips))(*[c.size for c in clips])
+        _raise(lib().wmi_pcm_to_mel_batch(self._h, len(clips), ptrs, ns), self._h)
+        self.n_clips = len(clips)
+
+    def encode(self, n_threads: int = 1, mel_offset: int = 0) -> None:
+        _raise(lib().wmi_encode(self._h, n_threads, mel_offset), self._h)
+
+    def decode_greedy(self, max_tokens: int, suppress_eot: bool = False):
+        toks = np.zeros((self.n_clips, max_tokens), np.int32)
+        cnt = np.zeros(self.n_clips, np.int32)
+        _raise(lib().wmi_decode_greedy(self._h, max_tokens, int(suppress_eot), _ptr(toks), _ptr(cnt)), self._h)
+        return [toks[i, :cnt[i]].copy() for i in range(self.n_clips)]
+
+    def decode_logits(self, tokens, clip: int = 0) -> np.ndarray:
+        tokens = np.ascontiguousarray(tokens, dtype=np.int32)
+        out = np.zeros((tokens.size, self.hparams["n_vocab"]), np.float32)
+        _raise(lib().wmi_decode_logits(self._h, clip, _ptr(tokens), tokens.size, _ptr(out)), self._h)
+        return out
+
+    def full(self, pcm, max_tokens: int = 224) -> np.ndarray:
+        """Transcribe: pcm_to_mel -> encode -> greedy decode (token ids)."""
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        toks = np.zeros(max_tokens, np.int32)
+        cnt = np.zeros(1, np.int32)
+        _raise(lib().wmi_full(self._h, _ptr(pcm), pcm.size, max_tokens, _ptr(toks), _ptr(cnt)), self._h)
+        self.n_clips = 1
+        return toks[:cnt[0]].copy()
+
+    def stage(self, clips) -> None:
+        clips = [np.ascontiguousarray(c, dtype=np.float32) for c in clips]
+        ptrs = (C.c_void_p * len(clips))(*[c.ctypes.data for c in clips])
+        ns = (C.c_size_t * len(clips))(*[c.size for c in clips])
+        _raise(lib().wmi_stage_pcm(self._h, len(clips), ptrs, ns), self._h)
+        self.n_clips = len(clips)
+
+    def run_staged(self, n_decode: int = 128, mel_offset: int = 0) -> None:
+        _raise(lib().wmi_run_staged(self._h, mel_offset, n_decode), self._h)
+        self._n_decode = n_decode
+
+    def tokens(self) -> np.ndarray:
+        out = np.zeros((self.n_clips, self._n_decode), np.int32)
+        _raise(lib().wmi_get_tokens(self._h, _ptr(out), out.size, None), self._h)
+        return out
+
+    def timings(self) -> dict:
+        t = Timings()
+        _raise(lib().wmi_get_timings(self._h, C.byref(t)), self._h)
+        return {"mel_ms": t.mel_ms, "encode_ms": t.encode_ms, "cross_kv_ms": t.cross_kv_ms,
+                "decode_ms": t.decode_ms, "n_decode_steps": t.n_decode_steps}
+
+    # --- parity getters -----------------------------------------------------
+    def mel(self, clip: int = 0) -> np.ndarray:
+        nm, nl = C.c_int32(), C.c_int32()
+        _raise(lib().wmi_get_mel(self._h, clip, None, 0, C.byref(nm), C.byref(nl)), self._h)
+        out = np.zeros((nm.value, nl.value), np.float32)
+        _raise(lib().wmi_get_mel(self._h, clip, _ptr(out), out.size, C.byref(nm), C.byref(nl)), self._h)
+        return out
+
+    def encoder_out(self, clip: int = 0) -> np.ndarray:
+        out = np.zeros((self.n_ctx, self.hparams["n_audio_state"]), np.float32)
+        _raise(lib().wmi_get_encoder_out(self._h, clip, _ptr(out), out.size), self._h)
+        return out
+
+    def cross_kv(self, clip: int = 0):
+        shp = (self.hparams["n_text_layer"], self.n_ctx, self.hparams["n_text_state"])
+        k = np.zeros(shp, np.uint16)
+        v = np.zeros(shp, np.uint16)
+        _raise(lib().wmi_get_cross_kv(self._h, clip, _ptr(k), _ptr(v), k.size), self._h)
+        return k, v
+
+    # --- multi-GPU ----------------------------------------------------------
+    @staticmethod
+    def dist_make_id() -> bytes:
+        n = lib().wmi_dist_id_size()
+        buf = C.create_string_buffer(n)
+        _raise(lib().wmi_dist_make_id(buf))
+        return buf.raw
+
+    def dist_init(self, rank: int, world: int, uid: bytes) -> None:
+        buf = C.create_string_buffer(uid, len(uid))
+        _raise(lib().wmi_dist_init(self._h, rank, world, buf), self._h)
+        self.rank, self.world = rank, world
+
+    def dist_gather_tokens(self):
+        total = self.world * self.n_clips * self._n_decode
+        out = np.zeros(total, np.int32) if self.rank == 0 else None
+        _raise(lib().wmi_dist_gather_tokens(self._h, _ptr(out) if out is not None else None, total), self._h)
+        return None if out is None else out.reshape(self.world, self.n_clips, self._n_decode)
+
+    def dist_barrier(self) -> None:
+        _raise(lib().wmi_dist_barrier(self._h), self._h)
+
+
+# reference-named free functions -----------------------------------------------
+def whisper_pcm_to_mel(ctx: WhisperContext, samples) -> None:
+    """main.rs:1681-1707."""
+    ctx.pcm_to_mel_batch([samples])
+
+
+def whisper_encode(ctx: WhisperContext, n_threads: int, mel_offset: int) -> None:
+    """main.rs:1799-2063 (n_threads accepted and ignored, as in the reference)."""
+    ctx.encode(n_threads, mel_offset)
