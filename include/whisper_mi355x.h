@@ -144,6 +144,18 @@ int wmi_get_timings(const wmi_context *ctx, wmi_timings *out);
 /* Block until all work queued on the context's stream is done. */
 int wmi_sync(wmi_context *ctx);
 
+/* Re-launch one kernel of the last pipeline call `iters` times between HIP
+ * events on the context stream (bench.py's live roofline measurement).
+ * which: 0 = decoder logits GEMV + argmax (HBM-bound), 1 = encoder MLP-up
+ * GEMM of layer 0 (MFMA), 2 = encoder attention of layer 0, 3 = cross-K/V GEMM. */
+typedef struct wmi_kernel_bench {
+    float avg_us;          /* mean launch duration */
+    double alg_bytes;      /* algorithmic HBM bytes per launch */
+    double alg_flops;      /* algorithmic FLOPs per launch */
+    char name[48];
+} wmi_kernel_bench;
+int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *out);
+
 /* ---- parity getters (copy device results into caller-owned buffers) --- */
 
 /* ctx.mel (main.rs:1574-1578): [n_mel][n_len] f32. */

@@ -175,6 +175,8 @@ struct wmi_context {
     // decoder small state
     float *dx = nullptr, *dlogits = nullptr;
     uint16_t *dq16 = nullptr, *datt16 = nullptr, *dhid16 = nullptr;
+    float *dS = nullptr, *dcmax = nullptr, *dopart = nullptr;
+    int s_stride = 0, n_chunks_max = 0;
     unsigned long long *damax = nullptr;
     DecState *dstate = nullptr;
     int32_t *dfeed = nullptr;
@@ -648,7 +650,12 @@ int alloc_workspace(wmi_context *ctx) {
     const size_t o_datt = A.take(B * nt * 2);
     const size_t o_dhid = A.take(B * 4 * nt * 2);
     const size_t o_dlog = A.take(B * (int64_t)hp.n_vocab * 4);
-    const size_t o_amax = A.take(B * 8);
+    const int64_t Smax = up(hp.n_audio_ctx > hp.n_text_ctx ? hp.n_audio_ctx : hp.n_text_ctx, 128);
+    const int64_t Cmax = Smax / 128, Hd = hp.n_text_head, Bd = B < 8 ? B : 8;
+    const size_t o_S = A.take(Bd * Hd * Smax * 4);
+    const size_t o_cmax = A.take(Bd * Hd * Cmax * 4);
+    const size_t o_opart = A.take(Bd * Cmax * nt * 4);
+    const size_t o_amax = A.take(8 * AMAX_SHARDS * 8);
     const size_t o_st = A.take(sizeof(DecState));
     const size_t o_ptrs = A.take(B * sizeof(float *));
     const size_t o_ns = A.take(B * 8);
@@ -678,6 +685,11 @@ int alloc_workspace(wmi_context *ctx) {
     ctx->datt16 = (uint16_t *)(b + o_datt);
     ctx->dhid16 = (uint16_t *)(b + o_dhid);
     ctx->dlogits = (float *)(b + o_dlog);
+    ctx->dS = (float *)(b + o_S);
+    ctx->dcmax = (float *)(b + o_cmax);
+    ctx->dopart = (float *)(b + o_opart);
+    ctx->s_stride = (int)Smax;
+    ctx->n_chunks_max = (int)Cmax;
     ctx->damax = (unsigned long long *)(b + o_amax);
     ctx->dstate = (DecState *)(b + o_st);
     ctx->d_pcm_ptrs = (float **)(b + o_ptrs);
@@ -753,6 +765,8 @@ int run_encode(wmi_context *ctx, int mel_offset) {
     if (B < 1) return set_err(ctx, WMI_E_INVALID_ARG, "encode before pcm_to_mel");
     if (mel_offset < 0) return set_err(ctx, WMI_E_INVALID_ARG, "negative mel_offset");
     if (nt != n) return set_err(ctx, WMI_E_UNSUPPORTED, "n_text_state != n_audio_state");
+    if (hp.n_text_ctx > 512) return set_err(ctx, WMI_E_UNSUPPORTED, "n_text_ctx %d > 512", hp.n_text_ctx);
+    if (n > 1280 || n % 128) return set_err(ctx, WMI_E_UNSUPPORTED, "n_state %d (need a multiple of 128, <= 1280)", n);
     if (n / H != 64) return set_err(ctx, WMI_E_UNSUPPORTED, "head dim %d != 64", n / H);
     hipStream_t s = ctx->stream;
     if (ctx->layout_T != T) {
@@ -827,11 +841,8 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     const int n = hp.n_text_state, H = hp.n_text_head, T = ctx->enc_T, Bt = ctx->enc_clips;
     hipStream_t s = ctx->stream;
     const float qs = powf((float)n / (float)H, -0.25f);
-    DecEmbedArgs em{};
-    em.te = ctx->te; em.pe = ctx->d_pe; em.x = ctx->dx; em.feed = ctx->dfeed; em.feed_len = feed_len;
-    em.feed_stride = feed_stride; em.amax = ctx->damax; em.tokens_out = ctx->dtokens + (size_t)b0 * out_stride;
-    em.out_stride = out_stride; em.st = ctx->dstate; em.n = n; em.B = B; em.record_only = 0;
-    HIPCHK(ctx, launch_dec_embed(s, em));
+    // per layer: [LN+QKV (+embed at l=0)] [self-attn] [Wo+res] [LN+Wcq+cross scores]
+    //            [cross softmax+PV] [Wco+res] [LN+W0+GELU] [W1+res]; then LN+logits+argmax
     for (int l = 0; l < hp.n_text_layer; ++l) {
         const DecLayerDev &d = ctx->dec[l];
         uint16_t *kc = ctx->kcache + (size_t)l * ctx->max_clips * hp.n_text_ctx * n;
@@ -840,28 +851,35 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         g.x = ctx->dx; g.ln_w = d.ln1_w; g.ln_b = d.ln1_b; g.W = d.wqkv; g.bias = d.bqkv; g.N = 3 * n; g.K = n; g.B = B;
         g.qscale = qs; g.out16 = ctx->dq16; g.ldo = n; g.kcache = kc; g.vcache = vc; g.n_text_ctx = hp.n_text_ctx;
         g.st = ctx->dstate;
+        if (l == 0) {
+            g.te = ctx->te; g.pe = ctx->d_pe; g.feed = ctx->dfeed; g.feed_len = feed_len; g.feed_stride = feed_stride;
+            g.amax = ctx->damax; g.tokens_out = ctx->dtokens + (size_t)b0 * out_stride; g.out_stride = out_stride;
+            g.x_out = ctx->dx;
+        }
         HIPCHK(ctx, launch_dec_gemv(s, DEC_QKV, g));
         DecAttnArgs at{};
         at.q = ctx->dq16; at.K = kc; at.V = vc; at.clip_stride = (int64_t)hp.n_text_ctx * n; at.M_fixed = 0;
-        at.st = ctx->dstate; at.out = ctx->datt16; at.exp_tab = ctx->exp_tab; at.n_exp = ctx->n_exp; at.H = H; at.n = n;
-        at.B = B;
+        at.st = ctx->dstate; at.S = ctx->dS; at.s_stride = ctx->s_stride; at.cmax = ctx->dcmax;
+        at.opart = ctx->dopart; at.n_chunks = 1; at.exp_tab = ctx->exp_tab; at.n_exp = ctx->n_exp;
+        at.H = H; at.n = n; at.B = B;
+        at.reset_amax = l == 0 ? ctx->damax : nullptr;
         HIPCHK(ctx, launch_dec_attn(s, at));
         g = DecGemvArgs{};
-        g.xin16 = ctx->datt16; g.W = d.wo; g.bias = d.bo; g.N = n; g.K = n; g.B = B; g.out32 = ctx->dx;
+        g.parts = ctx->dopart; g.n_parts = 1; g.W = d.wo; g.bias = d.bo; g.N = n; g.K = n; g.B = B;
+        g.out32 = ctx->dx;
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
-        g = DecGemvArgs{};
-        g.x = ctx->dx; g.ln_w = d.lnc_w; g.ln_b = d.lnc_b; g.W = d.wcq; g.bias = d.bcq; g.N = n; g.K = n; g.B = B;
-        g.qscale = qs; g.out16 = ctx->dq16; g.ldo = n;
-        HIPCHK(ctx, launch_dec_gemv(s, DEC_Q, g));
+        const int c_cross = (T + 127) / 128;
         at = DecAttnArgs{};
-        at.q = ctx->dq16;
         at.K = ctx->ck + ((size_t)l * Bt + b0) * T * n;
         at.V = ctx->cv + ((size_t)l * Bt + b0) * T * n;
-        at.clip_stride = (int64_t)T * n; at.M_fixed = T; at.st = ctx->dstate; at.out = ctx->datt16;
-        at.exp_tab = ctx->exp_tab; at.n_exp = ctx->n_exp; at.H = H; at.n = n; at.B = B;
+        at.clip_stride = (int64_t)T * n; at.M_fixed = T; at.st = ctx->dstate;
+        at.S = ctx->dS; at.s_stride = ctx->s_stride; at.cmax = ctx->dcmax; at.opart = ctx->dopart;
+        at.n_chunks = c_cross; at.exp_tab = ctx->exp_tab; at.n_exp = ctx->n_exp; at.H = H; at.n = n; at.B = B;
+        at.x = ctx->dx; at.ln_w = d.lnc_w; at.ln_b = d.lnc_b; at.Wq = d.wcq; at.bq = d.bcq; at.qscale = qs;
         HIPCHK(ctx, launch_dec_attn(s, at));
         g = DecGemvArgs{};
-        g.xin16 = ctx->datt16; g.W = d.wco; g.bias = d.bco; g.N = n; g.K = n; g.B = B; g.out32 = ctx->dx;
+        g.parts = ctx->dopart; g.n_parts = c_cross; g.W = d.wco; g.bias = d.bco; g.N = n; g.K = n; g.B = B;
+        g.out32 = ctx->dx;
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
         g = DecGemvArgs{};
         g.x = ctx->dx; g.ln_w = d.ln2_w; g.ln_b = d.ln2_b; g.W = d.w0; g.bias = d.b0; g.N = 4 * n; g.K = n; g.B = B;
@@ -948,7 +966,7 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
     for (int b0 = 0; b0 < Bt; b0 += 8) {
         const int B = Bt - b0 < 8 ? Bt - b0 : 8;
         HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
-        HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * 8, ctx->stream));
+        HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * AMAX_SHARDS * 8, ctx->stream));
         const int total_steps = np + n_gen - 1;
         int done_steps = 0;
         while (done_steps < total_steps) {
@@ -1186,7 +1204,7 @@ int wmi_decode_logits(wmi_context *ctx, int clip, const int32_t *tokens, int n_t
     if (rc) return rc;
     HIPCHK(ctx, hipMemcpyAsync(ctx->dfeed, tokens, (size_t)n_tokens * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
-    HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * 8, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * AMAX_SHARDS * 8, ctx->stream));
     const size_t V = ctx->hp.n_vocab;
     for (int i = 0; i < n_tokens; ++i) {
         rc = run_dec_steps(ctx, clip, 1, n_tokens, n_tokens, 0, 1, 1);
@@ -1289,6 +1307,80 @@ int wmi_get_cross_kv(const wmi_context *ctx, int clip, uint16_t *k, uint16_t *v,
         const size_t off = ((size_t)l * ctx->enc_clips + clip) * per;
         if (hipMemcpy(k + l * per, ctx->ck + off, per * 2, hipMemcpyDeviceToHost) != hipSuccess) return WMI_E_HIP;
         if (hipMemcpy(v + l * per, ctx->cv + off, per * 2, hipMemcpyDeviceToHost) != hipSuccess) return WMI_E_HIP;
+    }
+    return WMI_OK;
+}
+
+int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *out) {
+    if (!valid(ctx) || !out || iters < 1) return WMI_E_INVALID_ARG;
+    if (ctx->enc_T <= 0) return set_err(ctx, WMI_E_INVALID_ARG, "bench_kernel before a pipeline run");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const wmi_hparams &hp = ctx->hp;
+    const int n = hp.n_audio_state, T = ctx->enc_T, B = ctx->enc_clips, M = B * T;
+    memset(out, 0, sizeof(*out));
+    hipStream_t s = ctx->stream;
+    auto launch = [&]() -> int {
+        if (which == 0) {
+            DecGemvArgs g{};
+            g.x = ctx->dx; g.ln_w = ctx->dln_w; g.ln_b = ctx->dln_b; g.W = ctx->te; g.N = hp.n_vocab;
+            g.K = hp.n_text_state; g.B = B < 8 ? B : 8;
+            g.out32 = ctx->dlogits; g.amax = ctx->damax; g.suppress_id = ctx->sp.eot; g.st_advance = ctx->dstate;
+            HIPCHK(ctx, launch_dec_gemv(s, DEC_LOGITS, g));
+        } else if (which == 1) {
+            GemmArgs g{};
+            const EncLayerDev &e = ctx->enc[0];
+            g.A = ctx->xln; g.lda = n; g.B = e.w0; g.bias = e.b0; g.M = M; g.N = 4 * n; g.K = n;
+            g.out16 = ctx->hid; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
+            HIPCHK(ctx, launch_gemm(s, EPI_GELU16, g));
+        } else if (which == 2) {
+            AttnArgs at{};
+            at.q = ctx->q; at.k = ctx->k; at.vt = ctx->vt; at.out = ctx->att; at.exp_tab = ctx->exp_tab;
+            at.n_exp = ctx->n_exp; at.T = T; at.Tp = (int)up(T, 64); at.H = hp.n_audio_head; at.n_state = n;
+            at.n_clips = B; at.scale = 0.125f;
+            HIPCHK(ctx, launch_attn_enc(s, at));
+        } else if (which == 3) {
+            GemmArgs g{};
+            g.A = ctx->enc16; g.lda = n; g.B = ctx->wckv; g.bias = ctx->bckv; g.M = M;
+            g.N = hp.n_text_layer * 2 * hp.n_text_state; g.K = n;
+            g.ck = ctx->ck; g.cv = ctx->cv; g.T = T; g.n_state = hp.n_text_state; g.n_clips = B;
+            g.kscale = powf((float)n / (float)hp.n_audio_head, -0.25f);
+            HIPCHK(ctx, launch_gemm(s, EPI_CROSSKV, g));
+        } else {
+            return set_err(ctx, WMI_E_INVALID_ARG, "unknown kernel %d", which);
+        }
+        return WMI_OK;
+    };
+    int rc = launch();  // warm
+    if (rc) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[6], s));
+    for (int i = 0; i < iters; ++i) {
+        rc = launch();
+        if (rc) return rc;
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev[7], s));
+    HIPCHK(ctx, hipEventSynchronize(ctx->ev[7]));
+    float ms = 0;
+    HIPCHK(ctx, hipEventElapsedTime(&ms, ctx->ev[6], ctx->ev[7]));
+    out->avg_us = ms * 1000.0f / iters;
+    const double nt = hp.n_text_state, V = hp.n_vocab;
+    if (which == 0) {
+        const double b = B < 8 ? B : 8;
+        out->alg_bytes = V * nt * 2 + b * nt * 4 + b * V * 4 + 2 * nt * 4;
+        out->alg_flops = 2.0 * V * nt * b;
+        snprintf(out->name, sizeof out->name, "k_dec_gemv<DEC_LOGITS,LN>");
+    } else if (which == 1) {
+        out->alg_flops = 2.0 * M * (4.0 * n) * n;
+        out->alg_bytes = (double)M * n * 2 + 4.0 * n * n * 2 + (double)M * 4 * n * 2;
+        snprintf(out->name, sizeof out->name, "k_gemm<EPI_GELU16> (mlp.0)");
+    } else if (which == 2) {
+        out->alg_flops = 4.0 * T * (double)T * n * B;
+        out->alg_bytes = 4.0 * (double)M * n * 2;
+        snprintf(out->name, sizeof out->name, "k_attn_enc");
+    } else {
+        const double N = hp.n_text_layer * 2.0 * nt;
+        out->alg_flops = 2.0 * M * N * n;
+        out->alg_bytes = (double)M * n * 2 + N * n * 2 + (double)M * N * 2;
+        snprintf(out->name, sizeof out->name, "k_gemm<EPI_CROSSKV>");
     }
     return WMI_OK;
 }

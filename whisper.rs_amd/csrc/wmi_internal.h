@@ -93,6 +93,8 @@ struct DecGemvArgs {
     const float *x;          // LN input [B][K] f32 (ln != null)
     const float *ln_w, *ln_b;
     const uint16_t *xin16;   // non-LN input [B][K] f16
+    const float *parts;      // or: split-key attention partials [B][n_parts][K] f32, summed in order
+    int n_parts;
     const uint16_t *W;       // [N][K]
     const float *bias;       // [N] (null for logits)
     int N, K, B;
@@ -105,21 +107,41 @@ struct DecGemvArgs {
     int n_text_ctx;
     const DecState *st;
     const uint16_t *gelu_tab;
-    unsigned long long *amax;   // DEC_LOGITS: per-clip packed argmax
+    unsigned long long *amax;   // DEC_LOGITS: packed argmax, AMAX_SHARDS shards per clip
     int suppress_id;            // DEC_LOGITS: id excluded from argmax (-1 none)
     DecState *st_advance;       // DEC_LOGITS: pos += 1 (block 0)
+    // embed prologue (IN = 3, first layer): x = te[tok] + pe[pos], tok from
+    // feed[b][pos] while pos < feed_len, else from the previous step's argmax
+    const uint16_t *te;
+    const float *pe;
+    const int32_t *feed;
+    int feed_len, feed_stride;
+    int32_t *tokens_out;        // [B][out_stride], token of pos - feed_len
+    int out_stride;
+    float *x_out;               // residual stream written by block 0
 };
+constexpr int AMAX_SHARDS = 64;
 hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a);
 
 struct DecAttnArgs {
     const uint16_t *q;       // [B][n]
-    const uint16_t *K, *V;   // [B][ldkv_clip] rows of n
+    const uint16_t *K, *V;   // per clip: rows of n (clip_stride elements apart)
     int64_t clip_stride;     // elements between clips in K/V
     int M_fixed;             // >0: fixed key count (cross); 0: pos + 1 (self)
     const DecState *st;
-    uint16_t *out;           // [B][n]
+    float *S;                // scores [B][H][s_stride]
+    int s_stride;
+    float *cmax;             // per-chunk max [B][H][n_chunks]
+    float *opart;            // partial outputs [B][n_chunks][n]
+    int n_chunks;            // 128-key chunks in the grid (covers the max M)
     const uint16_t *exp_tab;
     int n_exp, H, n, B;
+    unsigned long long *reset_amax;  // self-attn: zero these B * AMAX_SHARDS words (block 0)
+    // cross-attention: q = f16((Wq LN(x) + bq) * qscale) computed in the score kernel
+    const float *x, *ln_w, *ln_b;
+    const uint16_t *Wq;
+    const float *bq;
+    float qscale;
 };
 hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a);
 

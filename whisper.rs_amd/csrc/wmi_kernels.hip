@@ -674,10 +674,10 @@ hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a) {
 }
 
 // ============================================================================
-// decoder step kernels (batch B <= 8 clips)
+// decoder step kernels (batch B <= 8 clips), latency-oriented
 // ============================================================================
-constexpr int DG_RPW = 4;  // output rows per wave
 constexpr int DG_MAXB = 8;
+constexpr int DG_KB = 1024;  // K elements per row per chunk: 16 lanes x 8 loads x 8 halfs
 
 __device__ __forceinline__ float dot8(const half8 w, const half8 x, float acc) {
     acc = __builtin_amdgcn_fdot2(half2v{w[0], w[1]}, half2v{x[0], x[1]}, acc, false);
@@ -687,217 +687,560 @@ __device__ __forceinline__ float dot8(const half8 w, const half8 x, float acc) {
     return acc;
 }
 
-template <int EPI, bool LN>
+// y[b][o] = W[o] . in[b]  for B <= 8 input rows.  A quarter-wave (16 lanes)
+// owns one output row; a wave owns 4*G rows, a workgroup 16*G.  Latency is
+// what matters at decode batch sizes, so every global load the kernel needs
+// (weight rows, input rows / attention partials, bias, residual) is issued
+// before anything waits: the whole kernel costs about one memory round trip.
+//   IN = 0: LayerNorm(x) prologue (x rows held in registers, double stats)
+//   IN = 1: f16 input vector
+//   IN = 2: sum (in chunk order) of split-key attention partials
+constexpr int DG_LNV = 5;  // float4 per lane for a LayerNorm row (K <= 1280)
+
+// previous step's greedy token of one clip: max over its AMAX_SHARDS packed
+// (ordered logit << 32 | ~id) words; called by a whole wave, result uniform
+__device__ __forceinline__ int32_t shard_token(const unsigned long long *sh, int lane) {
+    unsigned long long k = sh[lane];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(k, o);
+        k = t > k ? t : k;
+    }
+    return (int32_t)(0xffffffffu - (uint32_t)(k & 0xffffffffull));
+}
+
+// LayerNorm of one K-row held as float4 registers (ggml norm semantics)
+__device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K, const float *lw, const float *lb,
+                                               f16 *dst, int lane) {
+    double s1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < DG_LNV; ++i)
+        if ((lane + 64 * i) * 4 < K) s1 += ((double)xv[i].x + (double)xv[i].y) + ((double)xv[i].z + (double)xv[i].w);
+    s1 = wave_sum(s1);
+    const double mean = s1 / K;
+    double s2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < DG_LNV; ++i)
+        if ((lane + 64 * i) * 4 < K) {
+            const double d0 = (double)xv[i].x - mean, d1 = (double)xv[i].y - mean;
+            const double d2 = (double)xv[i].z - mean, d3 = (double)xv[i].w - mean;
+            s2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+        }
+    s2 = wave_sum(s2);
+    const float scale = (float)(1.0 / sqrt(s2 / K + (double)1e-5f));
+#pragma unroll
+    for (int i = 0; i < DG_LNV; ++i) {
+        const int e = (lane + 64 * i) * 4;
+        if (e < K) {
+            const float4 gw = *(const float4 *)(lw + e);
+            const float4 gb = *(const float4 *)(lb + e);
+            const float xx[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+            const float ww[4] = {gw.x, gw.y, gw.z, gw.w}, bb4[4] = {gb.x, gb.y, gb.z, gb.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float t = (float)((double)xx[u] - mean) * scale;
+                dst[e + u] = (f16)(bb4[u] + ww[u] * t);
+            }
+        }
+    }
+}
+
+template <int EPI, int IN, int G>
 __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
     f16 *xs = (f16 *)smraw;  // [B][K]
     __shared__ unsigned long long amax_s[DG_MAXB];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int K = a.K, B = a.B;
-    if (LN) {
-        for (int rb = w; rb < B; rb += 4)
-            layernorm_wave(a.x + (int64_t)rb * K, K, a.ln_w, a.ln_b, (uint16_t *)(xs + rb * K), nullptr, lane);
-    } else {
+    const int q = lane >> 4, l16 = lane & 15;
+    const int K = a.K, B = a.B, N = a.N;
+    const int rowbase = (blockIdx.x * 4 + w) * 4 * G;
+    const f16 *W = (const f16 *)a.W;
+    half8 wv[G][8];
+    auto load_chunk = [&](int k0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int row = rowbase + g * 4 + q;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const int k = k0 + c * 128 + l16 * 8;
+                if (row < N && k < K) wv[g][c] = *(const half8 *)(W + (int64_t)row * K + k);
+                else
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) wv[g][c][e] = (f16)0.0f;
+            }
+        }
+    };
+    load_chunk(0);
+    // epilogue operands, prefetched: lane l16 == bb owns (row, bb)
+    float ebias[G], eres[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int o = rowbase + g * 4 + q;
+        ebias[g] = (a.bias && o < N) ? a.bias[o] : 0.0f;
+        eres[g] = (EPI == DEC_RESID && o < N && l16 < B) ? a.out32[(int64_t)l16 * N + o] : 0.0f;
+    }
+    if (IN == 0 || IN == 3) {
+        // each wave normalises rows w and w + 4
+        const int pos = (IN == 3) ? a.st->pos : 0;
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            const int rb = w + 4 * rr;
+            if (rb < B) {
+                float4 xv[DG_LNV];
+                if (IN == 0) {
+                    const float4 *xr = (const float4 *)(a.x + (int64_t)rb * K);
+#pragma unroll
+                    for (int i = 0; i < DG_LNV; ++i) {
+                        const int e = (lane + 64 * i) * 4;
+                        xv[i] = e < K ? xr[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                } else {
+                    // x = te[tok] + pe[pos] (get_rows f16 -> f32, add)
+                    const bool fed = pos < a.feed_len;
+                    const int32_t tok = fed ? a.feed[rb * a.feed_stride + pos]
+                                            : shard_token(a.amax + rb * AMAX_SHARDS, lane);
+                    const f16 *ter = (const f16 *)a.te + (int64_t)tok * K;
+                    const float *per = a.pe + (int64_t)pos * K;
+#pragma unroll
+                    for (int i = 0; i < DG_LNV; ++i) {
+                        const int e = (lane + 64 * i) * 4;
+                        if (e < K) {
+                            const half4 tv = *(const half4 *)(ter + e);
+                            const float4 pv = *(const float4 *)(per + e);
+                            xv[i] = make_float4((float)tv[0] + pv.x, (float)tv[1] + pv.y, (float)tv[2] + pv.z,
+                                                (float)tv[3] + pv.w);
+                            if (blockIdx.x == 0) *(float4 *)(a.x_out + (int64_t)rb * K + e) = xv[i];
+                        } else {
+                            xv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+                        }
+                    }
+                    if (blockIdx.x == 0 && lane == 0 && !fed)
+                        a.tokens_out[rb * a.out_stride + (pos - a.feed_len)] = tok;
+                }
+                ln_regs_to_lds(xv, K, a.ln_w, a.ln_b, xs + rb * K, lane);
+            }
+        }
+    } else if (IN == 1) {
         const uint4 *src = (const uint4 *)a.xin16;
         uint4 *dst = (uint4 *)xs;
         for (int i = tid; i < B * K / 8; i += 256) dst[i] = src[i];
+    } else {
+        // partial sums: thread owns 4 consecutive inputs; all chunk loads issued first
+        constexpr int CMAXP = 16;
+        for (int i4 = tid; i4 < B * K / 4; i4 += 256) {
+            const int bb = (i4 * 4) / K, k = i4 * 4 - bb * K;
+            const float *p = a.parts + ((int64_t)bb * a.n_parts) * K + k;
+            float4 v[CMAXP];
+#pragma unroll
+            for (int c = 0; c < CMAXP; ++c)
+                v[c] = c < a.n_parts ? *(const float4 *)(p + (int64_t)c * K) : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 sacc = v[0];
+#pragma unroll
+            for (int c = 1; c < CMAXP; ++c)
+                if (c < a.n_parts) {
+                    sacc.x = sacc.x + v[c].x; sacc.y = sacc.y + v[c].y;
+                    sacc.z = sacc.z + v[c].z; sacc.w = sacc.w + v[c].w;
+                }
+            half4 hv;
+            hv[0] = (f16)sacc.x; hv[1] = (f16)sacc.y; hv[2] = (f16)sacc.z; hv[3] = (f16)sacc.w;
+            *(half4 *)(xs + bb * K + k) = hv;
+        }
     }
     if (EPI == DEC_LOGITS && tid < DG_MAXB) amax_s[tid] = 0ull;
     __syncthreads();
-    const int row0 = (blockIdx.x * 4 + w) * DG_RPW;
-    float acc[DG_RPW][DG_MAXB];
+    float acc[G][DG_MAXB];
 #pragma unroll
-    for (int r = 0; r < DG_RPW; ++r)
+    for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int bb = 0; bb < DG_MAXB; ++bb) acc[r][bb] = 0.0f;
-    for (int kc = lane * 8; kc < K; kc += 512) {
-        half8 wv[DG_RPW];
+        for (int bb = 0; bb < DG_MAXB; ++bb) acc[g][bb] = 0.0f;
+    for (int k0 = 0; k0 < K; k0 += DG_KB) {
+        if (k0 > 0) load_chunk(k0);
 #pragma unroll
-        for (int r = 0; r < DG_RPW; ++r) {
-            const int o = row0 + r;
-            if (o < a.N) wv[r] = *(const half8 *)((const f16 *)a.W + (int64_t)o * K + kc);
-            else
+        for (int c = 0; c < 8; ++c) {
+            const int k = k0 + c * 128 + l16 * 8;
+            if (k0 + c * 128 < K) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) wv[r][e] = (f16)0.0f;
-        }
+                for (int bb = 0; bb < DG_MAXB; ++bb) {
+                    if (bb < B) {
+                        const half8 xv = *(const half8 *)(xs + bb * K + k);
 #pragma unroll
-        for (int bb = 0; bb < DG_MAXB; ++bb) {
-            if (bb < B) {
-                const half8 xv = *(const half8 *)(xs + bb * K + kc);
-#pragma unroll
-                for (int r = 0; r < DG_RPW; ++r) acc[r][bb] = dot8(wv[r], xv, acc[r][bb]);
+                        for (int g = 0; g < G; ++g) acc[g][bb] = dot8(wv[g][c], xv, acc[g][bb]);
+                    }
+                }
             }
         }
     }
 #pragma unroll
-    for (int r = 0; r < DG_RPW; ++r)
+    for (int g = 0; g < G; ++g)
 #pragma unroll
         for (int bb = 0; bb < DG_MAXB; ++bb)
-            if (bb < B) acc[r][bb] = wave_sum(acc[r][bb]);
-    // epilogue: lane (r * B + bb) owns value (r, bb)
+            if (bb < B) {
+                float v = acc[g][bb];
+                v += __shfl_xor(v, 8);
+                v += __shfl_xor(v, 4);
+                v += __shfl_xor(v, 2);
+                v += __shfl_xor(v, 1);
+                acc[g][bb] = v;
+            }
     const int pos = (EPI == DEC_QKV) ? a.st->pos : 0;
 #pragma unroll
-    for (int r = 0; r < DG_RPW; ++r)
+    for (int g = 0; g < G; ++g) {
+        const int o = rowbase + g * 4 + q;
+        float v = 0.0f;
 #pragma unroll
-        for (int bb = 0; bb < DG_MAXB; ++bb) {
-            if (bb >= B || lane != r * DG_MAXB + bb) continue;
-            const int o = row0 + r;
-            if (o >= a.N) continue;
-            const float v = acc[r][bb];
-            if (EPI == DEC_QKV) {
-                const int n = a.N / 3, which = o / n, c = o - which * n;
-                if (which == 0) a.out16[bb * a.ldo + c] = f2h_bits((v + a.bias[o]) * a.qscale);
-                else if (which == 1)
-                    a.kcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(v * a.qscale);
-                else a.vcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(a.bias[o] + v);
-            } else if (EPI == DEC_Q) {
-                a.out16[bb * a.ldo + o] = f2h_bits((v + a.bias[o]) * a.qscale);
-            } else if (EPI == DEC_GELU) {
-                a.out16[bb * a.ldo + o] = a.gelu_tab[f2h_bits(v + a.bias[o])];
-            } else if (EPI == DEC_RESID) {
-                float *p = a.out32 + (int64_t)bb * a.N + o;
-                *p = (v + a.bias[o]) + *p;
-            } else if (EPI == DEC_LOGITS) {
-                a.out32[(int64_t)bb * a.N + o] = v;
-                if (o != a.suppress_id) {
-                    const unsigned long long key =
-                        ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)o);
-                    atomicMax(&amax_s[bb], key);
-                }
+        for (int bb = 0; bb < DG_MAXB; ++bb)
+            if (l16 == bb) v = acc[g][bb];
+        if (l16 >= B || o >= N) continue;
+        const int bb = l16;
+        if (EPI == DEC_QKV) {
+            const int n = N / 3, which = o / n, c = o - which * n;
+            if (which == 0) a.out16[bb * a.ldo + c] = f2h_bits((v + ebias[g]) * a.qscale);
+            else if (which == 1)
+                a.kcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(v * a.qscale);
+            else a.vcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(ebias[g] + v);
+        } else if (EPI == DEC_Q) {
+            a.out16[bb * a.ldo + o] = f2h_bits((v + ebias[g]) * a.qscale);
+        } else if (EPI == DEC_GELU) {
+            a.out16[bb * a.ldo + o] = a.gelu_tab[f2h_bits(v + ebias[g])];
+        } else if (EPI == DEC_RESID) {
+            a.out32[(int64_t)bb * N + o] = (v + ebias[g]) + eres[g];
+        } else if (EPI == DEC_LOGITS) {
+            a.out32[(int64_t)bb * N + o] = v;
+            if (o != a.suppress_id) {
+                const unsigned long long key =
+                    ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)o);
+                atomicMax(&amax_s[bb], key);
             }
         }
+    }
     if (EPI == DEC_LOGITS) {
         __syncthreads();
-        if (tid < B && amax_s[tid]) atomicMax(&a.amax[tid], amax_s[tid]);
+        if (tid < B && amax_s[tid]) atomicMax(&a.amax[tid * AMAX_SHARDS + (blockIdx.x & (AMAX_SHARDS - 1))], amax_s[tid]);
         if (blockIdx.x == 0 && tid == 0) a.st_advance->pos += 1;
     }
 }
 
-hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a) {
-    if (a.B < 1 || a.B > DG_MAXB || a.K % 8) return hipErrorInvalidValue;
-    dim3 grid(cdiv(a.N, 4 * DG_RPW)), block(256);
+template <int EPI, int IN>
+static hipError_t dec_gemv_g(hipStream_t s, int G, const DecGemvArgs &a) {
     const size_t lds = (size_t)a.B * a.K * 2;
-    const bool ln = a.ln_w != nullptr;
-#define DG(E, L)                                                              \
-    do {                                                                      \
-        hipError_t e_ = allow_lds(k_dec_gemv<E, L>, lds);                     \
-        if (e_ != hipSuccess) return e_;                                      \
-        hipLaunchKernelGGL((k_dec_gemv<E, L>), grid, block, lds, s, a);       \
-    } while (0)
-    switch (epi) {
-        case DEC_QKV: if (ln) DG(DEC_QKV, true); else DG(DEC_QKV, false); break;
-        case DEC_Q: if (ln) DG(DEC_Q, true); else DG(DEC_Q, false); break;
-        case DEC_GELU: if (ln) DG(DEC_GELU, true); else DG(DEC_GELU, false); break;
-        case DEC_RESID: if (ln) DG(DEC_RESID, true); else DG(DEC_RESID, false); break;
-        case DEC_LOGITS: if (ln) DG(DEC_LOGITS, true); else DG(DEC_LOGITS, false); break;
-        default: return hipErrorInvalidValue;
+    dim3 block(256);
+    if (G == 2) {
+        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 2>, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 2>), dim3(cdiv(a.N, 32)), block, lds, s, a);
+    } else {
+        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1>, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1>), dim3(cdiv(a.N, 16)), block, lds, s, a);
     }
-#undef DG
     return hipGetLastError();
 }
 
-// decoder attention for one (clip, head): scores over M keys (pre-scaled f16
-// K rows), softmax as ggml_compute_forward_soft_max_f32 (table exp, double
-// sum), P16 = f16(p * (1/sum)), out = sum_j P16_j V_j (f32) -> f16.
-constexpr int DA_THREADS = 512;
-__global__ __launch_bounds__(DA_THREADS) void k_dec_attn(DecAttnArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
-    const int h = blockIdx.x, b = blockIdx.y;
+hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a) {
+    if (a.B < 1 || a.B > DG_MAXB || a.K % 128) return hipErrorInvalidValue;
+    const int in = a.te ? 3 : (a.ln_w ? 0 : (a.parts ? 2 : 1));
+    const int G = a.N >= 8192 ? 2 : 1;
+#define DGC(E)                                                     \
+    case E:                                                        \
+        if (in == 0) return dec_gemv_g<E, 0>(s, G, a);             \
+        if (in == 1) return dec_gemv_g<E, 1>(s, G, a);             \
+        if (in == 3) return dec_gemv_g<E, 3>(s, G, a);             \
+        return dec_gemv_g<E, 2>(s, G, a);
+    switch (epi) {
+        DGC(DEC_QKV)
+        DGC(DEC_Q)
+        DGC(DEC_GELU)
+        DGC(DEC_RESID)
+        DGC(DEC_LOGITS)
+        default: return hipErrorInvalidValue;
+    }
+#undef DGC
+}
+
+// ---- decoder attention, split over 128-key chunks --------------------------
+// ggml_compute_forward_soft_max_f32 semantics need the row max and the row sum
+// before any P16 = f16(p * (1/sum)) exists, so the key range is split in two
+// passes: (1) scores + per-chunk max; (2) every chunk workgroup recomputes the
+// (cheap, L2-resident) global sum from the scores in the same order, so all
+// chunks use the identical 1/sum, then writes its partial P16 V.  The partials
+// are summed in chunk order by the consumer GEMV's prologue (IN = 2).
+constexpr int DA_CK = 128;
+
+// cross-attention scores for one 128-key chunk of one (clip, head), with the
+// query projection fused in: q_h = f16((Wq[h*64:(h+1)*64] LN(x) + bq) * qscale)
+// is recomputed by every chunk workgroup of the head (64 x n weights, L2
+// resident) instead of costing its own kernel.  K rows, Wq rows, bias and x
+// are all requested before the first wait.
+template <int KC>
+__global__ __launch_bounds__(256) void k_dec_xq_scores(DecAttnArgs a) {
+    const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    constexpr int NW = DA_THREADS / 64;
+    const int q = lane >> 4, l16 = lane & 15;
+    const int M = a.M_fixed;
+    const int n = a.n;  // == KC * 128
+    __shared__ __attribute__((aligned(16))) f16 xs[KC * 128];
+    __shared__ __attribute__((aligned(16))) f16 qh[64];
+    __shared__ float red[4];
+    // this chunk's K rows: thread = (key, half)
+    const int key = c * DA_CK + (tid >> 1), half = tid & 1;
+    half8 kf[4];
+    {
+        const f16 *kr = (const f16 *)a.K + (int64_t)b * a.clip_stride + (int64_t)key * n + h * 64 + half * 32;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (key < M) kf[i] = *(const half8 *)(kr + 8 * i);
+            else
+#pragma unroll
+                for (int e = 0; e < 8; ++e) kf[i][e] = (f16)0.0f;
+    }
+    // Wq rows of head h: wave w, quarter q owns rows w*16 + q*4 + i
+    half8 wq[4][KC];
+    float bqr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = h * 64 + w * 16 + q * 4 + i;
+        const f16 *wr = (const f16 *)a.Wq + (int64_t)r * n + l16 * 8;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) wq[i][kc] = *(const half8 *)(wr + kc * 128);
+        bqr[i] = a.bq[r];
+    }
+    if (w == 0) {
+        float4 xv[DG_LNV];
+        const float4 *xr = (const float4 *)(a.x + (int64_t)b * n);
+#pragma unroll
+        for (int i = 0; i < DG_LNV; ++i) {
+            const int e = (lane + 64 * i) * 4;
+            xv[i] = e < n ? xr[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        ln_regs_to_lds(xv, n, a.ln_w, a.ln_b, xs, lane);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) acc = dot8(wq[i][kc], *(const half8 *)(xs + kc * 128 + l16 * 8), acc);
+        acc += __shfl_xor(acc, 8);
+        acc += __shfl_xor(acc, 4);
+        acc += __shfl_xor(acc, 2);
+        acc += __shfl_xor(acc, 1);
+        if (l16 == 0) qh[w * 16 + q * 4 + i] = (f16)((acc + bqr[i]) * a.qscale);
+    }
+    __syncthreads();
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s = dot8(kf[i], *(const half8 *)(qh + half * 32 + 8 * i), s);
+    s += __shfl_xor(s, 1);
+    float *S = a.S + ((int64_t)b * a.H + h) * a.s_stride;
+    if (half == 0 && key < M) S[key] = s;
+    float m = (key < M) ? s : -INFINITY;
+    m = wave_max(m);
+    if (lane == 0) red[w] = m;
+    __syncthreads();
+    if (tid == 0)
+        a.cmax[((int64_t)b * a.H + h) * a.n_chunks + c] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+__global__ __launch_bounds__(256) void k_dec_attn_pv(DecAttnArgs a) {
+    const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int M = a.M_fixed > 0 ? a.M_fixed : a.st->pos + 1;
     const int n = a.n;
-    float *S = (float *)smraw;                         // [M]
-    uint16_t *P = (uint16_t *)(S + ((M + 3) & ~3));   // [M]
-    __shared__ float redf[NW];
-    __shared__ double redd[NW];
-    __shared__ float opart[NW][64];
-    const f16 *q = (const f16 *)a.q + (int64_t)b * n + h * 64;
-    const f16 *Kb = (const f16 *)a.K + (int64_t)b * a.clip_stride + h * 64;
-    const f16 *Vb = (const f16 *)a.V + (int64_t)b * a.clip_stride + h * 64;
-    half8 qv[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) qv[i] = *(const half8 *)(q + 8 * i);
-    float mx = -INFINITY;
-    for (int j = tid; j < M; j += DA_THREADS) {
-        const f16 *kr = Kb + (int64_t)j * n;
-        float s = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) s = dot8(*(const half8 *)(kr + 8 * i), qv[i], s);
-        S[j] = s;
-        mx = fmaxf(mx, s);
+    const int nC = (M + DA_CK - 1) / DA_CK;
+    float *Ob = a.opart + ((int64_t)b * a.n_chunks + c) * n + h * 64;
+    if (c >= nC) {
+        if (tid < 64) Ob[tid] = 0.0f;
+        return;
     }
-    mx = wave_max(mx);
-    if (lane == 0) redf[w] = mx;
-    __syncthreads();
-    mx = redf[0];
+    __shared__ double redd[4];
+    __shared__ float opart[4][64];
+    __shared__ __attribute__((aligned(16))) uint16_t P[DA_CK];
+    // prefetch this chunk's V rows (independent of the softmax): wave w keys
+    // w*32 .. w*32+31, lane = d
+    const f16 *Vb = (const f16 *)a.V + (int64_t)b * a.clip_stride + h * 64 + lane;
+    const int jw = c * DA_CK + w * 32;
+    f16 vv[32];
 #pragma unroll
-    for (int i = 1; i < NW; ++i) mx = fmaxf(mx, redf[i]);
+    for (int u = 0; u < 32; ++u) vv[u] = (jw + u < M) ? Vb[(int64_t)(jw + u) * n] : (f16)0.0f;
+    const int64_t bh = (int64_t)b * a.H + h;
+    const float *S = a.S + bh * a.s_stride;
+    constexpr int SU = 8;  // M <= 2048 in one unrolled sweep
+    float sv[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+        const int j = tid + 256 * u;
+        sv[u] = j < M ? S[j] : 0.0f;
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (i < nC) m = fmaxf(m, a.cmax[bh * a.n_chunks + i]);
     double sum = 0.0;
-    for (int j = tid; j < M; j += DA_THREADS) {
-        const uint32_t i = f2h_bits(S[j] - mx) & 0x7fffu;
-        const float p = (int)i < a.n_exp ? h2f_bits(a.exp_tab[i]) : 0.0f;
-        S[j] = p;
-        sum += (double)p;
+    float pmine = 0.0f;
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+        const int j = tid + 256 * u;
+        if (j < M) {
+            const uint32_t i = f2h_bits(sv[u] - m) & 0x7fffu;
+            const float p = (int)i < a.n_exp ? h2f_bits(a.exp_tab[i]) : 0.0f;
+            sum += (double)p;
+            if (j >= c * DA_CK && j < (c + 1) * DA_CK) pmine = p;
+        }
+    }
+    for (int j = tid + 256 * SU; j < M; j += 256) {  // M > 2048: not reached by Whisper shapes
+        const uint32_t i = f2h_bits(S[j] - m) & 0x7fffu;
+        sum += (double)((int)i < a.n_exp ? h2f_bits(a.exp_tab[i]) : 0.0f);
     }
     sum = wave_sum(sum);
     if (lane == 0) redd[w] = sum;
     __syncthreads();
-    double tot = 0.0;
+    const float inv = (float)(1.0 / (((redd[0] + redd[1]) + redd[2]) + redd[3]));
+    {
+        const int jj0 = c * DA_CK;
 #pragma unroll
-    for (int i = 0; i < NW; ++i) tot += redd[i];
-    const float inv = (float)(1.0 / tot);
-    for (int j = tid; j < M; j += DA_THREADS) P[j] = f2h_bits(S[j] * inv);
+        for (int u = 0; u < SU; ++u) {
+            const int j = tid + 256 * u;
+            if (j >= jj0 && j < jj0 + DA_CK) P[j - jj0] = f2h_bits(j < M ? pmine * inv : 0.0f);
+        }
+    }
     __syncthreads();
     float o = 0.0f;
-    for (int j = w; j < M; j += NW) o = o + h2f_bits(P[j]) * (float)Vb[(int64_t)j * n + lane];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) o = o + h2f_bits(P[w * 32 + u]) * (float)vv[u];
     opart[w][lane] = o;
     __syncthreads();
-    if (w == 0) {
-        float v = opart[0][lane];
+    if (w == 0) Ob[lane] = ((opart[0][lane] + opart[1][lane]) + opart[2][lane]) + opart[3][lane];
+}
+
+// self-attention over the KV cache (M = pos + 1 <= 512 keys): one workgroup
+// per (clip, head), every K and V load issued up front.  Output goes to
+// opart[b][0][n] (n_parts = 1 for the consumer).
+__global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
+    const int h = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int M = a.st->pos + 1;
+    const int n = a.n;
+    __shared__ float redf[4];
+    __shared__ double redd[4];
+    __shared__ __attribute__((aligned(16))) uint16_t P[512];
+    __shared__ float ored[32][64];
+    const f16 *Kb = (const f16 *)a.K + (int64_t)b * a.clip_stride + h * 64;
+    const f16 *Vb = (const f16 *)a.V + (int64_t)b * a.clip_stride + h * 64;
+    const f16 *qr = (const f16 *)a.q + (int64_t)b * n + h * 64;
+    if (a.reset_amax && h == 0 && b == 0)
+        for (int i = tid; i < a.B * AMAX_SHARDS; i += 256) a.reset_amax[i] = 0ull;
+    // scores: thread t owns keys t and t + 256
+    half8 kv[2][8];
 #pragma unroll
-        for (int i = 1; i < NW; ++i) v = v + opart[i][lane];
-        a.out[(int64_t)b * n + h * 64 + lane] = f2h_bits(v);
+    for (int r = 0; r < 2; ++r) {
+        const int j = tid + 256 * r;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (j < M) kv[r][i] = *(const half8 *)(Kb + (int64_t)j * n + 8 * i);
+            else
+#pragma unroll
+                for (int e = 0; e < 8; ++e) kv[r][i][e] = (f16)0.0f;
+    }
+    // PV: thread owns d-octet (tid & 7) and keys (tid >> 3) + 32 i
+    const int doct = tid & 7, jg = tid >> 3;
+    half8 vv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int j = jg + 32 * i;
+        if (j < M) vv[i] = *(const half8 *)(Vb + (int64_t)j * n + doct * 8);
+        else
+#pragma unroll
+            for (int e = 0; e < 8; ++e) vv[i][e] = (f16)0.0f;
+    }
+    half8 qv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qv[i] = *(const half8 *)(qr + 8 * i);
+    float sc[2];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s = dot8(kv[r][i], qv[i], s);
+        sc[r] = s;
+        if (tid + 256 * r < M) mx = fmaxf(mx, s);
+    }
+    mx = wave_max(mx);
+    if (lane == 0) redf[w] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
+    double sum = 0.0;
+    float p[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        p[r] = 0.0f;
+        if (tid + 256 * r < M) {
+            const uint32_t i = f2h_bits(sc[r] - mx) & 0x7fffu;
+            p[r] = (int)i < a.n_exp ? h2f_bits(a.exp_tab[i]) : 0.0f;
+            sum += (double)p[r];
+        }
+    }
+    sum = wave_sum(sum);
+    if (lane == 0) redd[w] = sum;
+    __syncthreads();
+    const float inv = (float)(1.0 / (((redd[0] + redd[1]) + redd[2]) + redd[3]));
+#pragma unroll
+    for (int r = 0; r < 2; ++r) P[tid + 256 * r] = f2h_bits(tid + 256 * r < M ? p[r] * inv : 0.0f);
+    __syncthreads();
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float pj = h2f_bits(P[jg + 32 * i]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vv[i][e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ored[jg][doct * 8 + e] = o[e];
+    __syncthreads();
+    if (tid < 64) {
+        float v = ored[0][tid];
+        for (int g = 1; g < 32; ++g) v = v + ored[g][tid];
+        a.opart[(int64_t)b * n + h * 64 + tid] = v;
     }
 }
 
 hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
-    const int Mmax = a.M_fixed > 0 ? a.M_fixed : 4096;
-    const size_t lds = (size_t)((Mmax + 3) & ~3) * 4 + (size_t)Mmax * 2 + 16;
-    hipError_t e = allow_lds(k_dec_attn, lds);
+    if (a.M_fixed == 0) {  // self-attention: M = pos + 1 <= 512
+        if (a.n_chunks != 1) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_dec_self_attn, dim3(a.H, a.B), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
+    if (a.M_fixed > 2048 || a.n_chunks > 16 || a.n % 128) return hipErrorInvalidValue;
+    dim3 grid(a.n_chunks, a.H, a.B);
+    switch (a.n / 128) {
+        case 1: hipLaunchKernelGGL(k_dec_xq_scores<1>, grid, dim3(256), 0, s, a); break;
+        case 2: hipLaunchKernelGGL(k_dec_xq_scores<2>, grid, dim3(256), 0, s, a); break;
+        case 3: hipLaunchKernelGGL(k_dec_xq_scores<3>, grid, dim3(256), 0, s, a); break;
+        case 5: hipLaunchKernelGGL(k_dec_xq_scores<5>, grid, dim3(256), 0, s, a); break;
+        case 4: hipLaunchKernelGGL(k_dec_xq_scores<4>, grid, dim3(256), 0, s, a); break;
+        case 6: hipLaunchKernelGGL(k_dec_xq_scores<6>, grid, dim3(256), 0, s, a); break;
+        case 8: hipLaunchKernelGGL(k_dec_xq_scores<8>, grid, dim3(256), 0, s, a); break;
+        case 10: hipLaunchKernelGGL(k_dec_xq_scores<10>, grid, dim3(256), 0, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_dec_attn, dim3(a.H, a.B), dim3(DA_THREADS), lds, s, a);
+    hipLaunchKernelGGL(k_dec_attn_pv, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void k_dec_embed(DecEmbedArgs a) {
-    __shared__ int32_t tok[DG_MAXB];
+// records the token produced by the last step (the in-step record happens in
+// the first layer's QKV prologue): one wave per clip
+__global__ __launch_bounds__(64) void k_dec_record(DecEmbedArgs a) {
+    const int b = blockIdx.x, lane = threadIdx.x;
     const int pos = a.st->pos;
-    const int tid = threadIdx.x;
-    if (tid < a.B) {
-        int32_t t;
-        if (pos < a.feed_len) {
-            t = a.feed[tid * a.feed_stride + pos];
-        } else {
-            const unsigned long long key = a.amax[tid];
-            t = (int32_t)(0xffffffffu - (uint32_t)(key & 0xffffffffull));
-            a.tokens_out[tid * a.out_stride + (pos - a.feed_len)] = t;
-        }
-        // the previous step's argmax is consumed (or, while feeding, unused):
-        // clear it before this step's logits kernel accumulates into it
-        a.amax[tid] = 0ull;
-        tok[tid] = t;
-    }
-    __syncthreads();
-    if (a.record_only) return;
-    for (int i = tid; i < a.B * a.n; i += 256) {
-        const int bb = i / a.n, c = i - bb * a.n;
-        a.x[i] = h2f_bits(a.te[(int64_t)tok[bb] * a.n + c]) + a.pe[(int64_t)pos * a.n + c];
-    }
+    const int32_t tok = shard_token(a.amax + b * AMAX_SHARDS, lane);
+    if (lane == 0 && pos >= a.feed_len) a.tokens_out[b * a.out_stride + (pos - a.feed_len)] = tok;
 }
 
 hipError_t launch_dec_embed(hipStream_t s, const DecEmbedArgs &a) {
-    hipLaunchKernelGGL(k_dec_embed, dim3(1), dim3(256), 0, s, a);
+    if (!a.record_only) return hipErrorInvalidValue;  // the embedding is fused into layer 0's QKV kernel
+    hipLaunchKernelGGL(k_dec_record, dim3(a.B), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

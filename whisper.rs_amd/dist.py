@@ -1,0 +1,113 @@
+"""Host-side rendezvous for one-process-per-GPU runs (torchrun-compatible env).
+
+The data-path collective is RCCL (wmi_dist_gather_tokens over xGMI).  What
+RCCL needs before it exists — every rank agreeing on one ncclUniqueId — and
+the benchmark's host bookkeeping (barrier, max-over-ranks of a timing) go
+through this small TCP star centred on rank 0, reading RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT as torch.distributed.run exports them.  No torch
+import: the benchmark process must load exactly one HIP runtime (ours).
+"""
+from __future__ import annotations
+
+import os
+import pickle
+import socket
+import struct
+import time
+
+_PORT_OFFSET = 23  # torchrun's own TCPStore holds MASTER_PORT itself
+
+
+def env_rank_world():
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), \
+        int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+
+
+def _send(sock, data: bytes):
+    sock.sendall(struct.pack("<Q", len(data)) + data)
+
+
+def _recv(sock) -> bytes:
+    hdr = b""
+    while len(hdr) < 8:
+        chunk = sock.recv(8 - len(hdr))
+        if not chunk:
+            raise ConnectionError("peer closed")
+        hdr += chunk
+    (n,) = struct.unpack("<Q", hdr)
+    buf = bytearray()
+    while len(buf) < n:
+        chunk = sock.recv(min(1 << 20, n - len(buf)))
+        if not chunk:
+            raise ConnectionError("peer closed")
+        buf += chunk
+    return bytes(buf)
+
+
+class Group:
+    """All-gather of small picklable objects over a TCP star (rank 0 hub)."""
+
+    def __init__(self, rank: int, world: int, addr: str | None = None, port: int | None = None,
+                 timeout: float = 300.0):
+        self.rank, self.world = rank, world
+        self.peers = []
+        self.sock = None
+        if world == 1:
+            return
+        addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = port or int(os.environ.get("MASTER_PORT", "29500")) + _PORT_OFFSET
+        if rank == 0:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind((addr, port))
+            srv.listen(world)
+            srv.settimeout(timeout)
+            peers = {}
+            while len(peers) < world - 1:
+                c, _ = srv.accept()
+                c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                r = struct.unpack("<i", _recv(c))[0]
+                peers[r] = c
+            srv.close()
+            self.peers = [peers[r] for r in range(1, world)]
+        else:
+            deadline = time.time() + timeout
+            while True:
+                try:
+                    s = socket.create_connection((addr, port), timeout=10)
+                    break
+                except OSError:
+                    if time.time() > deadline:
+                        raise
+                    time.sleep(0.2)
+            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            s.settimeout(timeout)
+            _send(s, struct.pack("<i", rank))
+            self.sock = s
+
+    def all_gather(self, obj):
+        if self.world == 1:
+            return [obj]
+        if self.rank == 0:
+            objs = [obj] + [pickle.loads(_recv(p)) for p in self.peers]
+            blob = pickle.dumps(objs)
+            for p in self.peers:
+                _send(p, blob)
+            return objs
+        _send(self.sock, pickle.dumps(obj))
+        return pickle.loads(_recv(self.sock))
+
+    def broadcast(self, obj, root: int = 0):
+        return self.all_gather(obj if self.rank == root else None)[root]
+
+    def barrier(self):
+        self.all_gather(None)
+
+    def max(self, x: float) -> float:
+        return max(self.all_gather(x))
+
+    def close(self):
+        for p in self.peers:
+            p.close()
+        if self.sock:
+            self.sock.close()

@@ -62,7 +62,7 @@ EXPORTS = (
     "wmi_get_hparams", "wmi_get_special_tokens", "wmi_set_audio_ctx", "wmi_token_to_bytes",
     "wmi_pcm_to_mel", "wmi_pcm_to_mel_batch", "wmi_encode", "wmi_decode_greedy", "wmi_decode_logits", "wmi_full",
     "wmi_stage_pcm", "wmi_run_staged", "wmi_get_tokens", "wmi_get_timings", "wmi_sync",
-    "wmi_get_mel", "wmi_get_encoder_out", "wmi_get_cross_kv",
+    "wmi_get_mel", "wmi_get_encoder_out", "wmi_get_cross_kv", "wmi_bench_kernel",
     "wmi_dist_id_size", "wmi_dist_make_id", "wmi_dist_init", "wmi_dist_gather_tokens", "wmi_dist_barrier",
 )
 
@@ -78,6 +78,11 @@ class Hparams(C.Structure):
 class SpecialTokens(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("eot", "sot", "prev", "solm", "not_", "beg", "translate", "transcribe",
                                          "is_multilingual")]
+
+
+class KernelBench(C.Structure):
+    _fields_ = [("avg_us", C.c_float), ("alg_bytes", C.c_double), ("alg_flops", C.c_double),
+                ("name", C.c_char * 48)]
 
 
 class Timings(C.Structure):
@@ -121,6 +126,7 @@ def lib():
         L.wmi_get_mel.argtypes = [vp, C.c_int, vp, sz, C.POINTER(i32), C.POINTER(i32)]
         L.wmi_get_encoder_out.argtypes = [vp, C.c_int, vp, sz]
         L.wmi_get_cross_kv.argtypes = [vp, C.c_int, vp, vp, sz]
+        L.wmi_bench_kernel.argtypes = [vp, C.c_int, C.c_int, C.POINTER(KernelBench)]
         L.wmi_dist_id_size.restype = sz
         L.wmi_dist_make_id.argtypes = [vp]
         L.wmi_dist_init.argtypes = [vp, C.c_int, C.c_int, vp]
@@ -257,6 +263,12 @@ class WhisperContext:
         _raise(lib().wmi_get_timings(self._h, C.byref(t)), self._h)
         return {"mel_ms": t.mel_ms, "encode_ms": t.encode_ms, "cross_kv_ms": t.cross_kv_ms,
                 "decode_ms": t.decode_ms, "n_decode_steps": t.n_decode_steps}
+
+    def bench_kernel(self, which: int, iters: int = 50) -> dict:
+        """Mean duration of one kernel of the last run (HIP events, same stream)."""
+        kb = KernelBench()
+        _raise(lib().wmi_bench_kernel(self._h, which, iters, C.byref(kb)), self._h)
+        return {"name": kb.name.decode(), "avg_us": kb.avg_us, "alg_bytes": kb.alg_bytes, "alg_flops": kb.alg_flops}
 
     # --- parity getters -----------------------------------------------------
     def mel(self, clip: int = 0) -> np.ndarray:
