@@ -31,11 +31,18 @@ import synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense FP16
-KERNELS = {0: ("hbm", "dec_logits"), 1: ("mfma", "enc_mlp0"), 2: ("mfma", "enc_attn"), 3: ("mfma", "cross_kv")}
+KERNELS = {0: ("hbm", "dec_logits"), 1: ("mfma", "enc_mlp0"), 2: ("mfma", "enc_attn"), 3: ("mfma", "cross_kv"),
+           4: ("hbm", "probe_empty"), 5: ("hbm", "probe_copy_1MiB")}
 
 
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def clip_seeds(rank: int, clips_per_gpu: int):
+    """Synthetic clip seeds of one rank: clip c of the global batch uses seed
+    1234 + c; rank r owns clips [r * cpg, (r + 1) * cpg)."""
+    return [1234 + rank * clips_per_gpu + i for i in range(clips_per_gpu)]
 
 
 def cpu_baseline(model_path: str, clip, n_decode: int, min_seconds: float, max_seconds: float):
@@ -96,7 +103,7 @@ def main():
     group = dist.Group(rank, world)
     cpg = args.clips_per_gpu
     path = synth.model_path(args.model)
-    clips = [synth.synth_pcm_f32(30.0, 1234 + rank * cpg + i) for i in range(cpg)]
+    clips = [synth.synth_pcm_f32(30.0, sd) for sd in clip_seeds(rank, cpg)]
     audio_s = 30.0 * cpg
 
     import wmi

@@ -156,6 +156,11 @@ typedef struct wmi_kernel_bench {
 } wmi_kernel_bench;
 int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *out);
 
+/* Device self-test: the decoder computes ggml's f16 exp table entries
+ * instead of looking them up; *n_mismatch = entries (of 31745 non-positive
+ * f16 inputs) where the computed value differs from the host-built table. */
+int wmi_selftest(wmi_context *ctx, int32_t *n_mismatch);
+
 /* ---- parity getters (copy device results into caller-owned buffers) --- */
 
 /* ctx.mel (main.rs:1574-1578): [n_mel][n_len] f32. */

@@ -71,6 +71,7 @@ def tables():
 
 class OracleModel:
     def __init__(self, path: str):
+        self.h = None
         L = lib()
         h = C.c_void_p()
         err = C.create_string_buffer(512)

@@ -48,6 +48,12 @@ def micro_ctx(wmi, micro_model):
     ctx.close()
 
 
+def test_device_exp_matches_ggml_table(micro_ctx):
+    """The decoder computes exp instead of reading ggml's f16 table: every one
+    of the 31745 non-positive f16 inputs must give the table's exact entry."""
+    assert micro_ctx.selftest() == 0
+
+
 def test_mel_bit_parity(micro_ctx, oracle_micro):
     for secs, seed in ((2.0, 1234), (30.0, 7), (0.37, 3)):
         pcm = synth.synth_pcm_f32(secs, seed)

@@ -1,0 +1,163 @@
+"""CPU tests of the oracle (oracle/wmi_oracle.c): pinned against the committed
+golden vectors of an independent NumPy restatement (tests/golden/), against
+HuggingFace's independent Whisper implementation, and for its own invariants.
+No GPU needed.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+import synth
+from conftest import ROOT, threads
+
+GOLDEN = os.path.join(ROOT, "tests", "golden", "micro_golden.npz")
+
+
+def f16(bits):
+    return np.asarray(bits, np.uint16).view(np.float16).astype(np.float32)
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return np.load(GOLDEN)
+
+
+def test_golden_inputs_regenerate_bitwise(golden, micro_model):
+    """The synthetic model / clip generators still produce the fixture's inputs."""
+    assert hashlib.sha256(open(micro_model, "rb").read()).hexdigest() == str(golden["model_sha256"])
+    pcm = synth.synth_pcm_f32(2.0, 1234)
+    assert hashlib.sha256(pcm.tobytes()).hexdigest() == str(golden["pcm_sha256"])
+
+
+def test_oracle_mel_vs_golden(oracle_micro, golden):
+    mel = oracle_micro.mel(synth.synth_pcm_f32(2.0, 1234))
+    assert mel.shape == golden["mel"].shape == (80, 200)
+    # f32 recursive FFT (reference) vs float64 numpy FFT: low-power bins carry
+    # the f32 FFT's absolute error, a few 1e-4 after log10 + normalisation
+    assert np.abs(mel - golden["mel"]).max() < 5e-4
+    assert np.abs(mel - golden["mel"]).mean() < 1e-5
+
+
+def test_oracle_encoder_vs_golden(oracle_micro, golden):
+    mel = oracle_micro.mel(synth.synth_pcm_f32(2.0, 1234))
+    enc, ck, cv = oracle_micro.encode(mel, n_ctx=int(golden["n_ctx"]), n_threads=threads())
+    assert np.abs(enc - golden["enc"]).max() < 1e-3
+    assert np.abs(enc - golden["enc"]).mean() < 1e-4
+    assert np.abs(f16(ck) - golden["ck"].astype(np.float32)).max() <= 1e-3
+    assert np.abs(f16(cv) - golden["cv"].astype(np.float32)).max() <= 1e-3
+
+
+def test_oracle_decoder_vs_golden(oracle_micro, golden):
+    mel = oracle_micro.mel(synth.synth_pcm_f32(2.0, 1234))
+    _, ck, cv = oracle_micro.encode(mel, n_ctx=int(golden["n_ctx"]), n_threads=threads())
+    lg = oracle_micro.decode_logits(ck, cv, golden["tf_tokens"], n_threads=threads())
+    top = np.argsort(-lg, axis=1, kind="stable")[:, :5]
+    np.testing.assert_array_equal(top, golden["tf_top5"])
+    assert np.abs(np.take_along_axis(lg, golden["tf_top5"], 1) - golden["tf_top5_logits"]).max() < 2e-3
+    toks, _ = oracle_micro.decode_greedy(ck, cv, len(golden["greedy"]), suppress_eot=True, n_threads=threads())
+    np.testing.assert_array_equal(toks, golden["greedy"])
+
+
+def test_tables():
+    gelu, expt = pyoracle.tables()
+    h = lambda x: np.float16(x).view(np.uint16)
+    assert expt[h(0.0)] == h(1.0) and expt[h(-0.0)] == h(1.0)
+    assert gelu[h(0.0)] == h(0.0)
+    x = np.arange(65536, dtype=np.uint16).view(np.float16).astype(np.float64)
+    ok = np.isfinite(x) & (np.abs(x) < 8)
+    xs = np.where(ok, x, 0.0)
+    ref = 0.5 * xs * (1 + np.tanh(np.sqrt(2 / np.pi) * xs * (1 + 0.044715 * xs * xs)))
+    got = np.where(ok, gelu.view(np.float16).astype(np.float64), 0.0)
+    assert np.abs(got - ref)[ok].max() <= np.abs(ref[ok]).max() * 2 ** -10
+    neg = (x <= 0) & np.isfinite(x)
+    assert np.all(np.abs(expt.view(np.float16).astype(np.float64)[neg] - np.exp(x[neg])) <= 2 ** -11 + 1e-12)
+
+
+def test_summation_order_noise_floor(oracle_micro):
+    """Exact (double) dot products vs ggml's f32 order: the floor every
+    reordered implementation (the HIP path included) lives at."""
+    mel = oracle_micro.mel(synth.synth_pcm_f32(30.0, 3))
+    a = oracle_micro.encode(mel, n_ctx=1500, n_threads=threads())[0]
+    pyoracle.set_dot_mode(True)
+    try:
+        b = oracle_micro.encode(mel, n_ctx=1500, n_threads=threads())[0]
+    finally:
+        pyoracle.set_dot_mode(False)
+    d = np.abs(a - b)
+    assert 0 < d.max() < 1e-3 and d.mean() < 1e-4
+
+
+def test_mel_edge_cases(oracle_micro):
+    assert oracle_micro.mel(np.zeros(0, np.float32)).shape == (80, 0)
+    assert oracle_micro.mel(np.zeros(159, np.float32)).shape == (80, 0)
+    m = oracle_micro.mel(np.zeros(16000, np.float32))
+    # silence: every bin at the 1e-10 clamp -> log10 = -10 -> (-10 + 4) / 4
+    assert m.shape == (80, 100) and np.all(m == np.float32((-10.0 + 4.0) / 4.0))
+
+
+def test_special_tokens_and_prompt(model_cache):
+    om = pyoracle.OracleModel(synth.model_path("micro", model_cache))
+    assert om.special["eot"] == 50256 and om.special["sot"] == 50257 and not om.special["multilingual"]
+    assert om.prompt() == [50257, 50362]
+    path = os.path.join(model_cache, "ml.bin")
+    synth.write_ggml(path, "micro", hp_override={"n_vocab": 51865})
+    om2 = pyoracle.OracleModel(path)
+    assert om2.special["eot"] == 50257 and om2.special["not"] == 50363 and om2.special["multilingual"]
+    assert om2.prompt() == [50258, 50259, 50359, 50363]
+
+
+@pytest.mark.slow
+def test_hf_transformers_crosscheck(oracle_micro, micro_model):
+    """Architecture pin: HuggingFace's Whisper (an implementation sharing no
+    code with ggml or this repo) loaded with the same weights agrees with the
+    oracle's encoder output and decoder logits up to the f16 rounding points
+    the oracle has and HF (fp32 throughout) does not."""
+    torch = pytest.importorskip("torch")
+    transformers = pytest.importorskip("transformers")
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_golden as mg
+    hp, _, T = mg.read_ggml(micro_model)
+    n_ctx = 64
+    cfg = transformers.WhisperConfig(
+        vocab_size=hp["n_vocab"], num_mel_bins=hp["n_mels"], d_model=hp["n_audio_state"],
+        encoder_layers=hp["n_audio_layer"], encoder_attention_heads=hp["n_audio_head"],
+        decoder_layers=hp["n_text_layer"], decoder_attention_heads=hp["n_text_head"],
+        encoder_ffn_dim=4 * hp["n_audio_state"], decoder_ffn_dim=4 * hp["n_text_state"],
+        max_source_positions=n_ctx, max_target_positions=hp["n_text_ctx"], activation_function="gelu_new",
+        pad_token_id=50256, bos_token_id=50257, eos_token_id=50256, decoder_start_token_id=50257)
+    model = transformers.WhisperModel(cfg).eval()
+    sd = {}
+    for k, v in T.items():
+        t = torch.from_numpy(np.array(v, np.float32))
+        k2 = (k.replace("encoder.blocks", "encoder.layers").replace("decoder.blocks", "decoder.layers")
+               .replace(".attn_ln", ".self_attn_layer_norm").replace(".cross_attn_ln", ".encoder_attn_layer_norm")
+               .replace(".mlp_ln", ".final_layer_norm").replace(".attn.", ".self_attn.")
+               .replace(".cross_attn.", ".encoder_attn.").replace(".query", ".q_proj").replace(".key", ".k_proj")
+               .replace(".value", ".v_proj").replace(".out", ".out_proj").replace(".mlp.0", ".fc1")
+               .replace(".mlp.2", ".fc2").replace("encoder.ln_post", "encoder.layer_norm")
+               .replace("decoder.ln.", "decoder.layer_norm.").replace("token_embedding", "embed_tokens"))
+        if k2 == "encoder.positional_embedding":
+            k2, t = "encoder.embed_positions.weight", t[:n_ctx]
+        elif k2 == "decoder.positional_embedding":
+            k2 = "decoder.embed_positions.weight"
+        elif k2.endswith("conv1.bias") or k2.endswith("conv2.bias"):
+            t = t.reshape(-1)
+        sd[k2] = t
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    assert not unexpected and all("k_proj.bias" in m for m in missing), (missing, unexpected)
+    mel = oracle_micro.mel(synth.synth_pcm_f32(2.0, 1234))
+    enc, ck, cv = oracle_micro.encode(mel, n_ctx=n_ctx, n_threads=threads())
+    with torch.no_grad():
+        feats = torch.from_numpy(mel[:, :2 * n_ctx][None].copy())
+        hf_enc = model.encoder(feats).last_hidden_state[0].numpy()
+        assert np.abs(hf_enc - enc).max() < 2e-2
+        toks = oracle_micro.prompt() + [1000, 1001, 1002, 1003]
+        lg = oracle_micro.decode_logits(ck, cv, np.array(toks, np.int32), n_threads=threads())
+        dec = model.decoder(input_ids=torch.tensor([toks]), encoder_hidden_states=torch.from_numpy(enc[None])).last_hidden_state
+        hf_lg = (dec[0] @ model.decoder.embed_tokens.weight.T).numpy()
+    assert np.abs(hf_lg - lg).max() < 2e-2
+    np.testing.assert_array_equal(hf_lg.argmax(1), lg.argmax(1))

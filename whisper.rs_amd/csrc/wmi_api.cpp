@@ -176,6 +176,9 @@ struct wmi_context {
     float *dx = nullptr, *dlogits = nullptr;
     uint16_t *dq16 = nullptr, *datt16 = nullptr, *dhid16 = nullptr;
     float *dS = nullptr, *dcmax = nullptr, *dopart = nullptr;
+    XSync *dsync = nullptr;     // [n_text_layer][8][n_text_head]
+    uint32_t *derr = nullptr;
+    size_t sync_bytes = 0;
     int s_stride = 0, n_chunks_max = 0;
     unsigned long long *damax = nullptr;
     DecState *dstate = nullptr;
@@ -208,6 +211,7 @@ struct wmi_context {
     hipGraph_t g_graph = nullptr;
     std::string g_key;
     bool use_graph = true;
+    bool use_coop = true;
     // dist
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
@@ -655,6 +659,8 @@ int alloc_workspace(wmi_context *ctx) {
     const size_t o_S = A.take(Bd * Hd * Smax * 4);
     const size_t o_cmax = A.take(Bd * Hd * Cmax * 4);
     const size_t o_opart = A.take(Bd * Cmax * nt * 4);
+    const size_t sync_bytes = (size_t)Lt * 8 * Hd * sizeof(XSync);
+    const size_t o_sync = A.take(sync_bytes + 256);
     const size_t o_amax = A.take(8 * AMAX_SHARDS * 8);
     const size_t o_st = A.take(sizeof(DecState));
     const size_t o_ptrs = A.take(B * sizeof(float *));
@@ -688,6 +694,9 @@ int alloc_workspace(wmi_context *ctx) {
     ctx->dS = (float *)(b + o_S);
     ctx->dcmax = (float *)(b + o_cmax);
     ctx->dopart = (float *)(b + o_opart);
+    ctx->dsync = (XSync *)(b + o_sync);
+    ctx->derr = (uint32_t *)(b + o_sync + sync_bytes);
+    ctx->sync_bytes = sync_bytes + 256;
     ctx->s_stride = (int)Smax;
     ctx->n_chunks_max = (int)Cmax;
     ctx->damax = (unsigned long long *)(b + o_amax);
@@ -876,6 +885,8 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         at.S = ctx->dS; at.s_stride = ctx->s_stride; at.cmax = ctx->dcmax; at.opart = ctx->dopart;
         at.n_chunks = c_cross; at.exp_tab = ctx->exp_tab; at.n_exp = ctx->n_exp; at.H = H; at.n = n; at.B = B;
         at.x = ctx->dx; at.ln_w = d.lnc_w; at.ln_b = d.lnc_b; at.Wq = d.wcq; at.bq = d.bcq; at.qscale = qs;
+        at.sync = ctx->use_coop ? ctx->dsync + (size_t)l * 8 * H : nullptr;
+        at.err = ctx->derr;
         HIPCHK(ctx, launch_dec_attn(s, at));
         g = DecGemvArgs{};
         g.parts = ctx->dopart; g.n_parts = c_cross; g.W = d.wco; g.bias = d.bco; g.N = n; g.K = n; g.B = B;
@@ -967,6 +978,7 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
         const int B = Bt - b0 < 8 ? Bt - b0 : 8;
         HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
         HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * AMAX_SHARDS * 8, ctx->stream));
+        HIPCHK(ctx, hipMemsetAsync(ctx->dsync, 0, ctx->sync_bytes, ctx->stream));
         const int total_steps = np + n_gen - 1;
         int done_steps = 0;
         while (done_steps < total_steps) {
@@ -998,6 +1010,12 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
         em.amax = ctx->damax; em.tokens_out = ctx->dtokens + (size_t)b0 * n_gen; em.out_stride = n_gen;
         em.st = ctx->dstate; em.n = ctx->hp.n_text_state; em.B = B; em.record_only = 1;
         HIPCHK(ctx, launch_dec_embed(ctx->stream, em));
+    }
+    {
+        uint32_t err = 0;
+        HIPCHK(ctx, hipMemcpyAsync(&err, ctx->derr, 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (err) return set_err(ctx, WMI_E_HIP, "cross-attention exchange timed out (workgroups not co-resident)");
     }
     if (host_tokens) {
         HIPCHK(ctx, hipMemcpyAsync(host_tokens->data(), ctx->dtokens, host_tokens->size() * 4, hipMemcpyDeviceToHost,
@@ -1085,6 +1103,7 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     rc = alloc_workspace(ctx.get());
     if (rc) { g_last_error = ctx->last_error; wmi_free(ctx.release()); return rc; }
     if (getenv("WMI_NO_GRAPH")) ctx->use_graph = false;
+    if (getenv("WMI_NO_COOP")) ctx->use_coop = false;
     *out = ctx.release();
     return WMI_OK;
 }
@@ -1205,6 +1224,7 @@ int wmi_decode_logits(wmi_context *ctx, int clip, const int32_t *tokens, int n_t
     HIPCHK(ctx, hipMemcpyAsync(ctx->dfeed, tokens, (size_t)n_tokens * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * AMAX_SHARDS * 8, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->dsync, 0, ctx->sync_bytes, ctx->stream));
     const size_t V = ctx->hp.n_vocab;
     for (int i = 0; i < n_tokens; ++i) {
         rc = run_dec_steps(ctx, clip, 1, n_tokens, n_tokens, 0, 1, 1);
@@ -1345,6 +1365,8 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
             g.ck = ctx->ck; g.cv = ctx->cv; g.T = T; g.n_state = hp.n_text_state; g.n_clips = B;
             g.kscale = powf((float)n / (float)hp.n_audio_head, -0.25f);
             HIPCHK(ctx, launch_gemm(s, EPI_CROSSKV, g));
+        } else if (which == 4 || which == 5) {
+            HIPCHK(ctx, launch_probe(s, which - 4, ctx->hid, ctx->hid + (1 << 20)));
         } else {
             return set_err(ctx, WMI_E_INVALID_ARG, "unknown kernel %d", which);
         }
@@ -1376,12 +1398,30 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
         out->alg_flops = 4.0 * T * (double)T * n * B;
         out->alg_bytes = 4.0 * (double)M * n * 2;
         snprintf(out->name, sizeof out->name, "k_attn_enc");
+    } else if (which == 4) {
+        snprintf(out->name, sizeof out->name, "k_probe_empty");
+    } else if (which == 5) {
+        out->alg_bytes = 2.0 * 256 * 256 * 16;
+        snprintf(out->name, sizeof out->name, "k_probe_copy (1 MiB)");
     } else {
         const double N = hp.n_text_layer * 2.0 * nt;
         out->alg_flops = 2.0 * M * N * n;
         out->alg_bytes = (double)M * n * 2 + N * n * 2 + (double)M * N * 2;
         snprintf(out->name, sizeof out->name, "k_gemm<EPI_CROSSKV>");
     }
+    return WMI_OK;
+}
+
+int wmi_selftest(wmi_context *ctx, int32_t *n_mismatch) {
+    if (!valid(ctx) || !n_mismatch) return WMI_E_INVALID_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));
+    HIPCHK(ctx, launch_selftest(ctx->stream, ctx->exp_tab, ctx->n_exp, ctx->derr));
+    uint32_t mm = 0;
+    HIPCHK(ctx, hipMemcpyAsync(&mm, ctx->derr, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    *n_mismatch = (int32_t)mm;
     return WMI_OK;
 }
 

@@ -10,6 +10,11 @@
 
 namespace wmi {
 
+// ---- launch-overhead probes: 0 = empty kernel, 1 = 256 x 4 KiB copy ---------
+hipError_t launch_probe(hipStream_t s, int which, const void *src, void *dst);
+// device exp (decoder attention) vs the host-built ggml exp table, all inputs
+hipError_t launch_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *mismatch);
+
 // ---- mel frontend (main.rs:1486-1671) ---------------------------------------
 // Constant tables built on the host with the reference's exact f32 formulas
 // (main.rs:1495, 1537, 1568), uploaded once.
@@ -142,6 +147,17 @@ struct DecAttnArgs {
     const uint16_t *Wq;
     const float *bq;
     float qscale;
+    // cooperative single-kernel cross-attention: per (clip, head) exchange
+    // words for this layer, zeroed at the start of every decode run
+    struct XSync *sync;
+    uint32_t *err;           // set to 1 if an exchange spin times out
+};
+// exchange words of one (layer, clip, head) for the cooperative kernel
+struct XSync {
+    uint32_t cnt1, cnt2;     // monotonic arrival counters (target (pos + 1) * n_chunks)
+    uint32_t max_ord[2];     // ordered-uint row max, by epoch parity
+    uint64_t sums[16];       // per-chunk exp sums (double bits), chunk order
+    uint32_t pad[12];
 };
 hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a);
 

@@ -66,6 +66,43 @@ static hipError_t allow_lds(K *kern, size_t bytes) {
 }
 
 // ============================================================================
+// launch-overhead probes (wmi_bench_kernel 4 / 5)
+// ============================================================================
+__global__ void k_probe_empty() {}
+__global__ __launch_bounds__(256) void k_probe_copy(const uint4 *src, uint4 *dst) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    dst[i] = src[i];
+}
+// ggml's table_exp_f16 entry for a non-positive f16 argument, computed:
+// f16((float)exp((double)x)) — the host builds the table with exactly this
+// expression, and a double exp within an ulp of glibc's lands on the same
+// float for every f16 input (wmi_selftest checks all of them on the device).
+__device__ __forceinline__ float exp_f16_exact(float arg) {
+    const f16 h = (f16)arg;
+    return (float)(f16)(float)exp((double)(float)h);
+}
+
+// every non-positive f16 argument: computed exp vs the host-built table
+__global__ void k_selftest_exp(const uint16_t *tab, int n_exp, uint32_t *mismatch) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > 0x7c00) return;
+    const float x = h2f_bits((uint16_t)(0x8000u | (uint32_t)j));
+    const uint16_t got = f2h_bits(exp_f16_exact(x));
+    const uint16_t want = j < n_exp ? tab[j] : (uint16_t)0;
+    if (got != want) atomicAdd(mismatch, 1u);
+}
+hipError_t launch_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *mismatch) {
+    hipLaunchKernelGGL(k_selftest_exp, dim3(cdiv(0x7c01, 256)), dim3(256), 0, s, exp_tab, n_exp, mismatch);
+    return hipGetLastError();
+}
+
+hipError_t launch_probe(hipStream_t s, int which, const void *src, void *dst) {
+    if (which == 0) hipLaunchKernelGGL(k_probe_empty, dim3(1), dim3(64), 0, s);
+    else hipLaunchKernelGGL(k_probe_copy, dim3(256), dim3(256), 0, s, (const uint4 *)src, (uint4 *)dst);
+    return hipGetLastError();
+}
+
+// ============================================================================
 // mel frontend
 // ============================================================================
 constexpr int MEL_WAVES = 4;
@@ -677,7 +714,7 @@ hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a) {
 // decoder step kernels (batch B <= 8 clips), latency-oriented
 // ============================================================================
 constexpr int DG_MAXB = 8;
-constexpr int DG_KB = 1024;  // K elements per row per chunk: 16 lanes x 8 loads x 8 halfs
+
 
 __device__ __forceinline__ float dot8(const half8 w, const half8 x, float acc) {
     acc = __builtin_amdgcn_fdot2(half2v{w[0], w[1]}, half2v{x[0], x[1]}, acc, false);
@@ -712,6 +749,14 @@ __device__ __forceinline__ int32_t shard_token(const unsigned long long *sh, int
 // LayerNorm of one K-row held as float4 registers (ggml norm semantics)
 __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K, const float *lw, const float *lb,
                                                f16 *dst, int lane) {
+    // gain/bias requested before the two reductions so their latency hides
+    float4 gw[DG_LNV], gb[DG_LNV];
+#pragma unroll
+    for (int i = 0; i < DG_LNV; ++i) {
+        const int e = (lane + 64 * i) * 4;
+        gw[i] = e < K ? *(const float4 *)(lw + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+        gb[i] = e < K ? *(const float4 *)(lb + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     double s1 = 0.0;
 #pragma unroll
     for (int i = 0; i < DG_LNV; ++i)
@@ -732,10 +777,8 @@ __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K
     for (int i = 0; i < DG_LNV; ++i) {
         const int e = (lane + 64 * i) * 4;
         if (e < K) {
-            const float4 gw = *(const float4 *)(lw + e);
-            const float4 gb = *(const float4 *)(lb + e);
             const float xx[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
-            const float ww[4] = {gw.x, gw.y, gw.z, gw.w}, bb4[4] = {gb.x, gb.y, gb.z, gb.w};
+            const float ww[4] = {gw[i].x, gw[i].y, gw[i].z, gw[i].w}, bb4[4] = {gb[i].x, gb[i].y, gb[i].z, gb[i].w};
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const float t = (float)((double)xx[u] - mean) * scale;
@@ -745,23 +788,32 @@ __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K
     }
 }
 
-template <int EPI, int IN, int G>
+
+// NC = 128-element K chunks a lane prefetches per row (8 for K <= 1024, 16 for
+// the MLP-down GEMV at K = 4n <= 2048); longer rows loop.
+template <int EPI, int IN, int G, int NC>
 __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
+    constexpr int DG_NC = NC, DG_KB = NC * 128;
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
     f16 *xs = (f16 *)smraw;  // [B][K]
     __shared__ unsigned long long amax_s[DG_MAXB];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int q = lane >> 4, l16 = lane & 15;
     const int K = a.K, B = a.B, N = a.N;
-    const int rowbase = (blockIdx.x * 4 + w) * 4 * G;
+    // row groups of 16*G rows; a grid smaller than the group count walks them
+    // (persistent form, used for the vocabulary-sized logits GEMV so the
+    // LayerNorm prologue is paid once per workgroup, not once per 32 rows)
+    const int nrg = (N + 16 * G - 1) / (16 * G);
+    int rg = blockIdx.x;
+    int rowbase = (rg * 4 + w) * 4 * G;
     const f16 *W = (const f16 *)a.W;
-    half8 wv[G][8];
+    half8 wv[G][DG_NC];
     auto load_chunk = [&](int k0) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int row = rowbase + g * 4 + q;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
+            for (int c = 0; c < DG_NC; ++c) {
                 const int k = k0 + c * 128 + l16 * 8;
                 if (row < N && k < K) wv[g][c] = *(const half8 *)(W + (int64_t)row * K + k);
                 else
@@ -848,69 +900,90 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
     }
     if (EPI == DEC_LOGITS && tid < DG_MAXB) amax_s[tid] = 0ull;
     __syncthreads();
-    float acc[G][DG_MAXB];
+    for (;;) {
+        float acc[G][DG_MAXB];
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+        for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int bb = 0; bb < DG_MAXB; ++bb) acc[g][bb] = 0.0f;
-    for (int k0 = 0; k0 < K; k0 += DG_KB) {
-        if (k0 > 0) load_chunk(k0);
+            for (int bb = 0; bb < DG_MAXB; ++bb) acc[g][bb] = 0.0f;
+        for (int k0 = 0; k0 < K; k0 += DG_KB) {
+            if (k0 > 0) load_chunk(k0);
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const int k = k0 + c * 128 + l16 * 8;
-            if (k0 + c * 128 < K) {
+            for (int c = 0; c < DG_NC; ++c) {
+                const int k = k0 + c * 128 + l16 * 8;
+                if (k0 + c * 128 < K) {
 #pragma unroll
-                for (int bb = 0; bb < DG_MAXB; ++bb) {
-                    if (bb < B) {
-                        const half8 xv = *(const half8 *)(xs + bb * K + k);
+                    for (int bb = 0; bb < DG_MAXB; ++bb) {
+                        if (bb < B) {
+                            const half8 xv = *(const half8 *)(xs + bb * K + k);
 #pragma unroll
-                        for (int g = 0; g < G; ++g) acc[g][bb] = dot8(wv[g][c], xv, acc[g][bb]);
+                            for (int g = 0; g < G; ++g) acc[g][bb] = dot8(wv[g][c], xv, acc[g][bb]);
+                        }
                     }
                 }
             }
         }
-    }
+        const int cur_rowbase = rowbase;
+        // prefetch the next row group before this group's reduction/epilogue
+        const int next = rg + gridDim.x;
+        if (next < nrg && K <= DG_KB) {
+            rowbase = (next * 4 + w) * 4 * G;
+            load_chunk(0);
+        }
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+        for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int bb = 0; bb < DG_MAXB; ++bb)
-            if (bb < B) {
-                float v = acc[g][bb];
-                v += __shfl_xor(v, 8);
-                v += __shfl_xor(v, 4);
-                v += __shfl_xor(v, 2);
-                v += __shfl_xor(v, 1);
-                acc[g][bb] = v;
+            for (int bb = 0; bb < DG_MAXB; ++bb)
+                if (bb < B) {
+                    float v = acc[g][bb];
+                    v += __shfl_xor(v, 8);
+                    v += __shfl_xor(v, 4);
+                    v += __shfl_xor(v, 2);
+                    v += __shfl_xor(v, 1);
+                    acc[g][bb] = v;
+                }
+        const int pos = (EPI == DEC_QKV) ? a.st->pos : 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int o = cur_rowbase + g * 4 + q;
+            float v = 0.0f;
+#pragma unroll
+            for (int bb = 0; bb < DG_MAXB; ++bb)
+                if (l16 == bb) v = acc[g][bb];
+            if (l16 >= B || o >= N) continue;
+            const int bb = l16;
+            if (EPI == DEC_QKV) {
+                const int n = N / 3, which = o / n, c = o - which * n;
+                if (which == 0) a.out16[bb * a.ldo + c] = f2h_bits((v + ebias[g]) * a.qscale);
+                else if (which == 1)
+                    a.kcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(v * a.qscale);
+                else a.vcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(ebias[g] + v);
+            } else if (EPI == DEC_Q) {
+                a.out16[bb * a.ldo + o] = f2h_bits((v + ebias[g]) * a.qscale);
+            } else if (EPI == DEC_GELU) {
+                a.out16[bb * a.ldo + o] = a.gelu_tab[f2h_bits(v + ebias[g])];
+            } else if (EPI == DEC_RESID) {
+                a.out32[(int64_t)bb * N + o] = (v + ebias[g]) + eres[g];
+            } else if (EPI == DEC_LOGITS) {
+                a.out32[(int64_t)bb * N + o] = v;
+                if (o != a.suppress_id) {
+                    const unsigned long long key =
+                        ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)o);
+                    atomicMax(&amax_s[bb], key);
+                }
             }
-    const int pos = (EPI == DEC_QKV) ? a.st->pos : 0;
+        }
+        if (next >= nrg) break;
+        rg = next;
+        if (K > DG_KB) {
+            rowbase = (rg * 4 + w) * 4 * G;
+            load_chunk(0);
+        }
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const int o = rowbase + g * 4 + q;
-        float v = 0.0f;
-#pragma unroll
-        for (int bb = 0; bb < DG_MAXB; ++bb)
-            if (l16 == bb) v = acc[g][bb];
-        if (l16 >= B || o >= N) continue;
-        const int bb = l16;
-        if (EPI == DEC_QKV) {
-            const int n = N / 3, which = o / n, c = o - which * n;
-            if (which == 0) a.out16[bb * a.ldo + c] = f2h_bits((v + ebias[g]) * a.qscale);
-            else if (which == 1)
-                a.kcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(v * a.qscale);
-            else a.vcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(ebias[g] + v);
-        } else if (EPI == DEC_Q) {
-            a.out16[bb * a.ldo + o] = f2h_bits((v + ebias[g]) * a.qscale);
-        } else if (EPI == DEC_GELU) {
-            a.out16[bb * a.ldo + o] = a.gelu_tab[f2h_bits(v + ebias[g])];
-        } else if (EPI == DEC_RESID) {
-            a.out32[(int64_t)bb * N + o] = (v + ebias[g]) + eres[g];
-        } else if (EPI == DEC_LOGITS) {
-            a.out32[(int64_t)bb * N + o] = v;
-            if (o != a.suppress_id) {
-                const unsigned long long key =
-                    ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)o);
-                atomicMax(&amax_s[bb], key);
-            }
+        for (int g = 0; g < G; ++g) {  // epilogue operands of the next group
+            const int o = rowbase + g * 4 + q;
+            ebias[g] = (a.bias && o < N) ? a.bias[o] : 0.0f;
+            eres[g] = (EPI == DEC_RESID && o < N && l16 < B) ? a.out32[(int64_t)l16 * N + o] : 0.0f;
         }
     }
     if (EPI == DEC_LOGITS) {
@@ -922,16 +995,21 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
 
 template <int EPI, int IN>
 static hipError_t dec_gemv_g(hipStream_t s, int G, const DecGemvArgs &a) {
+    (void)G;
     const size_t lds = (size_t)a.B * a.K * 2;
     dim3 block(256);
-    if (G == 2) {
-        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 2>, lds);
+    // the vocabulary GEMV runs persistent: 4 workgroups per CU walk the row groups
+    const int cap = EPI == DEC_LOGITS ? 1024 : 1 << 30;
+    const int nrg = cdiv(a.N, 16);
+    const dim3 grid(nrg < cap ? nrg : cap);
+    if (a.K > 1024) {
+        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 16>, lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 2>), dim3(cdiv(a.N, 32)), block, lds, s, a);
+        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 16>), grid, block, lds, s, a);
     } else {
-        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1>, lds);
+        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 8>, lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1>), dim3(cdiv(a.N, 16)), block, lds, s, a);
+        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 8>), grid, block, lds, s, a);
     }
     return hipGetLastError();
 }
@@ -939,7 +1017,7 @@ static hipError_t dec_gemv_g(hipStream_t s, int G, const DecGemvArgs &a) {
 hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a) {
     if (a.B < 1 || a.B > DG_MAXB || a.K % 128) return hipErrorInvalidValue;
     const int in = a.te ? 3 : (a.ln_w ? 0 : (a.parts ? 2 : 1));
-    const int G = a.N >= 8192 ? 2 : 1;
+    const int G = 1;
 #define DGC(E)                                                     \
     case E:                                                        \
         if (in == 0) return dec_gemv_g<E, 0>(s, G, a);             \
@@ -1081,15 +1159,13 @@ __global__ __launch_bounds__(256) void k_dec_attn_pv(DecAttnArgs a) {
     for (int u = 0; u < SU; ++u) {
         const int j = tid + 256 * u;
         if (j < M) {
-            const uint32_t i = f2h_bits(sv[u] - m) & 0x7fffu;
-            const float p = (int)i < a.n_exp ? h2f_bits(a.exp_tab[i]) : 0.0f;
+            const float p = exp_f16_exact(sv[u] - m);
             sum += (double)p;
             if (j >= c * DA_CK && j < (c + 1) * DA_CK) pmine = p;
         }
     }
     for (int j = tid + 256 * SU; j < M; j += 256) {  // M > 2048: not reached by Whisper shapes
-        const uint32_t i = f2h_bits(S[j] - m) & 0x7fffu;
-        sum += (double)((int)i < a.n_exp ? h2f_bits(a.exp_tab[i]) : 0.0f);
+        sum += (double)exp_f16_exact(S[j] - m);
     }
     sum = wave_sum(sum);
     if (lane == 0) redd[w] = sum;
@@ -1175,8 +1251,7 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     for (int r = 0; r < 2; ++r) {
         p[r] = 0.0f;
         if (tid + 256 * r < M) {
-            const uint32_t i = f2h_bits(sc[r] - mx) & 0x7fffu;
-            p[r] = (int)i < a.n_exp ? h2f_bits(a.exp_tab[i]) : 0.0f;
+            p[r] = exp_f16_exact(sc[r] - mx);
             sum += (double)p[r];
         }
     }
@@ -1204,6 +1279,156 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     }
 }
 
+
+// Cross-attention as ONE kernel: the n_chunks workgroups of a (clip, head)
+// each own 128 keys and exchange, through agent-scope atomics on XSync (the
+// guide's counter hand-off: returning atomic, vmcnt(0), release add; relaxed
+// poll, acquire fence, atomic reads), first the row max, then their chunk exp
+// sums, which every member adds in chunk order — so the ggml softmax stays
+// exact and deterministic without a second kernel re-reading the scores.
+// All members must be co-resident: the launcher only picks this form when the
+// grid is far below one workgroup per SIMD, and every spin is bounded (on
+// timeout the error word is set and the kernel finishes).
+__device__ __forceinline__ uint32_t spin_until(uint32_t *p, uint32_t target, uint32_t *err) {
+    uint32_t v = 0;
+    for (uint32_t it = 0;; ++it) {
+        v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v >= target) break;
+        if (it > (1u << 22)) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+    return v;
+}
+
+template <int KC>
+__global__ __launch_bounds__(256) void k_dec_xattn_coop(DecAttnArgs a) {
+    const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int q = lane >> 4, l16 = lane & 15;
+    const int M = a.M_fixed, C = a.n_chunks;
+    const int n = a.n;
+    __shared__ __attribute__((aligned(16))) f16 xs[KC * 128];
+    __shared__ __attribute__((aligned(16))) f16 qh[64];
+    __shared__ __attribute__((aligned(16))) uint16_t P[DA_CK];
+    __shared__ float red[4];
+    __shared__ double redd[4];
+    __shared__ float bcast[2];
+    __shared__ float opart[4][64];
+    XSync *sy = a.sync + ((int64_t)b * a.H + h);
+    const uint32_t epoch = (uint32_t)a.st->pos + 1u;
+    // ---- every independent load first: K rows, V rows, Wq rows, bias, x ----
+    const int key = c * DA_CK + (tid >> 1), half = tid & 1;
+    half8 kf[4];
+    {
+        const f16 *kr = (const f16 *)a.K + (int64_t)b * a.clip_stride + (int64_t)key * n + h * 64 + half * 32;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (key < M) kf[i] = *(const half8 *)(kr + 8 * i);
+            else
+#pragma unroll
+                for (int e = 0; e < 8; ++e) kf[i][e] = (f16)0.0f;
+    }
+    const f16 *Vb = (const f16 *)a.V + (int64_t)b * a.clip_stride + h * 64 + lane;
+    const int jw = c * DA_CK + w * 32;
+    f16 vv[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) vv[u] = (jw + u < M) ? Vb[(int64_t)(jw + u) * n] : (f16)0.0f;
+    half8 wq[4][KC];
+    float bqr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = h * 64 + w * 16 + q * 4 + i;
+        const f16 *wr = (const f16 *)a.Wq + (int64_t)r * n + l16 * 8;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) wq[i][kc] = *(const half8 *)(wr + kc * 128);
+        bqr[i] = a.bq[r];
+    }
+    if (w == 0) {
+        float4 xv[DG_LNV];
+        const float4 *xr = (const float4 *)(a.x + (int64_t)b * n);
+#pragma unroll
+        for (int i = 0; i < DG_LNV; ++i) {
+            const int e = (lane + 64 * i) * 4;
+            xv[i] = e < n ? xr[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        ln_regs_to_lds(xv, n, a.ln_w, a.ln_b, xs, lane);
+    }
+    __syncthreads();
+    // ---- q_h = f16((Wq_h LN(x) + bq) * qscale) ----
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) acc = dot8(wq[i][kc], *(const half8 *)(xs + kc * 128 + l16 * 8), acc);
+        acc += __shfl_xor(acc, 8);
+        acc += __shfl_xor(acc, 4);
+        acc += __shfl_xor(acc, 2);
+        acc += __shfl_xor(acc, 1);
+        if (l16 == 0) qh[w * 16 + q * 4 + i] = (f16)((acc + bqr[i]) * a.qscale);
+    }
+    __syncthreads();
+    // ---- scores of this chunk, chunk max ----
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s = dot8(kf[i], *(const half8 *)(qh + half * 32 + 8 * i), s);
+    s += __shfl_xor(s, 1);
+    float m = (key < M) ? s : -INFINITY;
+    m = wave_max(m);
+    if (lane == 0) red[w] = m;
+    __syncthreads();
+    if (tid == 0) {
+        const float mc = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        (void)atomicMax(&sy->max_ord[epoch & 1], ord_f32(mc));
+        if (c == 0) __hip_atomic_store(&sy->max_ord[(epoch + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // every exchanged word is only ever touched by agent-scope atomics, so
+        // completed-before (vmcnt) ordering suffices: no cache release/acquire
+        __hip_atomic_fetch_add(&sy->cnt1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        spin_until(&sy->cnt1, epoch * (uint32_t)C, a.err);
+        bcast[0] = unord_f32(__hip_atomic_load(&sy->max_ord[epoch & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    __syncthreads();
+    const float mrow = bcast[0];
+    // ---- this chunk's exp terms and their sum ----
+    float p = 0.0f;
+    if (key < M) {
+        p = exp_f16_exact(s - mrow);
+    }
+    double ps = half == 0 ? (double)p : 0.0;
+    ps = wave_sum(ps);
+    if (lane == 0) redd[w] = ps;
+    __syncthreads();
+    if (tid == 0) {
+        const double cs = ((redd[0] + redd[1]) + redd[2]) + redd[3];
+        (void)__hip_atomic_exchange(&sy->sums[c], __builtin_bit_cast(uint64_t, cs), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(&sy->cnt2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        spin_until(&sy->cnt2, epoch * (uint32_t)C, a.err);
+        double tot = 0.0;
+        for (int i = 0; i < C; ++i)
+            tot += __builtin_bit_cast(double, __hip_atomic_load(&sy->sums[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        bcast[1] = (float)(1.0 / tot);
+    }
+    __syncthreads();
+    const float inv = bcast[1];
+    if (half == 0) P[tid >> 1] = f2h_bits(key < M ? p * inv : 0.0f);
+    __syncthreads();
+    // ---- partial O = sum over this chunk of P16_j V_j ----
+    float o = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 32; ++u) o = o + h2f_bits(P[w * 32 + u]) * (float)vv[u];
+    opart[w][lane] = o;
+    __syncthreads();
+    if (w == 0)
+        a.opart[((int64_t)b * C + c) * n + h * 64 + lane] =
+            ((opart[0][lane] + opart[1][lane]) + opart[2][lane]) + opart[3][lane];
+}
+
 hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
     if (a.M_fixed == 0) {  // self-attention: M = pos + 1 <= 512
         if (a.n_chunks != 1) return hipErrorInvalidValue;
@@ -1212,6 +1437,20 @@ hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
     }
     if (a.M_fixed > 2048 || a.n_chunks > 16 || a.n % 128) return hipErrorInvalidValue;
     dim3 grid(a.n_chunks, a.H, a.B);
+    // cooperative single kernel while the grid stays well inside residency
+    // (<= 1 workgroup per SIMD-pair); otherwise the two-kernel form
+    if (a.sync && a.n_chunks * a.H * a.B <= 512 && a.n <= 768) {
+        switch (a.n / 128) {
+            case 1: hipLaunchKernelGGL(k_dec_xattn_coop<1>, grid, dim3(256), 0, s, a); break;
+            case 2: hipLaunchKernelGGL(k_dec_xattn_coop<2>, grid, dim3(256), 0, s, a); break;
+            case 3: hipLaunchKernelGGL(k_dec_xattn_coop<3>, grid, dim3(256), 0, s, a); break;
+            case 4: hipLaunchKernelGGL(k_dec_xattn_coop<4>, grid, dim3(256), 0, s, a); break;
+            case 5: hipLaunchKernelGGL(k_dec_xattn_coop<5>, grid, dim3(256), 0, s, a); break;
+            case 6: hipLaunchKernelGGL(k_dec_xattn_coop<6>, grid, dim3(256), 0, s, a); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (a.n / 128) {
         case 1: hipLaunchKernelGGL(k_dec_xq_scores<1>, grid, dim3(256), 0, s, a); break;
         case 2: hipLaunchKernelGGL(k_dec_xq_scores<2>, grid, dim3(256), 0, s, a); break;

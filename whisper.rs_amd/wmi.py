@@ -62,7 +62,7 @@ EXPORTS = (
     "wmi_get_hparams", "wmi_get_special_tokens", "wmi_set_audio_ctx", "wmi_token_to_bytes",
     "wmi_pcm_to_mel", "wmi_pcm_to_mel_batch", "wmi_encode", "wmi_decode_greedy", "wmi_decode_logits", "wmi_full",
     "wmi_stage_pcm", "wmi_run_staged", "wmi_get_tokens", "wmi_get_timings", "wmi_sync",
-    "wmi_get_mel", "wmi_get_encoder_out", "wmi_get_cross_kv", "wmi_bench_kernel",
+    "wmi_get_mel", "wmi_get_encoder_out", "wmi_get_cross_kv", "wmi_bench_kernel", "wmi_selftest",
     "wmi_dist_id_size", "wmi_dist_make_id", "wmi_dist_init", "wmi_dist_gather_tokens", "wmi_dist_barrier",
 )
 
@@ -127,6 +127,7 @@ def lib():
         L.wmi_get_encoder_out.argtypes = [vp, C.c_int, vp, sz]
         L.wmi_get_cross_kv.argtypes = [vp, C.c_int, vp, vp, sz]
         L.wmi_bench_kernel.argtypes = [vp, C.c_int, C.c_int, C.POINTER(KernelBench)]
+        L.wmi_selftest.argtypes = [vp, C.POINTER(i32)]
         L.wmi_dist_id_size.restype = sz
         L.wmi_dist_make_id.argtypes = [vp]
         L.wmi_dist_init.argtypes = [vp, C.c_int, C.c_int, vp]
@@ -269,6 +270,12 @@ class WhisperContext:
         kb = KernelBench()
         _raise(lib().wmi_bench_kernel(self._h, which, iters, C.byref(kb)), self._h)
         return {"name": kb.name.decode(), "avg_us": kb.avg_us, "alg_bytes": kb.alg_bytes, "alg_flops": kb.alg_flops}
+
+    def selftest(self) -> int:
+        """Mismatches of the device-computed f16 exp vs the host ggml table."""
+        n = C.c_int32()
+        _raise(lib().wmi_selftest(self._h, C.byref(n)), self._h)
+        return n.value
 
     # --- parity getters -----------------------------------------------------
     def mel(self, clip: int = 0) -> np.ndarray:
