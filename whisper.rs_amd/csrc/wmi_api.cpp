@@ -212,6 +212,10 @@ struct wmi_context {
     std::string g_key;
     bool use_graph = true;
     bool use_coop = true;
+    // WMI_TRACE=1: per-launch device timeline of the last decoder step
+    bool trace_on = false;
+    unsigned long long *d_trace = nullptr;
+    std::vector<std::string> trace_names;
     // dist
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
@@ -844,12 +848,54 @@ int run_encode(wmi_context *ctx, int mel_offset) {
     return WMI_OK;
 }
 
+constexpr int TRACE_SLOTS = 512;
+
+unsigned long long *tslot(wmi_context *ctx, const char *name, int l) {
+    if (!ctx->trace_on || ctx->trace_names.size() >= (size_t)TRACE_SLOTS) return nullptr;
+    char buf[64];
+    snprintf(buf, sizeof buf, "%s[%d]", name, l);
+    ctx->trace_names.push_back(buf);
+    return ctx->d_trace + 2 * (ctx->trace_names.size() - 1);
+}
+
+// prints the device timeline recorded for the last traced step to stderr
+int trace_dump(wmi_context *ctx) {
+    const size_t ns = ctx->trace_names.size();
+    std::vector<unsigned long long> t(2 * TRACE_SLOTS + 64 * 16);
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipMemcpy(t.data(), ctx->d_trace, t.size() * 8, hipMemcpyDeviceToHost));
+    for (int l = 0; l < ctx->hp.n_text_layer && ctx->use_coop; ++l) {
+        const unsigned long long *ph = t.data() + 2 * TRACE_SLOTS + 16 * l;
+        for (int wg = 0; wg < 2; ++wg) {
+            fprintf(stderr, "[wmi trace] cross_attn[%d] %s chunk phases:", l, wg ? "last " : "first");
+            for (int i = 1; i < 8; ++i) fprintf(stderr, " %7.2f", ((double)ph[8 * wg + i] - (double)ph[0]) * 0.01);
+            fprintf(stderr, "\n");
+        }
+    }
+    if (!ns) return WMI_OK;
+    const unsigned long long t0 = t[0];
+    unsigned long long prev_end = t0;
+    double busy = 0.0;
+    fprintf(stderr, "[wmi trace] %-22s %9s %9s %9s  (us, 100 MHz clock)\n", "launch", "start", "dur", "gap");
+    for (size_t i = 0; i < ns; ++i) {
+        const unsigned long long st = t[2 * i], en = ~t[2 * i + 1];
+        const double d = (en - st) * 0.01, g = ((double)st - (double)prev_end) * 0.01;
+        busy += d;
+        fprintf(stderr, "[wmi trace] %-22s %9.2f %9.2f %9.2f\n", ctx->trace_names[i].c_str(), (st - t0) * 0.01, d, g);
+        prev_end = en;
+    }
+    fprintf(stderr, "[wmi trace] step span %.2f us, sum of launch durations %.2f us, %zu launches\n",
+            (prev_end - t0) * 0.01, busy, ns);
+    return WMI_OK;
+}
+
 // one decoder step for clips [b0, b0 + B) of the encoded batch
 int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride, int suppress_eot, int out_stride) {
     const wmi_hparams &hp = ctx->hp;
     const int n = hp.n_text_state, H = hp.n_text_head, T = ctx->enc_T, Bt = ctx->enc_clips;
     hipStream_t s = ctx->stream;
     const float qs = powf((float)n / (float)H, -0.25f);
+    ctx->trace_names.clear();
     // per layer: [LN+QKV (+embed at l=0)] [self-attn] [Wo+res] [LN+Wcq+cross scores]
     //            [cross softmax+PV] [Wco+res] [LN+W0+GELU] [W1+res]; then LN+logits+argmax
     for (int l = 0; l < hp.n_text_layer; ++l) {
@@ -865,6 +911,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
             g.amax = ctx->damax; g.tokens_out = ctx->dtokens + (size_t)b0 * out_stride; g.out_stride = out_stride;
             g.x_out = ctx->dx;
         }
+        g.trace = tslot(ctx, "qkv", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_QKV, g));
         DecAttnArgs at{};
         at.q = ctx->dq16; at.K = kc; at.V = vc; at.clip_stride = (int64_t)hp.n_text_ctx * n; at.M_fixed = 0;
@@ -872,10 +919,12 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         at.opart = ctx->dopart; at.n_chunks = 1; at.exp_tab = ctx->exp_tab; at.n_exp = ctx->n_exp;
         at.H = H; at.n = n; at.B = B;
         at.reset_amax = l == 0 ? ctx->damax : nullptr;
+        at.trace = tslot(ctx, "self_attn", l);
         HIPCHK(ctx, launch_dec_attn(s, at));
         g = DecGemvArgs{};
         g.parts = ctx->dopart; g.n_parts = 1; g.W = d.wo; g.bias = d.bo; g.N = n; g.K = n; g.B = B;
         g.out32 = ctx->dx;
+        g.trace = tslot(ctx, "wo", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
         const int c_cross = (T + 127) / 128;
         at = DecAttnArgs{};
@@ -887,23 +936,29 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         at.x = ctx->dx; at.ln_w = d.lnc_w; at.ln_b = d.lnc_b; at.Wq = d.wcq; at.bq = d.bcq; at.qscale = qs;
         at.sync = ctx->use_coop ? ctx->dsync + (size_t)l * 8 * H : nullptr;
         at.err = ctx->derr;
+        at.trace = tslot(ctx, "cross_attn", l);
+        at.phase = ctx->trace_on ? ctx->d_trace + 2 * TRACE_SLOTS + 16 * l : nullptr;
         HIPCHK(ctx, launch_dec_attn(s, at));
         g = DecGemvArgs{};
         g.parts = ctx->dopart; g.n_parts = c_cross; g.W = d.wco; g.bias = d.bco; g.N = n; g.K = n; g.B = B;
         g.out32 = ctx->dx;
+        g.trace = tslot(ctx, "wco", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
         g = DecGemvArgs{};
         g.x = ctx->dx; g.ln_w = d.ln2_w; g.ln_b = d.ln2_b; g.W = d.w0; g.bias = d.b0; g.N = 4 * n; g.K = n; g.B = B;
         g.out16 = ctx->dhid16; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
+        g.trace = tslot(ctx, "mlp0", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_GELU, g));
         g = DecGemvArgs{};
         g.xin16 = ctx->dhid16; g.W = d.w1; g.bias = d.b1; g.N = n; g.K = 4 * n; g.B = B; g.out32 = ctx->dx;
+        g.trace = tslot(ctx, "mlp1", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
     }
     DecGemvArgs g{};
     g.x = ctx->dx; g.ln_w = ctx->dln_w; g.ln_b = ctx->dln_b; g.W = ctx->te; g.N = hp.n_vocab; g.K = n; g.B = B;
     g.out32 = ctx->dlogits; g.amax = ctx->damax; g.suppress_id = suppress_eot ? ctx->sp.eot : -1;
     g.st_advance = ctx->dstate;
+    g.trace = tslot(ctx, "logits", 0);
     HIPCHK(ctx, launch_dec_gemv(s, DEC_LOGITS, g));
     return WMI_OK;
 }
@@ -930,6 +985,7 @@ int run_dec_steps(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride
                   int steps) {
     if (!ctx->use_graph) {
         for (int i = 0; i < steps; ++i) {
+            if (ctx->trace_on) HIPCHK(ctx, hipMemsetAsync(ctx->d_trace, 0xff, TRACE_SLOTS * 16, ctx->stream));
             int rc = enqueue_dec_step(ctx, b0, B, feed_len, feed_stride, suppress_eot, out_stride);
             if (rc) return rc;
         }
@@ -951,7 +1007,10 @@ int run_dec_steps(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride
         HIPCHK(ctx, hipGraphInstantiate(&ctx->g_exec, graph, nullptr, nullptr, 0));
         ctx->g_key = key;
     }
-    for (int i = 0; i < steps; ++i) HIPCHK(ctx, hipGraphLaunch(ctx->g_exec, ctx->stream));
+    for (int i = 0; i < steps; ++i) {
+        if (ctx->trace_on) HIPCHK(ctx, hipMemsetAsync(ctx->d_trace, 0xff, TRACE_SLOTS * 16, ctx->stream));
+        HIPCHK(ctx, hipGraphLaunch(ctx->g_exec, ctx->stream));
+    }
     return WMI_OK;
 }
 
@@ -1016,6 +1075,10 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
         HIPCHK(ctx, hipMemcpyAsync(&err, ctx->derr, 4, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         if (err) return set_err(ctx, WMI_E_HIP, "cross-attention exchange timed out (workgroups not co-resident)");
+    }
+    if (ctx->trace_on) {
+        const int rc2 = trace_dump(ctx);
+        if (rc2) return rc2;
     }
     if (host_tokens) {
         HIPCHK(ctx, hipMemcpyAsync(host_tokens->data(), ctx->dtokens, host_tokens->size() * 4, hipMemcpyDeviceToHost,
@@ -1104,6 +1167,10 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (rc) { g_last_error = ctx->last_error; wmi_free(ctx.release()); return rc; }
     if (getenv("WMI_NO_GRAPH")) ctx->use_graph = false;
     if (getenv("WMI_NO_COOP")) ctx->use_coop = false;
+    if (getenv("WMI_TRACE")) {
+        ctx->trace_on = true;
+        HIPCHK(ctx.get(), hipMalloc(&ctx->d_trace, TRACE_SLOTS * 16 + 64 * 16 * 8));
+    }
     *out = ctx.release();
     return WMI_OK;
 }
@@ -1121,6 +1188,7 @@ void wmi_free(wmi_context *ctx) {
     if (ctx->dtokens) (void)hipFree(ctx->dtokens);
     if (ctx->d_gather) (void)hipFree(ctx->d_gather);
     if (ctx->d_ws) (void)hipFree(ctx->d_ws);
+    if (ctx->d_trace) (void)hipFree(ctx->d_trace);
     if (ctx->d_model) (void)hipFree(ctx->d_model);
     for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1339,6 +1407,10 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
     const int n = hp.n_audio_state, T = ctx->enc_T, B = ctx->enc_clips, M = B * T;
     memset(out, 0, sizeof(*out));
     hipStream_t s = ctx->stream;
+    const int bar_wg = which == 6 ? 128 : which == 7 ? 256 : 512, bar_rounds = 32;
+    uint32_t *bar_cnt = ctx->derr + 32;  // inside the 256-byte tail of the sync region
+    uint32_t bar_base = 0;
+    if (which >= 6 && which <= 8) HIPCHK(ctx, hipMemsetAsync(bar_cnt, 0, 4, s));
     auto launch = [&]() -> int {
         if (which == 0) {
             DecGemvArgs g{};
@@ -1367,6 +1439,9 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
             HIPCHK(ctx, launch_gemm(s, EPI_CROSSKV, g));
         } else if (which == 4 || which == 5) {
             HIPCHK(ctx, launch_probe(s, which - 4, ctx->hid, ctx->hid + (1 << 20)));
+        } else if (which >= 6 && which <= 8) {
+            HIPCHK(ctx, launch_probe_barrier(s, bar_wg, bar_rounds, bar_cnt, bar_base, ctx->derr));
+            bar_base += (uint32_t)(bar_wg * bar_rounds);
         } else {
             return set_err(ctx, WMI_E_INVALID_ARG, "unknown kernel %d", which);
         }
@@ -1403,6 +1478,8 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
     } else if (which == 5) {
         out->alg_bytes = 2.0 * 256 * 256 * 16;
         snprintf(out->name, sizeof out->name, "k_probe_copy (1 MiB)");
+    } else if (which >= 6 && which <= 8) {
+        snprintf(out->name, sizeof out->name, "k_probe_barrier (%d WG x %d barriers)", bar_wg, bar_rounds);
     } else {
         const double N = hp.n_text_layer * 2.0 * nt;
         out->alg_flops = 2.0 * M * N * n;

@@ -12,6 +12,7 @@ namespace wmi {
 
 // ---- launch-overhead probes: 0 = empty kernel, 1 = 256 x 4 KiB copy ---------
 hipError_t launch_probe(hipStream_t s, int which, const void *src, void *dst);
+hipError_t launch_probe_barrier(hipStream_t s, int n_wg, int rounds, uint32_t *cnt, uint32_t base, uint32_t *err);
 // device exp (decoder attention) vs the host-built ggml exp table, all inputs
 hipError_t launch_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *mismatch);
 
@@ -124,6 +125,7 @@ struct DecGemvArgs {
     int32_t *tokens_out;        // [B][out_stride], token of pos - feed_len
     int out_stride;
     float *x_out;               // residual stream written by block 0
+    unsigned long long *trace;  // WMI_TRACE: {min start, ~max end} s_memrealtime of this launch
 };
 constexpr int AMAX_SHARDS = 64;
 hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a);
@@ -151,13 +153,13 @@ struct DecAttnArgs {
     // words for this layer, zeroed at the start of every decode run
     struct XSync *sync;
     uint32_t *err;           // set to 1 if an exchange spin times out
+    unsigned long long *trace;  // WMI_TRACE slot (see DecGemvArgs)
+    unsigned long long *phase;  // WMI_TRACE: [2][8] phase times of the first and last chunk of (head 0, clip 0)
 };
 // exchange words of one (layer, clip, head) for the cooperative kernel
 struct XSync {
-    uint32_t cnt1, cnt2;     // monotonic arrival counters (target (pos + 1) * n_chunks)
-    uint32_t max_ord[2];     // ordered-uint row max, by epoch parity
-    uint64_t sums[16];       // per-chunk exp sums (double bits), chunk order
-    uint32_t pad[12];
+    uint32_t cnt;            // monotonic arrival counter (target (pos + 1) * n_chunks)
+    uint32_t pad[15];
 };
 hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a);
 

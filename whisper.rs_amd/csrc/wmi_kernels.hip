@@ -715,6 +715,21 @@ hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a) {
 // ============================================================================
 constexpr int DG_MAXB = 8;
 
+// WMI_TRACE timeline: thread 0 of every workgroup folds its start time into
+// slot[0] (min) and its end time into slot[1] (min of the complement = max);
+// s_memrealtime is the 100 MHz device-wide reference clock.
+__device__ __forceinline__ void trace_begin(unsigned long long *slot) {
+    if (slot && threadIdx.x == 0) atomicMin(slot, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void trace_phase(unsigned long long *ph, int i) {
+    if (ph && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 &&
+        (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
+        ph[(blockIdx.x ? 8 : 0) + i] = __builtin_amdgcn_s_memrealtime();
+}
+__device__ __forceinline__ void trace_end(unsigned long long *slot) {
+    if (slot && threadIdx.x == 0) atomicMin(slot + 1, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 
 __device__ __forceinline__ float dot8(const half8 w, const half8 x, float acc) {
     acc = __builtin_amdgcn_fdot2(half2v{w[0], w[1]}, half2v{x[0], x[1]}, acc, false);
@@ -746,6 +761,28 @@ __device__ __forceinline__ int32_t shard_token(const unsigned long long *sh, int
     return (int32_t)(0xffffffffu - (uint32_t)(k & 0xffffffffull));
 }
 
+// v if ok else 0, written so the compiler cannot sink the load of v into a
+// branch on ok (a select lets it, and the branch then serialises every load
+// behind an s_waitcnt); v must be finite (it is loaded from a clamped, valid
+// address)
+__device__ __forceinline__ float4 keep4(float4 v, bool ok) {
+    const float f = ok ? 1.0f : 0.0f;
+    return make_float4(v.x * f, v.y * f, v.z * f, v.w * f);
+}
+__device__ __forceinline__ float keep1(float v, bool ok) { return v * (ok ? 1.0f : 0.0f); }
+
+// LayerNorm input row as float4 registers: unconditional (clamped) loads so
+// every request is in flight before the first wait
+__device__ __forceinline__ void ln_load_row(const float *x, int K, int lane, float4 (&xv)[DG_LNV]) {
+    const float4 *xr = (const float4 *)x;
+#pragma unroll
+    for (int i = 0; i < DG_LNV; ++i) {
+        const int idx = lane + 64 * i;
+        const bool ok = idx * 4 < K;
+        xv[i] = keep4(xr[ok ? idx : 0], ok);
+    }
+}
+
 // LayerNorm of one K-row held as float4 registers (ggml norm semantics)
 __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K, const float *lw, const float *lb,
                                                f16 *dst, int lane) {
@@ -753,9 +790,9 @@ __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K
     float4 gw[DG_LNV], gb[DG_LNV];
 #pragma unroll
     for (int i = 0; i < DG_LNV; ++i) {
-        const int e = (lane + 64 * i) * 4;
-        gw[i] = e < K ? *(const float4 *)(lw + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-        gb[i] = e < K ? *(const float4 *)(lb + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int e = (lane + 64 * i) * 4, ec = e < K ? e : 0;
+        gw[i] = keep4(*(const float4 *)(lw + ec), e < K);
+        gb[i] = keep4(*(const float4 *)(lb + ec), e < K);
     }
     double s1 = 0.0;
 #pragma unroll
@@ -793,6 +830,7 @@ __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K
 // the MLP-down GEMV at K = 4n <= 2048); longer rows loop.
 template <int EPI, int IN, int G, int NC>
 __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
+    trace_begin(a.trace);
     constexpr int DG_NC = NC, DG_KB = NC * 128;
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
     f16 *xs = (f16 *)smraw;  // [B][K]
@@ -840,12 +878,7 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
             if (rb < B) {
                 float4 xv[DG_LNV];
                 if (IN == 0) {
-                    const float4 *xr = (const float4 *)(a.x + (int64_t)rb * K);
-#pragma unroll
-                    for (int i = 0; i < DG_LNV; ++i) {
-                        const int e = (lane + 64 * i) * 4;
-                        xv[i] = e < K ? xr[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
+                    ln_load_row(a.x + (int64_t)rb * K, K, lane, xv);
                 } else {
                     // x = te[tok] + pe[pos] (get_rows f16 -> f32, add)
                     const bool fed = pos < a.feed_len;
@@ -853,18 +886,21 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
                                             : shard_token(a.amax + rb * AMAX_SHARDS, lane);
                     const f16 *ter = (const f16 *)a.te + (int64_t)tok * K;
                     const float *per = a.pe + (int64_t)pos * K;
+                    half4 tv[DG_LNV];
+                    float4 pv[DG_LNV];
+#pragma unroll
+                    for (int i = 0; i < DG_LNV; ++i) {
+                        const int e = (lane + 64 * i) * 4, ec = e < K ? e : 0;
+                        tv[i] = *(const half4 *)(ter + ec);
+                        pv[i] = *(const float4 *)(per + ec);
+                    }
 #pragma unroll
                     for (int i = 0; i < DG_LNV; ++i) {
                         const int e = (lane + 64 * i) * 4;
-                        if (e < K) {
-                            const half4 tv = *(const half4 *)(ter + e);
-                            const float4 pv = *(const float4 *)(per + e);
-                            xv[i] = make_float4((float)tv[0] + pv.x, (float)tv[1] + pv.y, (float)tv[2] + pv.z,
-                                                (float)tv[3] + pv.w);
-                            if (blockIdx.x == 0) *(float4 *)(a.x_out + (int64_t)rb * K + e) = xv[i];
-                        } else {
-                            xv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-                        }
+                        xv[i] = keep4(make_float4((float)tv[i][0] + pv[i].x, (float)tv[i][1] + pv[i].y,
+                                                  (float)tv[i][2] + pv[i].z, (float)tv[i][3] + pv[i].w),
+                                      e < K);
+                        if (e < K && blockIdx.x == 0) *(float4 *)(a.x_out + (int64_t)rb * K + e) = xv[i];
                     }
                     if (blockIdx.x == 0 && lane == 0 && !fed)
                         a.tokens_out[rb * a.out_stride + (pos - a.feed_len)] = tok;
@@ -991,6 +1027,7 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
         if (tid < B && amax_s[tid]) atomicMax(&a.amax[tid * AMAX_SHARDS + (blockIdx.x & (AMAX_SHARDS - 1))], amax_s[tid]);
         if (blockIdx.x == 0 && tid == 0) a.st_advance->pos += 1;
     }
+    trace_end(a.trace);
 }
 
 template <int EPI, int IN>
@@ -1044,13 +1081,158 @@ hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a) {
 // are summed in chunk order by the consumer GEMV's prologue (IN = 2).
 constexpr int DA_CK = 128;
 
-// cross-attention scores for one 128-key chunk of one (clip, head), with the
-// query projection fused in: q_h = f16((Wq[h*64:(h+1)*64] LN(x) + bq) * qscale)
-// is recomputed by every chunk workgroup of the head (64 x n weights, L2
-// resident) instead of costing its own kernel.  K rows, Wq rows, bias and x
-// are all requested before the first wait.
-template <int KC>
-__global__ __launch_bounds__(256) void k_dec_xq_scores(DecAttnArgs a) {
+// Bounded spin on a monotonic agent-scope counter (cooperative kernels: every
+// member must be co-resident, which the launchers guarantee by grid size; on
+// timeout the error word is set and the kernel finishes instead of hanging).
+__device__ __forceinline__ uint32_t spin_until(uint32_t *p, uint32_t target, uint32_t *err) {
+    uint32_t v = 0;
+    for (uint32_t it = 0;; ++it) {
+        v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v >= target) break;
+        if (it > (1u << 22)) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+    return v;
+}
+
+// grid-barrier probe (wmi_bench_kernel 6-8): `rounds` device-wide barriers on
+// a monotonic counter (base = value left by earlier launches)
+__global__ __launch_bounds__(256) void k_probe_barrier(uint32_t *cnt, uint32_t base, int rounds, uint32_t *err) {
+    for (int r = 0; r < rounds; ++r) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            spin_until(cnt, base + (uint32_t)(r + 1) * gridDim.x, err);
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_probe_barrier(hipStream_t s, int n_wg, int rounds, uint32_t *cnt, uint32_t base, uint32_t *err) {
+    hipLaunchKernelGGL(k_probe_barrier, dim3(n_wg), dim3(256), 0, s, cnt, base, rounds, err);
+    return hipGetLastError();
+}
+
+// ---- words exchanged between workgroups of one launch ----------------------
+// agent-scope relaxed atomics: write-through stores / coherent loads, no cache
+// maintenance; ordering comes from s_waitcnt before the arrival counter
+template <bool COH>
+__device__ __forceinline__ float ld_x(const float *p) {
+    if constexpr (COH)
+        return __builtin_bit_cast(float, __hip_atomic_load((uint32_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    else
+        return *p;
+}
+template <bool COH>
+__device__ __forceinline__ void st_x(float *p, float v) {
+    if constexpr (COH)
+        __hip_atomic_store((uint32_t *)p, __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
+// Phase B of cross-attention for one 128-key chunk: row max over the chunk
+// maxima, the row's exp sum recomputed from all M scores (identical order in
+// every chunk workgroup, hence the identical 1/sum), P16 = f16(p / sum) for
+// this chunk's keys, partial P16 V -> opart[b][c][h*64 .. +64].  vf holds the
+// chunk's V rows: thread (doct = tid & 7, jg = tid >> 3) keys c*128 + jg*4 + u.
+template <bool COH>
+__device__ __forceinline__ void xattn_pv(const DecAttnArgs &a, int c, int h, int b, int M, const half8 (&vf)[4]) {
+    __shared__ double redd[4];
+    __shared__ float ow[4][64];
+    __shared__ __attribute__((aligned(16))) uint16_t P[DA_CK];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n = a.n;
+    const int nC = (M + DA_CK - 1) / DA_CK;
+    const int64_t bh = (int64_t)b * a.H + h;
+    const float *S = a.S + bh * a.s_stride;
+    // every request first: the chunk maxima and this thread's scores
+    float cm[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cm[i] = ld_x<COH>(a.cmax + bh * a.n_chunks + (i < nC ? i : 0));
+    constexpr int SU = 8;  // M <= 2048 in one unrolled sweep
+    float sv[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+        const int j = tid + 256 * u;
+        sv[u] = ld_x<COH>(S + (j < M ? j : M - 1));
+    }
+    float m = cm[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) m = fmaxf(m, cm[i]);
+    double sum = 0.0;
+    float pmine = 0.0f;
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+        const int j = tid + 256 * u;
+        const float p = keep1(exp_f16_exact(sv[u] - m), j < M);
+        sum += (double)p;
+        if (j >= c * DA_CK && j < (c + 1) * DA_CK) pmine = p;
+    }
+    for (int j = tid + 256 * SU; j < M; j += 256) sum += (double)exp_f16_exact(ld_x<COH>(S + j) - m);
+    sum = wave_sum(sum);
+    if (lane == 0) redd[w] = sum;
+    __syncthreads();
+    const float inv = (float)(1.0 / (((redd[0] + redd[1]) + redd[2]) + redd[3]));
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+        const int j = tid + 256 * u;
+        if (j >= c * DA_CK && j < (c + 1) * DA_CK) P[j - c * DA_CK] = f2h_bits(j < M ? pmine * inv : 0.0f);
+    }
+    __syncthreads();
+    const int doct = tid & 7, jg = tid >> 3;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const float pj = h2f_bits(P[jg * 4 + u]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vf[u][e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        o[e] += __shfl_xor(o[e], 8);
+        o[e] += __shfl_xor(o[e], 16);
+        o[e] += __shfl_xor(o[e], 32);
+    }
+    if (lane < 8)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ow[w][lane * 8 + e] = o[e];
+    __syncthreads();
+    if (tid < 64)
+        a.opart[((int64_t)b * a.n_chunks + c) * n + h * 64 + tid] =
+            ((ow[0][tid] + ow[1][tid]) + ow[2][tid]) + ow[3][tid];
+}
+
+// this chunk's V rows for xattn_pv (clamped rows: every load unconditional)
+__device__ __forceinline__ void xattn_load_v(const DecAttnArgs &a, int c, int h, int b, int M, half8 (&vf)[4]) {
+    const int tid = threadIdx.x, doct = tid & 7, jg = tid >> 3;
+    const f16 *Vb = (const f16 *)a.V + (int64_t)b * a.clip_stride + h * 64 + doct * 8;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int j = c * DA_CK + jg * 4 + u;
+        // rows past M repeat row M - 1 (finite); their P16 is 0
+        vf[u] = *(const half8 *)(Vb + (int64_t)(j < M ? j : M - 1) * a.n);
+    }
+}
+
+// Cross-attention for one 128-key chunk of one (clip, head).
+// Phase A: q_h = f16((Wq_h LN(x) + bq) * qscale), recomputed by every chunk
+// workgroup of the head from L2-resident rows instead of costing a kernel;
+// the chunk's scores -> S, its max -> cmax.  MODE 0 stops there (first kernel
+// of the two-kernel form, k_dec_attn_pv is the second).  MODE 1 (cooperative,
+// all chunk workgroups co-resident): one arrival counter per (layer, clip,
+// head) replaces the kernel boundary, then phase B runs in the same launch.
+template <int KC, int MODE>
+__global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
+    trace_begin(a.trace);
+    trace_phase(a.phase, 0);
+    constexpr bool COH = MODE == 1;
     const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int q = lane >> 4, l16 = lane & 15;
@@ -1059,19 +1241,17 @@ __global__ __launch_bounds__(256) void k_dec_xq_scores(DecAttnArgs a) {
     __shared__ __attribute__((aligned(16))) f16 xs[KC * 128];
     __shared__ __attribute__((aligned(16))) f16 qh[64];
     __shared__ float red[4];
-    // this chunk's K rows: thread = (key, half)
+    // ---- every independent load first (all unconditional) ----
     const int key = c * DA_CK + (tid >> 1), half = tid & 1;
     half8 kf[4];
     {
-        const f16 *kr = (const f16 *)a.K + (int64_t)b * a.clip_stride + (int64_t)key * n + h * 64 + half * 32;
+        const f16 *kr = (const f16 *)a.K + (int64_t)b * a.clip_stride + (int64_t)(key < M ? key : M - 1) * n +
+                        h * 64 + half * 32;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (key < M) kf[i] = *(const half8 *)(kr + 8 * i);
-            else
-#pragma unroll
-                for (int e = 0; e < 8; ++e) kf[i][e] = (f16)0.0f;
+        for (int i = 0; i < 4; ++i) kf[i] = *(const half8 *)(kr + 8 * i);
     }
-    // Wq rows of head h: wave w, quarter q owns rows w*16 + q*4 + i
+    half8 vf[4];
+    if (MODE == 1) xattn_load_v(a, c, h, b, M, vf);
     half8 wq[4][KC];
     float bqr[4];
 #pragma unroll
@@ -1084,15 +1264,11 @@ __global__ __launch_bounds__(256) void k_dec_xq_scores(DecAttnArgs a) {
     }
     if (w == 0) {
         float4 xv[DG_LNV];
-        const float4 *xr = (const float4 *)(a.x + (int64_t)b * n);
-#pragma unroll
-        for (int i = 0; i < DG_LNV; ++i) {
-            const int e = (lane + 64 * i) * 4;
-            xv[i] = e < n ? xr[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        ln_load_row(a.x + (int64_t)b * n, n, lane, xv);
         ln_regs_to_lds(xv, n, a.ln_w, a.ln_b, xs, lane);
     }
     __syncthreads();
+    trace_phase(a.phase, 1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         float acc = 0.0f;
@@ -1105,93 +1281,55 @@ __global__ __launch_bounds__(256) void k_dec_xq_scores(DecAttnArgs a) {
         if (l16 == 0) qh[w * 16 + q * 4 + i] = (f16)((acc + bqr[i]) * a.qscale);
     }
     __syncthreads();
+    trace_phase(a.phase, 2);
     float s = 0.0f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) s = dot8(kf[i], *(const half8 *)(qh + half * 32 + 8 * i), s);
     s += __shfl_xor(s, 1);
     float *S = a.S + ((int64_t)b * a.H + h) * a.s_stride;
-    if (half == 0 && key < M) S[key] = s;
+    if (half == 0 && key < M) st_x<COH>(S + key, s);
     float m = (key < M) ? s : -INFINITY;
     m = wave_max(m);
     if (lane == 0) red[w] = m;
     __syncthreads();
     if (tid == 0)
-        a.cmax[((int64_t)b * a.H + h) * a.n_chunks + c] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        st_x<COH>(a.cmax + ((int64_t)b * a.H + h) * a.n_chunks + c, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+    if (MODE == 0) {
+        trace_end(a.trace);
+        return;
+    }
+    // ---- arrival: this chunk's scores and max are globally visible ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    trace_phase(a.phase, 3);
+    if (tid == 0) {
+        XSync *sy = a.sync + ((int64_t)b * a.H + h);
+        const uint32_t epoch = (uint32_t)a.st->pos + 1u;
+        __hip_atomic_fetch_add(&sy->cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        spin_until(&sy->cnt, epoch * (uint32_t)a.n_chunks, a.err);
+    }
+    __syncthreads();
+    trace_phase(a.phase, 4);
+    xattn_pv<COH>(a, c, h, b, M, vf);
+    trace_phase(a.phase, 7);
+    trace_end(a.trace);
 }
 
 __global__ __launch_bounds__(256) void k_dec_attn_pv(DecAttnArgs a) {
+    trace_begin(a.trace);
     const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int M = a.M_fixed > 0 ? a.M_fixed : a.st->pos + 1;
-    const int n = a.n;
-    const int nC = (M + DA_CK - 1) / DA_CK;
-    float *Ob = a.opart + ((int64_t)b * a.n_chunks + c) * n + h * 64;
-    if (c >= nC) {
-        if (tid < 64) Ob[tid] = 0.0f;
-        return;
-    }
-    __shared__ double redd[4];
-    __shared__ float opart[4][64];
-    __shared__ __attribute__((aligned(16))) uint16_t P[DA_CK];
-    // prefetch this chunk's V rows (independent of the softmax): wave w keys
-    // w*32 .. w*32+31, lane = d
-    const f16 *Vb = (const f16 *)a.V + (int64_t)b * a.clip_stride + h * 64 + lane;
-    const int jw = c * DA_CK + w * 32;
-    f16 vv[32];
-#pragma unroll
-    for (int u = 0; u < 32; ++u) vv[u] = (jw + u < M) ? Vb[(int64_t)(jw + u) * n] : (f16)0.0f;
-    const int64_t bh = (int64_t)b * a.H + h;
-    const float *S = a.S + bh * a.s_stride;
-    constexpr int SU = 8;  // M <= 2048 in one unrolled sweep
-    float sv[SU];
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-        const int j = tid + 256 * u;
-        sv[u] = j < M ? S[j] : 0.0f;
-    }
-    float m = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        if (i < nC) m = fmaxf(m, a.cmax[bh * a.n_chunks + i]);
-    double sum = 0.0;
-    float pmine = 0.0f;
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-        const int j = tid + 256 * u;
-        if (j < M) {
-            const float p = exp_f16_exact(sv[u] - m);
-            sum += (double)p;
-            if (j >= c * DA_CK && j < (c + 1) * DA_CK) pmine = p;
-        }
-    }
-    for (int j = tid + 256 * SU; j < M; j += 256) {  // M > 2048: not reached by Whisper shapes
-        sum += (double)exp_f16_exact(S[j] - m);
-    }
-    sum = wave_sum(sum);
-    if (lane == 0) redd[w] = sum;
-    __syncthreads();
-    const float inv = (float)(1.0 / (((redd[0] + redd[1]) + redd[2]) + redd[3]));
-    {
-        const int jj0 = c * DA_CK;
-#pragma unroll
-        for (int u = 0; u < SU; ++u) {
-            const int j = tid + 256 * u;
-            if (j >= jj0 && j < jj0 + DA_CK) P[j - jj0] = f2h_bits(j < M ? pmine * inv : 0.0f);
-        }
-    }
-    __syncthreads();
-    float o = 0.0f;
-#pragma unroll
-    for (int u = 0; u < 32; ++u) o = o + h2f_bits(P[w * 32 + u]) * (float)vv[u];
-    opart[w][lane] = o;
-    __syncthreads();
-    if (w == 0) Ob[lane] = ((opart[0][lane] + opart[1][lane]) + opart[2][lane]) + opart[3][lane];
+    const int M = a.M_fixed;
+    half8 vf[4];
+    xattn_load_v(a, c, h, b, M, vf);
+    xattn_pv<false>(a, c, h, b, M, vf);
+    trace_end(a.trace);
 }
 
 // self-attention over the KV cache (M = pos + 1 <= 512 keys): one workgroup
 // per (clip, head), every K and V load issued up front.  Output goes to
 // opart[b][0][n] (n_parts = 1 for the consumer).
 __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
+    trace_begin(a.trace);
     const int h = blockIdx.x, b = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int M = a.st->pos + 1;
@@ -1277,157 +1415,9 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
         for (int g = 1; g < 32; ++g) v = v + ored[g][tid];
         a.opart[(int64_t)b * n + h * 64 + tid] = v;
     }
+    trace_end(a.trace);
 }
 
-
-// Cross-attention as ONE kernel: the n_chunks workgroups of a (clip, head)
-// each own 128 keys and exchange, through agent-scope atomics on XSync (the
-// guide's counter hand-off: returning atomic, vmcnt(0), release add; relaxed
-// poll, acquire fence, atomic reads), first the row max, then their chunk exp
-// sums, which every member adds in chunk order — so the ggml softmax stays
-// exact and deterministic without a second kernel re-reading the scores.
-// All members must be co-resident: the launcher only picks this form when the
-// grid is far below one workgroup per SIMD, and every spin is bounded (on
-// timeout the error word is set and the kernel finishes).
-__device__ __forceinline__ uint32_t spin_until(uint32_t *p, uint32_t target, uint32_t *err) {
-    uint32_t v = 0;
-    for (uint32_t it = 0;; ++it) {
-        v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v >= target) break;
-        if (it > (1u << 22)) {
-            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    asm volatile("" ::: "memory");
-    return v;
-}
-
-template <int KC>
-__global__ __launch_bounds__(256) void k_dec_xattn_coop(DecAttnArgs a) {
-    const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int q = lane >> 4, l16 = lane & 15;
-    const int M = a.M_fixed, C = a.n_chunks;
-    const int n = a.n;
-    __shared__ __attribute__((aligned(16))) f16 xs[KC * 128];
-    __shared__ __attribute__((aligned(16))) f16 qh[64];
-    __shared__ __attribute__((aligned(16))) uint16_t P[DA_CK];
-    __shared__ float red[4];
-    __shared__ double redd[4];
-    __shared__ float bcast[2];
-    __shared__ float opart[4][64];
-    XSync *sy = a.sync + ((int64_t)b * a.H + h);
-    const uint32_t epoch = (uint32_t)a.st->pos + 1u;
-    // ---- every independent load first: K rows, V rows, Wq rows, bias, x ----
-    const int key = c * DA_CK + (tid >> 1), half = tid & 1;
-    half8 kf[4];
-    {
-        const f16 *kr = (const f16 *)a.K + (int64_t)b * a.clip_stride + (int64_t)key * n + h * 64 + half * 32;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (key < M) kf[i] = *(const half8 *)(kr + 8 * i);
-            else
-#pragma unroll
-                for (int e = 0; e < 8; ++e) kf[i][e] = (f16)0.0f;
-    }
-    const f16 *Vb = (const f16 *)a.V + (int64_t)b * a.clip_stride + h * 64 + lane;
-    const int jw = c * DA_CK + w * 32;
-    f16 vv[32];
-#pragma unroll
-    for (int u = 0; u < 32; ++u) vv[u] = (jw + u < M) ? Vb[(int64_t)(jw + u) * n] : (f16)0.0f;
-    half8 wq[4][KC];
-    float bqr[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = h * 64 + w * 16 + q * 4 + i;
-        const f16 *wr = (const f16 *)a.Wq + (int64_t)r * n + l16 * 8;
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc) wq[i][kc] = *(const half8 *)(wr + kc * 128);
-        bqr[i] = a.bq[r];
-    }
-    if (w == 0) {
-        float4 xv[DG_LNV];
-        const float4 *xr = (const float4 *)(a.x + (int64_t)b * n);
-#pragma unroll
-        for (int i = 0; i < DG_LNV; ++i) {
-            const int e = (lane + 64 * i) * 4;
-            xv[i] = e < n ? xr[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        ln_regs_to_lds(xv, n, a.ln_w, a.ln_b, xs, lane);
-    }
-    __syncthreads();
-    // ---- q_h = f16((Wq_h LN(x) + bq) * qscale) ----
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc) acc = dot8(wq[i][kc], *(const half8 *)(xs + kc * 128 + l16 * 8), acc);
-        acc += __shfl_xor(acc, 8);
-        acc += __shfl_xor(acc, 4);
-        acc += __shfl_xor(acc, 2);
-        acc += __shfl_xor(acc, 1);
-        if (l16 == 0) qh[w * 16 + q * 4 + i] = (f16)((acc + bqr[i]) * a.qscale);
-    }
-    __syncthreads();
-    // ---- scores of this chunk, chunk max ----
-    float s = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) s = dot8(kf[i], *(const half8 *)(qh + half * 32 + 8 * i), s);
-    s += __shfl_xor(s, 1);
-    float m = (key < M) ? s : -INFINITY;
-    m = wave_max(m);
-    if (lane == 0) red[w] = m;
-    __syncthreads();
-    if (tid == 0) {
-        const float mc = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-        (void)atomicMax(&sy->max_ord[epoch & 1], ord_f32(mc));
-        if (c == 0) __hip_atomic_store(&sy->max_ord[(epoch + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // every exchanged word is only ever touched by agent-scope atomics, so
-        // completed-before (vmcnt) ordering suffices: no cache release/acquire
-        __hip_atomic_fetch_add(&sy->cnt1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        spin_until(&sy->cnt1, epoch * (uint32_t)C, a.err);
-        bcast[0] = unord_f32(__hip_atomic_load(&sy->max_ord[epoch & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    __syncthreads();
-    const float mrow = bcast[0];
-    // ---- this chunk's exp terms and their sum ----
-    float p = 0.0f;
-    if (key < M) {
-        p = exp_f16_exact(s - mrow);
-    }
-    double ps = half == 0 ? (double)p : 0.0;
-    ps = wave_sum(ps);
-    if (lane == 0) redd[w] = ps;
-    __syncthreads();
-    if (tid == 0) {
-        const double cs = ((redd[0] + redd[1]) + redd[2]) + redd[3];
-        (void)__hip_atomic_exchange(&sy->sums[c], __builtin_bit_cast(uint64_t, cs), __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(&sy->cnt2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        spin_until(&sy->cnt2, epoch * (uint32_t)C, a.err);
-        double tot = 0.0;
-        for (int i = 0; i < C; ++i)
-            tot += __builtin_bit_cast(double, __hip_atomic_load(&sy->sums[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        bcast[1] = (float)(1.0 / tot);
-    }
-    __syncthreads();
-    const float inv = bcast[1];
-    if (half == 0) P[tid >> 1] = f2h_bits(key < M ? p * inv : 0.0f);
-    __syncthreads();
-    // ---- partial O = sum over this chunk of P16_j V_j ----
-    float o = 0.0f;
-#pragma unroll
-    for (int u = 0; u < 32; ++u) o = o + h2f_bits(P[w * 32 + u]) * (float)vv[u];
-    opart[w][lane] = o;
-    __syncthreads();
-    if (w == 0)
-        a.opart[((int64_t)b * C + c) * n + h * 64 + lane] =
-            ((opart[0][lane] + opart[1][lane]) + opart[2][lane]) + opart[3][lane];
-}
 
 hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
     if (a.M_fixed == 0) {  // self-attention: M = pos + 1 <= 512
@@ -1435,35 +1425,24 @@ hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
         hipLaunchKernelGGL(k_dec_self_attn, dim3(a.H, a.B), dim3(256), 0, s, a);
         return hipGetLastError();
     }
-    if (a.M_fixed > 2048 || a.n_chunks > 16 || a.n % 128) return hipErrorInvalidValue;
+    if (a.M_fixed > 2048 || a.n_chunks > 16 || a.n_chunks * DA_CK < a.M_fixed || a.n % 128) return hipErrorInvalidValue;
     dim3 grid(a.n_chunks, a.H, a.B);
-    // cooperative single kernel while the grid stays well inside residency
-    // (<= 1 workgroup per SIMD-pair); otherwise the two-kernel form
-    if (a.sync && a.n_chunks * a.H * a.B <= 512 && a.n <= 768) {
-        switch (a.n / 128) {
-            case 1: hipLaunchKernelGGL(k_dec_xattn_coop<1>, grid, dim3(256), 0, s, a); break;
-            case 2: hipLaunchKernelGGL(k_dec_xattn_coop<2>, grid, dim3(256), 0, s, a); break;
-            case 3: hipLaunchKernelGGL(k_dec_xattn_coop<3>, grid, dim3(256), 0, s, a); break;
-            case 4: hipLaunchKernelGGL(k_dec_xattn_coop<4>, grid, dim3(256), 0, s, a); break;
-            case 5: hipLaunchKernelGGL(k_dec_xattn_coop<5>, grid, dim3(256), 0, s, a); break;
-            case 6: hipLaunchKernelGGL(k_dec_xattn_coop<6>, grid, dim3(256), 0, s, a); break;
-            default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
+    // cooperative single kernel while the grid stays far inside residency
+    // (<= 2 workgroups per CU) and the Wq rows fit the register budget;
+    // otherwise the two-kernel form
+    const bool coop = a.sync && a.n_chunks * a.H * a.B <= 512 && a.n <= 768;
+#define XA(KC)                                                                                  \
+    case KC:                                                                                    \
+        if (coop) hipLaunchKernelGGL((k_dec_xattn<KC, 1>), grid, dim3(256), 0, s, a);          \
+        else hipLaunchKernelGGL((k_dec_xattn<KC, 0>), grid, dim3(256), 0, s, a);               \
+        break;
     switch (a.n / 128) {
-        case 1: hipLaunchKernelGGL(k_dec_xq_scores<1>, grid, dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL(k_dec_xq_scores<2>, grid, dim3(256), 0, s, a); break;
-        case 3: hipLaunchKernelGGL(k_dec_xq_scores<3>, grid, dim3(256), 0, s, a); break;
-        case 5: hipLaunchKernelGGL(k_dec_xq_scores<5>, grid, dim3(256), 0, s, a); break;
-        case 4: hipLaunchKernelGGL(k_dec_xq_scores<4>, grid, dim3(256), 0, s, a); break;
-        case 6: hipLaunchKernelGGL(k_dec_xq_scores<6>, grid, dim3(256), 0, s, a); break;
-        case 8: hipLaunchKernelGGL(k_dec_xq_scores<8>, grid, dim3(256), 0, s, a); break;
-        case 10: hipLaunchKernelGGL(k_dec_xq_scores<10>, grid, dim3(256), 0, s, a); break;
+        XA(1) XA(2) XA(3) XA(4) XA(5) XA(6) XA(8) XA(10)
         default: return hipErrorInvalidValue;
     }
+#undef XA
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || coop) return e;
     hipLaunchKernelGGL(k_dec_attn_pv, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
