@@ -128,6 +128,15 @@ int wmi_decode_greedy(wmi_context *ctx, int max_tokens, int suppress_eot,
  * time from position 0 and writes logits[n][n_vocab] (f32). */
 int wmi_decode_logits(wmi_context *ctx, int clip, const int32_t *tokens, int n_tokens, float *logits);
 
+/* Beam search (config C5; absent from the reference, semantics after OpenAI
+ * whisper's BeamSearchDecoder without length penalty, stated in
+ * oracle/wmi_oracle.h).  beam_size <= 8; one clip at a time, beam_size decoder
+ * rows.  tokens is [n_clips][max_tokens]: the best hypothesis (ending in EOT
+ * if it finished); n_tokens[c] its length; scores[c] (optional) its summed
+ * log-probability. */
+int wmi_decode_beam(wmi_context *ctx, int beam_size, int max_tokens, int suppress_eot, int32_t *tokens,
+                    int32_t *n_tokens, double *scores);
+
 /* Transcribe: pcm_to_mel -> encode -> decode_greedy for one clip. */
 int wmi_full(wmi_context *ctx, const float *pcm, size_t n_samples, int max_tokens,
              int32_t *tokens, int32_t *n_tokens);
@@ -139,6 +148,8 @@ int wmi_stage_pcm(wmi_context *ctx, int n_clips, const float *const *pcm, const 
 /* mel -> encode -> cross-KV -> decode (n_decode tokens, EOT suppressed) on
  * the staged clips; token ids stay on the device until wmi_get_tokens. */
 int wmi_run_staged(wmi_context *ctx, int mel_offset, int n_decode);
+/* Same with beam search of beam_size (EOT suppressed, exactly n_decode tokens). */
+int wmi_run_staged_beam(wmi_context *ctx, int mel_offset, int n_decode, int beam_size);
 int wmi_get_tokens(const wmi_context *ctx, int32_t *tokens, size_t cap, int32_t *n_per_clip);
 int wmi_get_timings(const wmi_context *ctx, wmi_timings *out);
 /* Block until all work queued on the context's stream is done. */

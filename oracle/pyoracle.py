@@ -43,6 +43,8 @@ def lib():
         L.or_encode.argtypes = [vp, fp, i32, C.c_int, C.c_int, C.c_int, fp, hp_, hp_, C.c_void_p]
         L.or_decode_logits.argtypes = [vp, hp_, hp_, C.c_int, ip, C.c_int, C.c_int, fp]
         L.or_decode_greedy.argtypes = [vp, hp_, hp_, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.POINTER(i32), fp]
+        L.or_decode_beam.argtypes = [vp, hp_, hp_, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.POINTER(i32),
+                                     C.POINTER(C.c_double), C.POINTER(C.c_float)]
         _lib = L
     return _lib
 
@@ -141,3 +143,15 @@ class OracleModel:
         if rc:
             raise OracleError(rc, "decode_greedy")
         return toks[:n.value], margins[:n.value]
+
+    def decode_beam(self, ck, cv, beam: int, max_tokens: int, suppress_eot: bool = False, n_threads: int = 8):
+        """Beam search (wmi_oracle.h): (tokens, score, smallest selection margin)."""
+        toks = np.zeros(max_tokens + 1, np.int32)
+        n = C.c_int32()
+        score = C.c_double()
+        gap = C.c_float()
+        rc = lib().or_decode_beam(self.h, ck, cv, ck.shape[1], beam, max_tokens, int(suppress_eot), n_threads, toks,
+                                  C.byref(n), C.byref(score), C.byref(gap))
+        if rc:
+            raise OracleError(rc, "decode_beam")
+        return toks[:n.value], score.value, gap.value

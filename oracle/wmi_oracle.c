@@ -944,3 +944,167 @@ int or_decode_greedy(const or_model *m, const uint16_t *cross_k, const uint16_t 
     dec_fini(&st);
     return WMI_OK;
 }
+
+/* ------------------------------------------------------------------------ */
+/* beam search (config C5).  Absent from the reference and from whisper.cpp  */
+/* 1.0.3; the semantics are defined in wmi_oracle.h (after OpenAI whisper's  */
+/* BeamSearchDecoder without length penalty) and restated by the HIP path.   */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    double score;
+    int beam, rank, id;
+} beam_cand;
+
+/* (score desc, beam asc, rank asc): a stable sort of beam-major, top-k-order insertion by score */
+static int cand_before(const beam_cand *a, const beam_cand *b) {
+    if (a->score != b->score) return a->score > b->score;
+    if (a->beam != b->beam) return a->beam < b->beam;
+    return a->rank < b->rank;
+}
+
+/* top k of lg[0..V) by (value desc, id asc) */
+static void topk_row(const float *lg, int V, int k, int *ids) {
+    for (int i = 0; i < k; ++i) ids[i] = -1;
+    for (int v = 0; v < V; ++v) {
+        const float x = lg[v];
+        int p = k;
+        while (p > 0 && (ids[p - 1] < 0 || x > lg[ids[p - 1]])) --p;
+        if (p == k) continue;
+        for (int j = k - 1; j > p; --j) ids[j] = ids[j - 1];
+        ids[p] = v;
+    }
+}
+
+static double row_lse(const float *lg, int V) {
+    float mx = -INFINITY;
+    for (int v = 0; v < V; ++v) mx = lg[v] > mx ? lg[v] : mx;
+    double s = 0.0;
+    for (int v = 0; v < V; ++v) s += exp((double)lg[v] - (double)mx);
+    return (double)mx + log(s);
+}
+
+int or_decode_beam(const or_model *m, const uint16_t *cross_k, const uint16_t *cross_v, int n_ctx, int beam,
+                   int max_tokens, int suppress_eot, int nt, int32_t *tokens_out, int32_t *n_out, double *score_out,
+                   float *min_gap) {
+    if (n_ctx <= 0) n_ctx = m->hp[HP_N_AUDIO_CTX];
+    if (beam < 1 || beam > 8 || max_tokens < 1) return WMI_E_INVALID_ARG;
+    int32_t prompt[8];
+    const int np = or_prompt(m, prompt);
+    if (np + max_tokens > m->hp[HP_N_TEXT_CTX]) return WMI_E_INVALID_ARG;
+    const int K = beam, eot = m->sp[0];
+    dec_state *st = calloc(2 * K, sizeof(dec_state));
+    for (int i = 0; i < 2 * K; ++i) dec_init(m, &st[i], n_ctx);
+    dec_state *cur = st, *nxt = st + K;
+    const int V = st[0].V, n = st[0].n, L = st[0].L, tctx = st[0].n_text_ctx;
+    float *lg = malloc(sizeof(float) * V * K);
+    int32_t *hist = calloc((size_t)K * max_tokens, 4), *nhist = calloc((size_t)K * max_tokens, 4);
+    int32_t *fin_tok = calloc((size_t)K * (max_tokens + 1), 4);
+    int fin_len[8], n_fin = 0;
+    double fin_score[8], score[8], nscore[8];
+    int32_t tok[8], ntok[8], parent[8];
+    beam_cand *cands = malloc(sizeof(beam_cand) * K * (K + 1));
+    float gap = INFINITY;
+    int pos = 0;
+    for (; pos < np - 1; ++pos) dec_step(m, &cur[0], cross_k, cross_v, n_ctx, prompt[pos], pos, lg, nt);
+    int n_active = 1, t = 0;
+    tok[0] = prompt[np - 1];
+    score[0] = 0.0;
+    for (t = 0; t < max_tokens && n_fin < K; ++t, ++pos) {
+        int nc = 0;
+        for (int b = 0; b < n_active; ++b) {
+            float *row = lg + (size_t)b * V;
+            dec_step(m, &cur[b], cross_k, cross_v, n_ctx, tok[b], pos, row, nt);
+            if (suppress_eot) row[eot] = -INFINITY;
+            const double lse = row_lse(row, V);
+            int ids[9];
+            topk_row(row, V, K + 1, ids);
+            for (int r = 0; r <= K; ++r) {
+                cands[nc].score = score[b] + ((double)row[ids[r]] - lse);
+                cands[nc].beam = b;
+                cands[nc].rank = r;
+                cands[nc].id = ids[r];
+                ++nc;
+            }
+        }
+        /* insertion sort by the ranking key (nc <= 72) */
+        for (int i = 1; i < nc; ++i) {
+            beam_cand c = cands[i];
+            int j = i;
+            while (j > 0 && cand_before(&c, &cands[j - 1])) { cands[j] = cands[j - 1]; --j; }
+            cands[j] = c;
+        }
+        int na = 0, i = 0;
+        for (; i < nc && na < K; ++i) {
+            const beam_cand *c = &cands[i];
+            if (c->id == eot) {
+                if (n_fin < K) {
+                    memcpy(fin_tok + (size_t)n_fin * (max_tokens + 1), hist + (size_t)c->beam * max_tokens, 4 * t);
+                    fin_tok[(size_t)n_fin * (max_tokens + 1) + t] = eot;
+                    fin_len[n_fin] = t;
+                    fin_score[n_fin] = c->score;
+                    ++n_fin;
+                }
+                continue;
+            }
+            parent[na] = c->beam;
+            ntok[na] = c->id;
+            nscore[na] = c->score;
+            ++na;
+        }
+        /* selection margin: last kept active vs the next non-EOT candidate */
+        for (; i < nc; ++i)
+            if (cands[i].id != eot) {
+                const float g = (float)(nscore[na - 1] - cands[i].score);
+                gap = g < gap ? g : gap;
+                break;
+            }
+        for (int s = 0; s < na; ++s) {
+            const int p = parent[s];
+            memcpy(nhist + (size_t)s * max_tokens, hist + (size_t)p * max_tokens, 4 * t);
+            nhist[(size_t)s * max_tokens + t] = ntok[s];
+            for (int l = 0; l < L; ++l) {
+                const size_t off = (size_t)l * tctx * n;
+                memcpy(nxt[s].mk + off, cur[p].mk + off, (size_t)(pos + 1) * n * 2);
+                memcpy(nxt[s].mv + off, cur[p].mv + off, (size_t)(pos + 1) * n * 2);
+            }
+            tok[s] = ntok[s];
+            score[s] = nscore[s];
+        }
+        dec_state *tmp = cur; cur = nxt; nxt = tmp;
+        int32_t *th = hist; hist = nhist; nhist = th;
+        n_active = na;
+    }
+    /* final ranking: finished first (in order), then active in slot order, up to K */
+    int best_src = -1, best_i = 0;
+    double best = -INFINITY, second = -INFINITY;
+    int considered = 0;
+    for (int f = 0; f < n_fin && considered < K; ++f, ++considered) {
+        const double sc = fin_score[f] / (double)(fin_len[f] > 0 ? fin_len[f] : 1);
+        if (sc > best) { second = best; best = sc; best_src = 0; best_i = f; }
+        else if (sc > second) second = sc;
+    }
+    for (int s = 0; s < n_active && considered < K; ++s, ++considered) {
+        const double sc = score[s] / (double)(t > 0 ? t : 1);
+        if (sc > best) { second = best; best = sc; best_src = 1; best_i = s; }
+        else if (sc > second) second = sc;
+    }
+    int nout;
+    if (best_src == 0) {
+        nout = fin_len[best_i] + 1;
+        memcpy(tokens_out, fin_tok + (size_t)best_i * (max_tokens + 1), 4 * nout);
+        if (score_out) *score_out = fin_score[best_i];
+    } else {
+        nout = t;
+        memcpy(tokens_out, hist + (size_t)best_i * max_tokens, 4 * nout);
+        if (score_out) *score_out = score[best_i];
+    }
+    if (isfinite(second)) {
+        const float g = (float)(best - second);
+        gap = g < gap ? g : gap;
+    }
+    *n_out = nout;
+    if (min_gap) *min_gap = gap;
+    for (int i = 0; i < 2 * K; ++i) dec_fini(&st[i]);
+    free(st); free(lg); free(hist); free(nhist); free(fin_tok); free(cands);
+    return WMI_OK;
+}

@@ -65,6 +65,29 @@ int or_decode_greedy(const or_model *m, const uint16_t *cross_k, const uint16_t 
                      int max_tokens, int suppress_eot, int n_threads,
                      int32_t *tokens_out, int32_t *n_out, float *margins);
 
+/* Beam search (config C5).  Absent from the reference and from whisper.cpp
+ * 1.0.3, so the semantics are defined here, after OpenAI whisper's
+ * BeamSearchDecoder without length penalty (parity unpinned beyond this
+ * restatement):
+ *  - K = beam hypotheses; step 0 expands hypothesis 0 (the prompt) only;
+ *  - each active hypothesis b contributes its top K+1 tokens by logit
+ *    (ties: lower id), scored score_b + (logit - lse_b), lse_b = max +
+ *    log(sum exp(logit - max)) in double over all n_vocab logits (EOT at -inf
+ *    when suppressed);
+ *  - candidates ranked by (score desc, beam asc, rank asc); walking the
+ *    ranking, an EOT candidate finishes its hypothesis (kept while fewer than
+ *    K have finished), any other fills the next active slot, until K slots
+ *    are filled;
+ *  - stops when K hypotheses have finished or max_tokens steps ran; the
+ *    result is the best score / length (length excludes EOT) among the first
+ *    K of: finished hypotheses in order, then active ones in slot order.
+ * tokens_out receives the chosen sequence (with its EOT if finished);
+ * min_gap (optional) the smallest selection margin met (last kept vs first
+ * rejected candidate at every step, best vs second in the final choice). */
+int or_decode_beam(const or_model *m, const uint16_t *cross_k, const uint16_t *cross_v, int n_ctx, int beam,
+                   int max_tokens, int suppress_eot, int n_threads, int32_t *tokens_out, int32_t *n_out,
+                   double *score_out, float *min_gap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2,7 +2,7 @@
 
 Tolerances (north_star "within 1e-3 on encoder activations"): max abs error
 <= max(1e-3, 1.25 x the arithmetic's own noise floor) and mean abs error
-<= 3e-4.  The noise floor is measured in the test: the same CPU restatement
+<= max(3e-4, 1.25 x the floor's mean).  The noise floor is measured in the test: the same CPU restatement
 run with exact (double) dot products instead of ggml's AVX2 f32 accumulation
 order.  At base that floor is 1.34e-3 max / 1.9e-4 mean — an absolute 1e-3
 bound is below what ANY reordering of the same f16/f32 arithmetic achieves
@@ -84,6 +84,7 @@ def _check_encoder(ctx, om, pcm, n_ctx, mel_offset=0):
         pyoracle.set_dot_mode(False)
     enc_ref, ck_ref, cv_ref = om.encode(mel, n_ctx=n_ctx, mel_offset=mel_offset, n_threads=threads())
     floor = np.abs(enc_exact - enc_ref).max()
+    floor_mean = np.abs(enc_exact - enc_ref).mean()
     ctx.set_audio_ctx(n_ctx)
     ctx.pcm_to_mel_batch([pcm])
     ctx.encode(1, mel_offset)
@@ -91,7 +92,7 @@ def _check_encoder(ctx, om, pcm, n_ctx, mel_offset=0):
     assert enc.shape == enc_ref.shape
     err = np.abs(enc - enc_ref)
     assert err.max() <= max(ENC_TOL, 1.25 * floor), (err.max(), floor)
-    assert err.mean() <= 3e-4, err.mean()
+    assert err.mean() <= max(3e-4, 1.25 * floor_mean), (err.mean(), floor_mean)
     ck, cv = ctx.cross_kv(0)
     # cross K/V are f16 projections of the encoder output: same absolute
     # budget plus one f16 rounding of the stored value
@@ -182,6 +183,136 @@ def test_full_size_models(wmi, model_cache, model):
         near = np.nonzero(margins < 1e-3)[0]
         upto = near[0] + 1 if near.size else len(ref)
         np.testing.assert_array_equal(got[:upto], ref[:upto])
+    finally:
+        ctx.close()
+        om.close()
+
+
+# --- beam search (config C5; semantics restated in oracle/wmi_oracle.h) ------
+BEAM_GAP = 2e-3  # selection margins below this may flip under f32 reordering
+
+
+def _beam_case(ctx, om, seeds, K, n_tok, suppress_eot, n_ctx=64, secs=2.0):
+    """First seed whose oracle beam search has no near-tie selection (margin
+    < BEAM_GAP) anywhere; the HIP path must then reproduce it exactly."""
+    for seed in seeds:
+        pcm = synth.synth_pcm_f32(secs, seed)
+        mel = om.mel(pcm, n_threads=threads())
+        _, ck, cv = om.encode(mel, n_ctx=n_ctx, n_threads=threads())
+        ref, score, gap = om.decode_beam(ck, cv, K, n_tok, suppress_eot=suppress_eot, n_threads=threads())
+        if gap >= BEAM_GAP:
+            ctx.set_audio_ctx(n_ctx)
+            ctx.pcm_to_mel_batch([pcm])
+            ctx.encode(1, 0)
+            got, got_score = ctx.decode_beam(K, n_tok, suppress_eot=suppress_eot)[0]
+            return ref, score, got, got_score
+    pytest.skip(f"no seed without a near-tie selection in {list(seeds)}")
+
+
+@pytest.mark.parametrize("K", [1, 2, 3])
+def test_beam_search_micro(micro_ctx, oracle_micro, K):
+    ref, score, got, got_score = _beam_case(micro_ctx, oracle_micro, range(100, 130), K, 20, True)
+    np.testing.assert_array_equal(got, ref)
+    assert abs(got_score - score) < 1e-2
+
+
+def test_beam_search_tiny_en_beam5(wmi, model_cache):
+    """C5's beam width on a full-size model (the micro model's logits barely
+    depend on the audio, so its 5-beam selections are all near-ties)."""
+    path = synth.model_path("tiny.en", model_cache)
+    om = pyoracle.OracleModel(path)
+    ctx = wmi.WhisperContext.new(path, 0, max_clips=1)
+    try:
+        ref, score, got, got_score = _beam_case(ctx, om, range(1234, 1240), 5, 16, True, n_ctx=1500, secs=30.0)
+        np.testing.assert_array_equal(got, ref)
+        assert abs(got_score - score) < 1e-2
+    finally:
+        ctx.close()
+        om.close()
+
+
+def test_beam_one_equals_greedy(micro_ctx):
+    micro_ctx.set_audio_ctx(64)
+    micro_ctx.pcm_to_mel_batch([synth.synth_pcm_f32(2.0, 4)])
+    micro_ctx.encode(1, 0)
+    g = micro_ctx.decode_greedy(16, suppress_eot=True)[0]
+    b, _ = micro_ctx.decode_beam(1, 16, suppress_eot=True)[0]
+    np.testing.assert_array_equal(b, g)
+
+
+@pytest.fixture(scope="module")
+def eot_twin_model(model_cache):
+    """micro with EOT's embedding row equal to the row greedy keeps choosing:
+    EOT then ties the best candidate every step, so hypotheses finish and the
+    finished-list / early-stop logic runs (exact ties, identical on both sides)."""
+    import os
+    path = os.path.join(model_cache, "ggml-synth-micro-eot-twin.bin")
+    if not os.path.exists(path):
+        def hook(name, arr):
+            if name == "decoder.token_embedding.weight":
+                arr = arr.copy()
+                arr[50256] = arr[48938]
+            return arr
+        synth.write_ggml(path, "micro", tensor_hook=hook)
+    return path
+
+
+def test_beam_search_finishing(wmi, eot_twin_model):
+    om = pyoracle.OracleModel(eot_twin_model)
+    ctx = wmi.WhisperContext.new(eot_twin_model, 0, max_clips=1)
+    try:
+        for K in (2, 4):
+            ref, score, got, got_score = _beam_case(ctx, om, range(200, 230), K, 30, False)
+            assert ref[-1] == om.special["eot"]  # a finished hypothesis won
+            np.testing.assert_array_equal(got, ref)
+            assert abs(got_score - score) < 1e-2
+    finally:
+        ctx.close()
+        om.close()
+
+
+def test_base_batch_of_8_equals_single(wmi, model_cache):
+    """C4's per-GPU shard: 8 x 30 s clips through the batched encoder (M =
+    12000 rows per GEMM) and 8 decoder rows give bitwise the single-clip
+    results (which the full-size test pins to the oracle)."""
+    ctx = wmi.WhisperContext.new(synth.model_path("base", model_cache), 0, max_clips=8)
+    try:
+        clips = [synth.synth_pcm_f32(30.0, 1234 + i) for i in range(8)]
+        ctx.pcm_to_mel_batch(clips)
+        ctx.encode(1, 0)
+        enc_b = [ctx.encoder_out(i) for i in range(8)]
+        tok_b = ctx.decode_greedy(12, suppress_eot=True)
+        for i in (0, 3, 7):
+            ctx.pcm_to_mel_batch([clips[i]])
+            ctx.encode(1, 0)
+            np.testing.assert_array_equal(ctx.encoder_out(0), enc_b[i])
+            np.testing.assert_array_equal(ctx.decode_greedy(12, suppress_eot=True)[0], tok_b[i])
+    finally:
+        ctx.close()
+
+
+@pytest.mark.slow
+def test_large_v3(wmi, model_cache):
+    """C5's model: 128 mels, vocab 51866 (multilingual specials shifted by one
+    more id), n_state 1280 / 20 heads / 32 + 32 layers; encoder at the noise
+    floor, greedy ids, and 5-beam search when its selections are decisive."""
+    path = synth.model_path("large-v3", model_cache)
+    om = pyoracle.OracleModel(path)
+    ctx = wmi.WhisperContext.new(path, 0, max_clips=1)
+    try:
+        assert ctx.hparams["n_mels"] == 128 and ctx.hparams["n_vocab"] == 51866
+        pcm = synth.synth_pcm_f32(30.0, 1234)
+        _, ck_ref, cv_ref = _check_encoder(ctx, om, pcm, 1500)
+        ref, margins = om.decode_greedy(ck_ref, cv_ref, 12, suppress_eot=True, n_threads=threads())
+        got = ctx.decode_greedy(12, suppress_eot=True)[0]
+        near = np.nonzero(margins < 1e-3)[0]
+        upto = near[0] + 1 if near.size else len(ref)
+        np.testing.assert_array_equal(got[:upto], ref[:upto])
+        bref, bscore, gap = om.decode_beam(ck_ref, cv_ref, 5, 6, suppress_eot=True, n_threads=threads())
+        bgot, bgot_score = ctx.decode_beam(5, 6, suppress_eot=True)[0]
+        if gap >= BEAM_GAP:
+            np.testing.assert_array_equal(bgot, bref)
+        assert abs(bgot_score - bscore) < 2e-2
     finally:
         ctx.close()
         om.close()

@@ -177,6 +177,13 @@ struct wmi_context {
     uint16_t *dq16 = nullptr, *datt16 = nullptr, *dhid16 = nullptr;
     float *dS = nullptr, *dcmax = nullptr, *dopart = nullptr;
     XSync *dsync = nullptr;     // [n_text_layer][8][n_text_head]
+    // beam search (config C5)
+    BeamPart *dbparts = nullptr;
+    BeamState *dbstate = nullptr;
+    int32_t *dkvsrc = nullptr, *dhist_par = nullptr, *dhist_tok = nullptr;
+    std::vector<int32_t> kvsrc_init;
+    int beam_k = 0;             // > 0 while enqueueing a beam-search step
+    int beam_max_tokens = 0;
     uint32_t *derr = nullptr;
     size_t sync_bytes = 0;
     int s_stride = 0, n_chunks_max = 0;
@@ -203,6 +210,7 @@ struct wmi_context {
     int cur_ctx = 0;   // exp_n_audio_ctx
     // staged decode results
     int staged_n_decode = 0;
+    std::vector<std::vector<int32_t>> staged_beam;  // host results of a staged beam search
     // timings
     hipEvent_t ev[8] = {};
     wmi_timings timings{};
@@ -651,15 +659,22 @@ int alloc_workspace(wmi_context *ctx) {
     const size_t o_enc16 = A.take(B * T * n * 2);
     const size_t o_ck = A.take(Lt * B * T * nt * 2);
     const size_t o_cv = A.take(Lt * B * T * nt * 2);
-    const size_t o_kc = A.take(Lt * B * hp.n_text_ctx * nt * 2);
-    const size_t o_vc = A.take(Lt * B * hp.n_text_ctx * nt * 2);
-    const size_t o_dx = A.take(B * nt * 4);
-    const size_t o_dq = A.take(B * nt * 2);
-    const size_t o_datt = A.take(B * nt * 2);
-    const size_t o_dhid = A.take(B * 4 * nt * 2);
-    const size_t o_dlog = A.take(B * (int64_t)hp.n_vocab * 4);
+    // decoder rows: up to DEC_ROWS clips (greedy) or beam hypotheses at a time
+    const int64_t R = DEC_ROWS;
+    const size_t o_kc = A.take(Lt * R * hp.n_text_ctx * nt * 2);
+    const size_t o_vc = A.take(Lt * R * hp.n_text_ctx * nt * 2);
+    const size_t o_dx = A.take(R * nt * 4);
+    const size_t o_dq = A.take(R * nt * 2);
+    const size_t o_datt = A.take(R * nt * 2);
+    const size_t o_dhid = A.take(R * 4 * nt * 2);
+    const size_t o_dlog = A.take(R * (int64_t)hp.n_vocab * 4);
     const int64_t Smax = up(hp.n_audio_ctx > hp.n_text_ctx ? hp.n_audio_ctx : hp.n_text_ctx, 128);
-    const int64_t Cmax = Smax / 128, Hd = hp.n_text_head, Bd = B < 8 ? B : 8;
+    const int64_t Cmax = Smax / 128, Hd = hp.n_text_head, Bd = R;
+    const size_t o_bparts = A.take(R * BEAM_NS * sizeof(BeamPart));
+    const size_t o_bstate = A.take(sizeof(BeamState));
+    const size_t o_kvsrc = A.take(R * hp.n_text_ctx * 4);
+    const size_t o_hpar = A.take((size_t)hp.n_text_ctx * BEAM_MAX * 4);
+    const size_t o_htok = A.take((size_t)hp.n_text_ctx * BEAM_MAX * 4);
     const size_t o_S = A.take(Bd * Hd * Smax * 4);
     const size_t o_cmax = A.take(Bd * Hd * Cmax * 4);
     const size_t o_opart = A.take(Bd * Cmax * nt * 4);
@@ -698,6 +713,14 @@ int alloc_workspace(wmi_context *ctx) {
     ctx->dS = (float *)(b + o_S);
     ctx->dcmax = (float *)(b + o_cmax);
     ctx->dopart = (float *)(b + o_opart);
+    ctx->dbparts = (BeamPart *)(b + o_bparts);
+    ctx->dbstate = (BeamState *)(b + o_bstate);
+    ctx->dkvsrc = (int32_t *)(b + o_kvsrc);
+    ctx->dhist_par = (int32_t *)(b + o_hpar);
+    ctx->dhist_tok = (int32_t *)(b + o_htok);
+    ctx->kvsrc_init.resize((size_t)R * hp.n_text_ctx);
+    for (int64_t r = 0; r < R; ++r)
+        for (int j = 0; j < hp.n_text_ctx; ++j) ctx->kvsrc_init[(size_t)r * hp.n_text_ctx + j] = (int32_t)r;
     ctx->dsync = (XSync *)(b + o_sync);
     ctx->derr = (uint32_t *)(b + o_sync + sync_bytes);
     ctx->sync_bytes = sync_bytes + 256;
@@ -896,12 +919,13 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     hipStream_t s = ctx->stream;
     const float qs = powf((float)n / (float)H, -0.25f);
     ctx->trace_names.clear();
+    const bool beam = ctx->beam_k > 0;
     // per layer: [LN+QKV (+embed at l=0)] [self-attn] [Wo+res] [LN+Wcq+cross scores]
     //            [cross softmax+PV] [Wco+res] [LN+W0+GELU] [W1+res]; then LN+logits+argmax
     for (int l = 0; l < hp.n_text_layer; ++l) {
         const DecLayerDev &d = ctx->dec[l];
-        uint16_t *kc = ctx->kcache + (size_t)l * ctx->max_clips * hp.n_text_ctx * n;
-        uint16_t *vc = ctx->vcache + (size_t)l * ctx->max_clips * hp.n_text_ctx * n;
+        uint16_t *kc = ctx->kcache + (size_t)l * DEC_ROWS * hp.n_text_ctx * n;
+        uint16_t *vc = ctx->vcache + (size_t)l * DEC_ROWS * hp.n_text_ctx * n;
         DecGemvArgs g{};
         g.x = ctx->dx; g.ln_w = d.ln1_w; g.ln_b = d.ln1_b; g.W = d.wqkv; g.bias = d.bqkv; g.N = 3 * n; g.K = n; g.B = B;
         g.qscale = qs; g.out16 = ctx->dq16; g.ldo = n; g.kcache = kc; g.vcache = vc; g.n_text_ctx = hp.n_text_ctx;
@@ -910,6 +934,10 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
             g.te = ctx->te; g.pe = ctx->d_pe; g.feed = ctx->dfeed; g.feed_len = feed_len; g.feed_stride = feed_stride;
             g.amax = ctx->damax; g.tokens_out = ctx->dtokens + (size_t)b0 * out_stride; g.out_stride = out_stride;
             g.x_out = ctx->dx;
+            if (beam) {
+                g.tokens_out = nullptr;
+                g.beam_tok = ctx->dbstate->tok;
+            }
         }
         g.trace = tslot(ctx, "qkv", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_QKV, g));
@@ -918,7 +946,12 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         at.st = ctx->dstate; at.S = ctx->dS; at.s_stride = ctx->s_stride; at.cmax = ctx->dcmax;
         at.opart = ctx->dopart; at.n_chunks = 1; at.exp_tab = ctx->exp_tab; at.n_exp = ctx->n_exp;
         at.H = H; at.n = n; at.B = B;
-        at.reset_amax = l == 0 ? ctx->damax : nullptr;
+        at.reset_amax = (l == 0 && !beam) ? ctx->damax : nullptr;
+        at.clip_div = 1;
+        if (beam) {
+            at.kv_src = ctx->dkvsrc;
+            at.kv_src_stride = hp.n_text_ctx;
+        }
         at.trace = tslot(ctx, "self_attn", l);
         HIPCHK(ctx, launch_dec_attn(s, at));
         g = DecGemvArgs{};
@@ -936,6 +969,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         at.x = ctx->dx; at.ln_w = d.lnc_w; at.ln_b = d.lnc_b; at.Wq = d.wcq; at.bq = d.bcq; at.qscale = qs;
         at.sync = ctx->use_coop ? ctx->dsync + (size_t)l * 8 * H : nullptr;
         at.err = ctx->derr;
+        at.clip_div = beam ? B : 1;  // beam rows all read clip b0's cross K/V
         at.trace = tslot(ctx, "cross_attn", l);
         at.phase = ctx->trace_on ? ctx->d_trace + 2 * TRACE_SLOTS + 16 * l : nullptr;
         HIPCHK(ctx, launch_dec_attn(s, at));
@@ -959,7 +993,17 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     g.out32 = ctx->dlogits; g.amax = ctx->damax; g.suppress_id = suppress_eot ? ctx->sp.eot : -1;
     g.st_advance = ctx->dstate;
     g.trace = tslot(ctx, "logits", 0);
+    if (beam) g.amax = nullptr;
     HIPCHK(ctx, launch_dec_gemv(s, DEC_LOGITS, g));
+    if (beam) {
+        BeamArgs ba{};
+        ba.logits = ctx->dlogits; ba.V = hp.n_vocab; ba.K = ctx->beam_k; ba.suppress_id = suppress_eot ? ctx->sp.eot : -1;
+        ba.eot = ctx->sp.eot; ba.feed_len = feed_len; ba.max_tokens = ctx->beam_max_tokens; ba.tctx = hp.n_text_ctx;
+        ba.st = ctx->dstate; ba.parts = ctx->dbparts; ba.bs = ctx->dbstate; ba.kv_src = ctx->dkvsrc;
+        ba.hist_parent = ctx->dhist_par; ba.hist_tok = ctx->dhist_tok;
+        ba.trace = tslot(ctx, "beam", 0);
+        HIPCHK(ctx, launch_beam_step(s, ba));
+    }
     return WMI_OK;
 }
 
@@ -992,8 +1036,9 @@ int run_dec_steps(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride
         return WMI_OK;
     }
     char key[160];
-    snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%p/%p", b0, B, feed_len, feed_stride, suppress_eot, out_stride,
-             ctx->enc_T, ctx->enc_clips, (void *)ctx->dfeed, (void *)ctx->dtokens);
+    snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%p/%p/%d/%d", b0, B, feed_len, feed_stride, suppress_eot,
+             out_stride, ctx->enc_T, ctx->enc_clips, (void *)ctx->dfeed, (void *)ctx->dtokens, ctx->beam_k,
+             ctx->beam_max_tokens);
     if (ctx->g_key != key) {
         if (ctx->g_exec) { (void)hipGraphExecDestroy(ctx->g_exec); ctx->g_exec = nullptr; }
         if (ctx->g_graph) { (void)hipGraphDestroy(ctx->g_graph); ctx->g_graph = nullptr; }
@@ -1096,6 +1141,101 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
 }
 
 bool valid(const wmi_context *ctx) { return ctx != nullptr && ctx->d_model != nullptr; }
+
+
+// beam search (config C5) of every encoded clip, one clip (K decoder rows) at
+// a time; per-clip best hypothesis (tokens, score) on the host
+int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_stop,
+             std::vector<std::vector<int32_t>> *out_tokens, std::vector<double> *out_scores) {
+    const int Bt = ctx->enc_clips;
+    const wmi_hparams &hp = ctx->hp;
+    if (ctx->enc_T <= 0 || Bt < 1) return set_err(ctx, WMI_E_INVALID_ARG, "decode before encode");
+    if (K < 1 || K > BEAM_MAX) return set_err(ctx, WMI_E_INVALID_ARG, "beam size %d outside [1, %d]", K, BEAM_MAX);
+    int32_t prompt[8];
+    const int np = prompt_tokens(ctx, prompt);
+    if (n_gen < 1 || np + n_gen > hp.n_text_ctx)
+        return set_err(ctx, WMI_E_INVALID_ARG, "max_tokens %d: prompt %d + tokens must fit n_text_ctx %d", n_gen, np,
+                       hp.n_text_ctx);
+    int rc = ensure_decode_buffers(ctx, 8 * np, 1);
+    if (rc) return rc;
+    std::vector<int32_t> feed(8 * np);
+    for (int b = 0; b < 8; ++b)
+        for (int i = 0; i < np; ++i) feed[b * np + i] = prompt[i];
+    HIPCHK(ctx, hipMemcpy(ctx->dfeed, feed.data(), feed.size() * 4, hipMemcpyHostToDevice));
+    BeamState init{};
+    init.n_active = 1;
+    if (out_tokens) out_tokens->assign(Bt, {});
+    if (out_scores) out_scores->assign(Bt, 0.0);
+    ctx->beam_k = K;
+    ctx->beam_max_tokens = n_gen;
+    struct Reset { wmi_context *c; ~Reset() { c->beam_k = 0; } } reset{ctx};
+    for (int clip = 0; clip < Bt; ++clip) {
+        HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
+        HIPCHK(ctx, hipMemsetAsync(ctx->dsync, 0, ctx->sync_bytes, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->dbstate, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->dkvsrc, ctx->kvsrc_init.data(), ctx->kvsrc_init.size() * 4,
+                                   hipMemcpyHostToDevice, ctx->stream));
+        const int total_steps = np + n_gen - 1;
+        int done_steps = 0;
+        while (done_steps < total_steps) {
+            int chunk = total_steps - done_steps;
+            if (early_stop && chunk > 32) chunk = 32;
+            rc = run_dec_steps(ctx, clip, K, np, np, suppress_eot, 1, chunk);
+            if (rc) return rc;
+            done_steps += chunk;
+            if (early_stop && done_steps < total_steps) {
+                int32_t done = 0;
+                HIPCHK(ctx, hipMemcpyAsync(&done, &ctx->dbstate->done, 4, hipMemcpyDeviceToHost, ctx->stream));
+                HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+                if (done) break;
+            }
+        }
+        BeamState bs{};
+        HIPCHK(ctx, hipMemcpyAsync(&bs, ctx->dbstate, sizeof bs, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        const int ns = bs.n_steps;
+        if (ns < 1) return set_err(ctx, WMI_E_HIP, "beam search produced no step");
+        std::vector<int32_t> hpar((size_t)ns * BEAM_MAX), htok((size_t)ns * BEAM_MAX);
+        HIPCHK(ctx, hipMemcpy(hpar.data(), ctx->dhist_par, hpar.size() * 4, hipMemcpyDeviceToHost));
+        HIPCHK(ctx, hipMemcpy(htok.data(), ctx->dhist_tok, htok.size() * 4, hipMemcpyDeviceToHost));
+        auto backtrack = [&](int tlast, int slot) {
+            std::vector<int32_t> seq(tlast + 1);
+            for (int t = tlast; t >= 0; --t) {
+                seq[t] = htok[(size_t)t * BEAM_MAX + slot];
+                slot = hpar[(size_t)t * BEAM_MAX + slot];
+            }
+            return seq;
+        };
+        // finished hypotheses in order, then active ones in slot order, first K
+        double best = -INFINITY;
+        int best_src = -1, best_i = 0, considered = 0;
+        for (int f = 0; f < bs.n_fin && considered < K; ++f, ++considered) {
+            const double sc = bs.fin_score[f] / (double)(bs.fin_t[f] > 0 ? bs.fin_t[f] : 1);
+            if (sc > best) { best = sc; best_src = 0; best_i = f; }
+        }
+        for (int a = 0; a < bs.n_active && considered < K; ++a, ++considered) {
+            const double sc = bs.score[a] / (double)ns;
+            if (sc > best) { best = sc; best_src = 1; best_i = a; }
+        }
+        std::vector<int32_t> seq;
+        double score;
+        if (best_src == 0) {
+            const int t = bs.fin_t[best_i];
+            if (t > 0) seq = backtrack(t - 1, bs.fin_beam[best_i]);
+            seq.push_back(ctx->sp.eot);
+            score = bs.fin_score[best_i];
+        } else {
+            seq = backtrack(ns - 1, best_i);
+            score = bs.score[best_i];
+        }
+        if (out_tokens) (*out_tokens)[clip] = seq;
+        if (out_scores) (*out_scores)[clip] = score;
+    }
+    uint32_t err = 0;
+    HIPCHK(ctx, hipMemcpy(&err, ctx->derr, 4, hipMemcpyDeviceToHost));
+    if (err) return set_err(ctx, WMI_E_HIP, "cross-attention exchange timed out (workgroups not co-resident)");
+    return WMI_OK;
+}
 
 }  // namespace
 
@@ -1303,6 +1443,22 @@ int wmi_decode_logits(wmi_context *ctx, int clip, const int32_t *tokens, int n_t
     return WMI_OK;
 }
 
+int wmi_decode_beam(wmi_context *ctx, int beam_size, int max_tokens, int suppress_eot, int32_t *tokens,
+                    int32_t *n_tokens, double *scores) {
+    if (!valid(ctx) || !tokens || !n_tokens) return WMI_E_INVALID_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    std::vector<std::vector<int32_t>> tk;
+    std::vector<double> sc;
+    int rc = run_beam(ctx, beam_size, max_tokens, suppress_eot, !suppress_eot, &tk, &sc);
+    if (rc) return rc;
+    for (size_t c = 0; c < tk.size(); ++c) {
+        memcpy(tokens + c * max_tokens, tk[c].data(), tk[c].size() * 4);
+        n_tokens[c] = (int32_t)tk[c].size();
+        if (scores) scores[c] = sc[c];
+    }
+    return WMI_OK;
+}
+
 int wmi_full(wmi_context *ctx, const float *pcm, size_t n_samples, int max_tokens, int32_t *tokens, int32_t *n_tokens) {
     int rc = wmi_pcm_to_mel(ctx, pcm, n_samples);
     if (rc) return rc;
@@ -1317,7 +1473,9 @@ int wmi_stage_pcm(wmi_context *ctx, int n_clips, const float *const *pcm, const 
     return stage_pcm(ctx, n_clips, pcm, n_samples);
 }
 
-int wmi_run_staged(wmi_context *ctx, int mel_offset, int n_decode) {
+int wmi_run_staged(wmi_context *ctx, int mel_offset, int n_decode) { return wmi_run_staged_beam(ctx, mel_offset, n_decode, 0); }
+
+int wmi_run_staged_beam(wmi_context *ctx, int mel_offset, int n_decode, int beam_size) {
     if (!valid(ctx)) return WMI_E_INVALID_ARG;
     if (ctx->n_clips < 1) return set_err(ctx, WMI_E_INVALID_ARG, "nothing staged");
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -1328,7 +1486,12 @@ int wmi_run_staged(wmi_context *ctx, int mel_offset, int n_decode) {
     rc = run_encode(ctx, mel_offset);
     if (rc) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
-    rc = run_greedy(ctx, n_decode, 1, false, nullptr, nullptr);
+    if (beam_size > 0) {
+        rc = run_beam(ctx, beam_size, n_decode, 1, false, &ctx->staged_beam, nullptr);
+    } else {
+        rc = run_greedy(ctx, n_decode, 1, false, nullptr, nullptr);
+        ctx->staged_beam.clear();
+    }
     if (rc) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1347,6 +1510,15 @@ int wmi_get_tokens(const wmi_context *ctx, int32_t *tokens, size_t cap, int32_t 
     if (!ctx || !tokens) return WMI_E_INVALID_ARG;
     const size_t need = (size_t)ctx->enc_clips * ctx->staged_n_decode;
     if (cap < need) return WMI_E_NO_SPACE;
+    if (!ctx->staged_beam.empty()) {  // last staged run was a beam search
+        for (size_t c = 0; c < ctx->staged_beam.size(); ++c) {
+            const std::vector<int32_t> &sq = ctx->staged_beam[c];
+            for (int i = 0; i < ctx->staged_n_decode; ++i)
+                tokens[c * ctx->staged_n_decode + i] = i < (int)sq.size() ? sq[i] : -1;
+            if (n_per_clip) n_per_clip[c] = (int32_t)sq.size();
+        }
+        return WMI_OK;
+    }
     if (hipMemcpy(tokens, ctx->dtokens, need * 4, hipMemcpyDeviceToHost) != hipSuccess) return WMI_E_HIP;
     if (n_per_clip)
         for (int b = 0; b < ctx->enc_clips; ++b) n_per_clip[b] = ctx->staged_n_decode;

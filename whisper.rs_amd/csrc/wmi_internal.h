@@ -125,9 +125,11 @@ struct DecGemvArgs {
     int32_t *tokens_out;        // [B][out_stride], token of pos - feed_len
     int out_stride;
     float *x_out;               // residual stream written by block 0
+    const int32_t *beam_tok;    // beam search: token of row b past the prompt (BeamState::tok), else null
     unsigned long long *trace;  // WMI_TRACE: {min start, ~max end} s_memrealtime of this launch
 };
 constexpr int AMAX_SHARDS = 64;
+constexpr int DEC_ROWS = 8;  // decoder rows per step: clips (greedy) or beam hypotheses
 hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a);
 
 struct DecAttnArgs {
@@ -153,6 +155,12 @@ struct DecAttnArgs {
     // words for this layer, zeroed at the start of every decode run
     struct XSync *sync;
     uint32_t *err;           // set to 1 if an exchange spin times out
+    // beam search: self-attention reads key/value row j < pos of decoder row b
+    // from cache slot kv_src[b * kv_src_stride + j] (its hypothesis' history);
+    // cross-attention rows b share clip b / clip_div
+    const int32_t *kv_src;
+    int kv_src_stride;
+    int clip_div;
     unsigned long long *trace;  // WMI_TRACE slot (see DecGemvArgs)
     unsigned long long *phase;  // WMI_TRACE: [2][8] phase times of the first and last chunk of (head 0, clip 0)
 };
@@ -162,6 +170,34 @@ struct XSync {
     uint32_t pad[15];
 };
 hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a);
+
+// ---- beam search (config C5; semantics in oracle/wmi_oracle.h) -------------
+constexpr int BEAM_MAX = 8, BEAM_NS = 16, BEAM_TK = BEAM_MAX + 1;
+struct BeamPart {            // one vocabulary split of one row
+    float m;                 // split max
+    float pad;
+    double sum;              // sum exp(logit - m) over the split
+    float val[BEAM_TK];      // split top-(K+1) by (value desc, id asc)
+    int32_t id[BEAM_TK];
+};
+struct BeamState {
+    int32_t n_active, n_fin, done, n_steps;
+    double score[BEAM_MAX];      // cumulative log-probability of active slot s
+    int32_t tok[BEAM_MAX];       // token slot s feeds at the next step
+    int32_t fin_t[BEAM_MAX], fin_beam[BEAM_MAX];
+    double fin_score[BEAM_MAX];
+};
+struct BeamArgs {
+    const float *logits;     // [K][V]
+    int V, K, suppress_id, eot, feed_len, max_tokens, tctx;
+    const DecState *st;
+    BeamPart *parts;         // [K][BEAM_NS]
+    BeamState *bs;
+    int32_t *kv_src;         // [K][tctx]
+    int32_t *hist_parent, *hist_tok;  // [max_tokens][BEAM_MAX]
+    unsigned long long *trace;
+};
+hipError_t launch_beam_step(hipStream_t s, const BeamArgs &a);
 
 struct DecEmbedArgs {
     const uint16_t *te;      // [V][n]

@@ -883,7 +883,7 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
                     // x = te[tok] + pe[pos] (get_rows f16 -> f32, add)
                     const bool fed = pos < a.feed_len;
                     const int32_t tok = fed ? a.feed[rb * a.feed_stride + pos]
-                                            : shard_token(a.amax + rb * AMAX_SHARDS, lane);
+                                            : (a.beam_tok ? a.beam_tok[rb] : shard_token(a.amax + rb * AMAX_SHARDS, lane));
                     const f16 *ter = (const f16 *)a.te + (int64_t)tok * K;
                     const float *per = a.pe + (int64_t)pos * K;
                     half4 tv[DG_LNV];
@@ -902,7 +902,7 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
                                       e < K);
                         if (e < K && blockIdx.x == 0) *(float4 *)(a.x_out + (int64_t)rb * K + e) = xv[i];
                     }
-                    if (blockIdx.x == 0 && lane == 0 && !fed)
+                    if (blockIdx.x == 0 && lane == 0 && !fed && a.tokens_out)
                         a.tokens_out[rb * a.out_stride + (pos - a.feed_len)] = tok;
                 }
                 ln_regs_to_lds(xv, K, a.ln_w, a.ln_b, xs + rb * K, lane);
@@ -1002,7 +1002,7 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
                 a.out32[(int64_t)bb * N + o] = (v + ebias[g]) + eres[g];
             } else if (EPI == DEC_LOGITS) {
                 a.out32[(int64_t)bb * N + o] = v;
-                if (o != a.suppress_id) {
+                if (a.amax && o != a.suppress_id) {
                     const unsigned long long key =
                         ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)o);
                     atomicMax(&amax_s[bb], key);
@@ -1024,7 +1024,7 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
     }
     if (EPI == DEC_LOGITS) {
         __syncthreads();
-        if (tid < B && amax_s[tid]) atomicMax(&a.amax[tid * AMAX_SHARDS + (blockIdx.x & (AMAX_SHARDS - 1))], amax_s[tid]);
+        if (a.amax && tid < B && amax_s[tid]) atomicMax(&a.amax[tid * AMAX_SHARDS + (blockIdx.x & (AMAX_SHARDS - 1))], amax_s[tid]);
         if (blockIdx.x == 0 && tid == 0) a.st_advance->pos += 1;
     }
     trace_end(a.trace);
@@ -1212,7 +1212,7 @@ __device__ __forceinline__ void xattn_pv(const DecAttnArgs &a, int c, int h, int
 // this chunk's V rows for xattn_pv (clamped rows: every load unconditional)
 __device__ __forceinline__ void xattn_load_v(const DecAttnArgs &a, int c, int h, int b, int M, half8 (&vf)[4]) {
     const int tid = threadIdx.x, doct = tid & 7, jg = tid >> 3;
-    const f16 *Vb = (const f16 *)a.V + (int64_t)b * a.clip_stride + h * 64 + doct * 8;
+    const f16 *Vb = (const f16 *)a.V + (int64_t)(b / a.clip_div) * a.clip_stride + h * 64 + doct * 8;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int j = c * DA_CK + jg * 4 + u;
@@ -1245,7 +1245,7 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
     const int key = c * DA_CK + (tid >> 1), half = tid & 1;
     half8 kf[4];
     {
-        const f16 *kr = (const f16 *)a.K + (int64_t)b * a.clip_stride + (int64_t)(key < M ? key : M - 1) * n +
+        const f16 *kr = (const f16 *)a.K + (int64_t)(b / a.clip_div) * a.clip_stride + (int64_t)(key < M ? key : M - 1) * n +
                         h * 64 + half * 32;
 #pragma unroll
         for (int i = 0; i < 4; ++i) kf[i] = *(const half8 *)(kr + 8 * i);
@@ -1338,34 +1338,47 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     __shared__ double redd[4];
     __shared__ __attribute__((aligned(16))) uint16_t P[512];
     __shared__ float ored[32][64];
-    const f16 *Kb = (const f16 *)a.K + (int64_t)b * a.clip_stride + h * 64;
-    const f16 *Vb = (const f16 *)a.V + (int64_t)b * a.clip_stride + h * 64;
     const f16 *qr = (const f16 *)a.q + (int64_t)b * n + h * 64;
     if (a.reset_amax && h == 0 && b == 0)
         for (int i = tid; i < a.B * AMAX_SHARDS; i += 256) a.reset_amax[i] = 0ull;
-    // scores: thread t owns keys t and t + 256
+    // cache row of key j: slot b, or (beam search) the slot holding the
+    // hypothesis' history; keys past M load row M - 1 (finite, masked below).
+    // Scores: thread t owns keys t and t + 256; PV: thread owns d-octet
+    // (tid & 7) and keys (tid >> 3) + 32 i.
+    const int doct = tid & 7, jg = tid >> 3;
+    int jk[2], jv[16];
+    int64_t sk[2], sv[16];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) jk[r] = min(tid + 256 * r, M - 1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) jv[i] = min(jg + 32 * i, M - 1);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) sk[r] = b;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sv[i] = b;
+    if (a.kv_src) {  // every table load first, then every cache load
+        const int32_t *src = a.kv_src + (int64_t)b * a.kv_src_stride;
+        int tk[2], tv[16];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) tk[r] = src[jk[r]];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tv[i] = src[jv[i]];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) sk[r] = jk[r] < M - 1 ? tk[r] : b;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sv[i] = jv[i] < M - 1 ? tv[i] : b;
+    }
     half8 kv[2][8];
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-        const int j = tid + 256 * r;
+        const f16 *kr = (const f16 *)a.K + sk[r] * a.clip_stride + (int64_t)jk[r] * n + h * 64;
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            if (j < M) kv[r][i] = *(const half8 *)(Kb + (int64_t)j * n + 8 * i);
-            else
-#pragma unroll
-                for (int e = 0; e < 8; ++e) kv[r][i][e] = (f16)0.0f;
+        for (int i = 0; i < 8; ++i) kv[r][i] = *(const half8 *)(kr + 8 * i);
     }
-    // PV: thread owns d-octet (tid & 7) and keys (tid >> 3) + 32 i
-    const int doct = tid & 7, jg = tid >> 3;
     half8 vv[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int j = jg + 32 * i;
-        if (j < M) vv[i] = *(const half8 *)(Vb + (int64_t)j * n + doct * 8);
-        else
-#pragma unroll
-            for (int e = 0; e < 8; ++e) vv[i][e] = (f16)0.0f;
-    }
+    for (int i = 0; i < 16; ++i)
+        vv[i] = *(const half8 *)((const f16 *)a.V + sv[i] * a.clip_stride + (int64_t)jv[i] * n + h * 64 + doct * 8);
     half8 qv[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) qv[i] = *(const half8 *)(qr + 8 * i);
@@ -1459,6 +1472,224 @@ __global__ __launch_bounds__(64) void k_dec_record(DecEmbedArgs a) {
 hipError_t launch_dec_embed(hipStream_t s, const DecEmbedArgs &a) {
     if (!a.record_only) return hipErrorInvalidValue;  // the embedding is fused into layer 0's QKV kernel
     hipLaunchKernelGGL(k_dec_record, dim3(a.B), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+
+// ============================================================================
+// beam search step (config C5; semantics in oracle/wmi_oracle.h)
+// ============================================================================
+// (value desc, id asc) as one unsigned key: larger key = earlier in the order
+__device__ __forceinline__ unsigned long long beam_key(float v, int id) {
+    return ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)id);
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(k, o);
+        k = t > k ? t : k;
+    }
+    return k;
+}
+
+// one vocabulary split of one row: split max, sum exp(logit - max) (double)
+// and the split's top-(K+1)
+__global__ __launch_bounds__(256) void k_beam_topk(BeamArgs a) {
+    trace_begin(a.trace);
+    const int sp = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (a.st->pos < a.feed_len || a.bs->done || b >= a.bs->n_active) {
+        trace_end(a.trace);
+        return;
+    }
+    __shared__ float redf[4];
+    __shared__ double redd[4];
+    __shared__ unsigned long long redk[4];
+    constexpr int U = 16;  // split length <= 4096
+    const int chunk = (a.V + BEAM_NS - 1) / BEAM_NS, lo = sp * chunk, hi = min(a.V, lo + chunk);
+    const float *row = a.logits + (int64_t)b * a.V;
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = lo + tid + 256 * u;
+        v[u] = row[i < hi ? i : lo];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = lo + tid + 256 * u;
+        if (i >= hi || i == a.suppress_id) v[u] = -INFINITY;
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < U; ++u) m = fmaxf(m, v[u]);
+    m = wave_max(m);
+    if (lane == 0) redf[w] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
+    double sum = 0.0;
+    if (m > -INFINITY)
+#pragma unroll
+        for (int u = 0; u < U; ++u) sum += exp((double)v[u] - (double)m);
+    sum = wave_sum(sum);
+    if (lane == 0) redd[w] = sum;
+    BeamPart *out = a.parts + (int64_t)b * BEAM_NS + sp;
+    uint32_t taken = 0;
+    for (int r = 0; r <= a.K; ++r) {
+        unsigned long long best = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = lo + tid + 256 * u;
+            const unsigned long long k = (i < hi && !((taken >> u) & 1u)) ? beam_key(v[u], i) : 0ull;
+            best = k > best ? k : best;
+        }
+        best = wave_max_u64(best);
+        if (lane == 0) redk[w] = best;
+        __syncthreads();
+        unsigned long long k0 = redk[0];
+#pragma unroll
+        for (int i = 1; i < 4; ++i) k0 = redk[i] > k0 ? redk[i] : k0;
+        const int id = (int)(0xffffffffu - (uint32_t)(k0 & 0xffffffffull));
+        const int rel = id - lo;
+        if (k0 && (rel & 255) == tid) taken |= 1u << (rel >> 8);
+        if (tid == 0) {
+            out->val[r] = k0 ? unord_f32((uint32_t)(k0 >> 32)) : -INFINITY;
+            out->id[r] = k0 ? id : -1;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        out->m = m;
+        out->sum = ((redd[0] + redd[1]) + redd[2]) + redd[3];
+    }
+    trace_end(a.trace);
+}
+
+// candidate i before candidate j in the ranking (score desc, beam asc, rank asc)
+__device__ __forceinline__ bool cand_before(double si, int bi, int ri, double sj, int bj, int rj) {
+    if (si != sj) return si > sj;
+    if (bi != bj) return bi < bj;
+    return ri < rj;
+}
+
+// one workgroup: merge the splits, rank the K x (K+1) candidates, fill the
+// next hypotheses, record finished ones, and re-point the KV history table
+__global__ __launch_bounds__(256) void k_beam_select(BeamArgs a) {
+    trace_begin(a.trace);
+    BeamState *bs = a.bs;
+    const int pos = a.st->pos;
+    if (pos < a.feed_len || bs->done) {
+        trace_end(a.trace);
+        return;
+    }
+    const int t = pos - a.feed_len, K = a.K, TK = K + 1;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int NC = BEAM_MAX * BEAM_TK;
+    __shared__ double lse[BEAM_MAX];
+    __shared__ float cval[NC];
+    __shared__ int cid[NC];
+    __shared__ double cscore[NC];
+    __shared__ int order[NC];
+    __shared__ int sel_parent[BEAM_MAX], sel_tok[BEAM_MAX], n_new_s;
+    __shared__ double sel_score[BEAM_MAX];
+    __shared__ int32_t src_old[BEAM_MAX][512];
+    const int na_old = bs->n_active;
+    // 1. per active row: log-sum-exp and the row's top-(K+1) over the splits
+    for (int b = w; b < na_old; b += 4) {
+        const BeamPart *pp = a.parts + (int64_t)b * BEAM_NS;
+        const float pm = lane < BEAM_NS ? pp[lane].m : -INFINITY;
+        const double ps = lane < BEAM_NS ? pp[lane].sum : 0.0;
+        const float M = wave_max(pm);
+        const double S = wave_sum(pm > -INFINITY ? ps * exp((double)pm - (double)M) : 0.0);
+        if (lane == 0) lse[b] = (double)M + log(S);
+        unsigned long long key[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int c = lane + 64 * k;
+            key[k] = 0ull;
+            if (c < BEAM_NS * TK) {
+                const int id = pp[c / TK].id[c % TK];
+                if (id >= 0) key[k] = beam_key(pp[c / TK].val[c % TK], id);
+            }
+        }
+        for (int r = 0; r < TK; ++r) {
+            unsigned long long best = key[0] > key[1] ? key[0] : key[1];
+            best = key[2] > best ? key[2] : best;
+            best = wave_max_u64(best);
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (key[k] == best) key[k] = 0ull;
+            if (lane == 0) {
+                cval[b * TK + r] = unord_f32((uint32_t)(best >> 32));
+                cid[b * TK + r] = (int)(0xffffffffu - (uint32_t)(best & 0xffffffffull));
+            }
+        }
+    }
+    __syncthreads();
+    // 2. scores and ranking
+    const int nc = na_old * TK;
+    if (tid < nc) cscore[tid] = bs->score[tid / TK] + ((double)cval[tid] - lse[tid / TK]);
+    __syncthreads();
+    if (tid < nc) {
+        int rank = 0;
+        const double si = cscore[tid];
+        const int bi = tid / TK, ri = tid % TK;
+        for (int j = 0; j < nc; ++j)
+            if (cand_before(cscore[j], j / TK, j % TK, si, bi, ri)) ++rank;
+        order[rank] = tid;
+    }
+    // history table of the parents, positions < pos - 1
+    for (int i = tid; i < na_old * (pos - 1); i += 256) {
+        const int r = i / (pos - 1), j = i - r * (pos - 1);
+        src_old[r][j] = a.kv_src[r * a.tctx + j];
+    }
+    __syncthreads();
+    // 3. walk the ranking
+    if (tid == 0) {
+        int na = 0, nf = bs->n_fin;
+        for (int k = 0; k < nc && na < K; ++k) {
+            const int c = order[k];
+            if (cid[c] == a.eot) {
+                if (nf < K) {
+                    bs->fin_t[nf] = t;
+                    bs->fin_beam[nf] = c / TK;
+                    bs->fin_score[nf] = cscore[c];
+                    ++nf;
+                }
+                continue;
+            }
+            sel_parent[na] = c / TK;
+            sel_tok[na] = cid[c];
+            sel_score[na] = cscore[c];
+            ++na;
+        }
+        n_new_s = na;
+        bs->n_fin = nf;
+        bs->n_active = na;
+        bs->n_steps = t + 1;
+        if (nf >= K || t + 1 >= a.max_tokens) bs->done = 1;
+    }
+    __syncthreads();
+    // 4. next hypotheses: scores, fed tokens, back-pointers, KV history table
+    const int nn = n_new_s;
+    if (tid < nn) {
+        bs->score[tid] = sel_score[tid];
+        bs->tok[tid] = sel_tok[tid];
+        a.hist_parent[t * BEAM_MAX + tid] = sel_parent[tid];
+        a.hist_tok[t * BEAM_MAX + tid] = sel_tok[tid];
+    }
+    for (int i = tid; i < nn * pos; i += 256) {
+        const int sl = i / pos, j = i - sl * pos, p = sel_parent[sl];
+        a.kv_src[sl * a.tctx + j] = j < pos - 1 ? src_old[p][j] : p;
+    }
+    trace_end(a.trace);
+}
+
+hipError_t launch_beam_step(hipStream_t s, const BeamArgs &a) {
+    if (a.K < 1 || a.K > BEAM_MAX || a.tctx > 512 || (a.V + BEAM_NS - 1) / BEAM_NS > 4096)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_beam_topk, dim3(BEAM_NS, a.K), dim3(256), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_beam_select, dim3(1), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -182,8 +182,9 @@ def _vocab_tokens(n: int):
 
 
 def write_ggml(path: str, model: str = "base", hp_override: dict | None = None,
-               wscale: float = 0.02, n_vocab_file: int | None = None) -> dict:
-    """Write a synthetic ggml-v1 Whisper file; returns the hparams used."""
+               wscale: float = 0.02, n_vocab_file: int | None = None, tensor_hook=None) -> dict:
+    """Write a synthetic ggml-v1 Whisper file; returns the hparams used.
+    tensor_hook(name, array) -> array may edit tensors before they are written."""
     hp = dict(MODEL_DIMS[model])
     hp["f16"] = 1
     if hp_override:
@@ -202,6 +203,8 @@ def write_ggml(path: str, model: str = "base", hp_override: dict | None = None,
             f.write(tok)
         for name, shape, kind in tensor_specs(hp):
             arr = tensor_value(name, shape, kind, hp, wscale)
+            if tensor_hook is not None:
+                arr = tensor_hook(name, arr)
             ftype = 1 if arr.dtype == np.float16 else 0
             ne = tuple(reversed(shape))
             nb = name.encode()

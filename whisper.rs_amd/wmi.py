@@ -60,8 +60,8 @@ _ERRORS = {c.code: c for c in (UnexpectIO, BadMagic, NotEnoughSpace, UnknownTens
 EXPORTS = (
     "wmi_init_from_file", "wmi_free", "wmi_strerror", "wmi_last_error", "wmi_last_error_global",
     "wmi_get_hparams", "wmi_get_special_tokens", "wmi_set_audio_ctx", "wmi_token_to_bytes",
-    "wmi_pcm_to_mel", "wmi_pcm_to_mel_batch", "wmi_encode", "wmi_decode_greedy", "wmi_decode_logits", "wmi_full",
-    "wmi_stage_pcm", "wmi_run_staged", "wmi_get_tokens", "wmi_get_timings", "wmi_sync",
+    "wmi_pcm_to_mel", "wmi_pcm_to_mel_batch", "wmi_encode", "wmi_decode_greedy", "wmi_decode_logits",
+    "wmi_decode_beam", "wmi_full", "wmi_stage_pcm", "wmi_run_staged", "wmi_run_staged_beam", "wmi_get_tokens", "wmi_get_timings", "wmi_sync",
     "wmi_get_mel", "wmi_get_encoder_out", "wmi_get_cross_kv", "wmi_bench_kernel", "wmi_selftest",
     "wmi_dist_id_size", "wmi_dist_make_id", "wmi_dist_init", "wmi_dist_gather_tokens", "wmi_dist_barrier",
 )
@@ -120,6 +120,8 @@ def lib():
         L.wmi_decode_logits.argtypes = [vp, C.c_int, vp, C.c_int, vp]
         L.wmi_full.argtypes = [vp, vp, sz, C.c_int, vp, vp]
         L.wmi_run_staged.argtypes = [vp, C.c_int, C.c_int]
+        L.wmi_run_staged_beam.argtypes = [vp, C.c_int, C.c_int, C.c_int]
+        L.wmi_decode_beam.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp, vp, vp]
         L.wmi_get_tokens.argtypes = [vp, vp, sz, vp]
         L.wmi_get_timings.argtypes = [vp, C.POINTER(Timings)]
         L.wmi_sync.argtypes = [vp]
@@ -228,6 +230,15 @@ class WhisperContext:
         _raise(lib().wmi_decode_greedy(self._h, max_tokens, int(suppress_eot), _ptr(toks), _ptr(cnt)), self._h)
         return [toks[i, :cnt[i]].copy() for i in range(self.n_clips)]
 
+    def decode_beam(self, beam_size: int, max_tokens: int, suppress_eot: bool = False):
+        """Beam search per clip: [(tokens, score)] (semantics: oracle/wmi_oracle.h)."""
+        toks = np.zeros((self.n_clips, max_tokens), np.int32)
+        cnt = np.zeros(self.n_clips, np.int32)
+        sc = np.zeros(self.n_clips, np.float64)
+        _raise(lib().wmi_decode_beam(self._h, beam_size, max_tokens, int(suppress_eot), _ptr(toks), _ptr(cnt),
+                                     _ptr(sc)), self._h)
+        return [(toks[i, :cnt[i]].copy(), float(sc[i])) for i in range(self.n_clips)]
+
     def decode_logits(self, tokens, clip: int = 0) -> np.ndarray:
         tokens = np.ascontiguousarray(tokens, dtype=np.int32)
         out = np.zeros((tokens.size, self.hparams["n_vocab"]), np.float32)
@@ -250,8 +261,8 @@ class WhisperContext:
         _raise(lib().wmi_stage_pcm(self._h, len(clips), ptrs, ns), self._h)
         self.n_clips = len(clips)
 
-    def run_staged(self, n_decode: int = 128, mel_offset: int = 0) -> None:
-        _raise(lib().wmi_run_staged(self._h, mel_offset, n_decode), self._h)
+    def run_staged(self, n_decode: int = 128, mel_offset: int = 0, beam_size: int = 0) -> None:
+        _raise(lib().wmi_run_staged_beam(self._h, mel_offset, n_decode, beam_size), self._h)
         self._n_decode = n_decode
 
     def tokens(self) -> np.ndarray:
