@@ -43,6 +43,7 @@ def lib():
         L.or_encode.argtypes = [vp, fp, i32, C.c_int, C.c_int, C.c_int, fp, hp_, hp_, C.c_void_p]
         L.or_decode_logits.argtypes = [vp, hp_, hp_, C.c_int, ip, C.c_int, C.c_int, fp]
         L.or_decode_greedy.argtypes = [vp, hp_, hp_, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.POINTER(i32), fp]
+        L.or_dequant.argtypes = [C.c_int, C.c_void_p, C.c_int64, hp_]
         L.or_decode_beam.argtypes = [vp, hp_, hp_, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.POINTER(i32),
                                      C.POINTER(C.c_double), C.POINTER(C.c_float)]
         _lib = L
@@ -62,6 +63,16 @@ class OracleError(RuntimeError):
 def set_dot_mode(exact_double: bool) -> None:
     """Switch dot-product accumulation (noise-floor measurement only)."""
     lib().or_set_dot_mode(int(exact_double))
+
+
+def dequant(qtype: int, blocks: bytes, nel: int) -> np.ndarray:
+    """The oracle loader's dequantisation (f16 bits) of ggml blocks."""
+    out = np.zeros(nel, np.uint16)
+    buf = C.create_string_buffer(bytes(blocks), len(blocks))
+    rc = lib().or_dequant(qtype, C.cast(buf, C.c_void_p), nel, out)
+    if rc:
+        raise OracleError(rc, "dequant")
+    return out
 
 
 def tables():

@@ -203,6 +203,74 @@ static void reg_add(reg_entry *r, int *n, const char *name, int dtype, int n_dim
     e->dst = dst;
 }
 
+/* ggml quantised blocks (QNT version 2 layouts; SURVEY.md §A.8 and §8f
+ * item 2: the reference loader rejects them, main.rs:1423-1434).  Weights are
+ * dequantised to f16 — w = f16(q * d (+ m)), f32 multiply then add, no FMA —
+ * and every matmul then follows the f16 semantics (§A.4), as ggml's GPU
+ * back-ends do (dequantise -> f16 GEMM).  Types: 2 q4_0, 3 q4_1, 6 q5_0,
+ * 7 q5_1, 8 q8_0; 32 weights per block. */
+static int qblock_bytes(int t) {
+    switch (t) {
+        case 2: return 18;
+        case 3: return 20;
+        case 6: return 22;
+        case 7: return 24;
+        case 8: return 34;
+        default: return 0;
+    }
+}
+
+static void dequant_row_f16(int t, const uint8_t *src, int64_t nel, uint16_t *dst) {
+    const int bs = qblock_bytes(t);
+    for (int64_t ib = 0; ib < nel / 32; ++ib) {
+        const uint8_t *b = src + ib * bs;
+        uint16_t *y = dst + ib * 32;
+        uint16_t hd, hm;
+        memcpy(&hd, b, 2);
+        const float d = h2f(hd);
+        if (t == 2) { /* q4_0: {d, qs[16]}, (nibble - 8) * d */
+            for (int j = 0; j < 16; ++j) {
+                y[j] = f2h((float)((b[2 + j] & 0x0F) - 8) * d);
+                y[j + 16] = f2h((float)((b[2 + j] >> 4) - 8) * d);
+            }
+        } else if (t == 3) { /* q4_1: {d, m, qs[16]}, nibble * d + m */
+            memcpy(&hm, b + 2, 2);
+            const float m = h2f(hm);
+            for (int j = 0; j < 16; ++j) {
+                y[j] = f2h((float)(b[4 + j] & 0x0F) * d + m);
+                y[j + 16] = f2h((float)(b[4 + j] >> 4) * d + m);
+            }
+        } else if (t == 6 || t == 7) { /* q5_0 {d, qh, qs} (q - 16) * d; q5_1 {d, m, qh, qs} q * d + m */
+            const int o = t == 6 ? 2 : 4;
+            float m = 0.0f;
+            if (t == 7) { memcpy(&hm, b + 2, 2); m = h2f(hm); }
+            uint32_t qh;
+            memcpy(&qh, b + o, 4);
+            const uint8_t *qs = b + o + 4;
+            for (int j = 0; j < 16; ++j) {
+                const int x0 = (qs[j] & 0x0F) | (((qh >> j) & 1) << 4);
+                const int x1 = (qs[j] >> 4) | (((qh >> (j + 16)) & 1) << 4);
+                if (t == 6) {
+                    y[j] = f2h((float)(x0 - 16) * d);
+                    y[j + 16] = f2h((float)(x1 - 16) * d);
+                } else {
+                    y[j] = f2h((float)x0 * d + m);
+                    y[j + 16] = f2h((float)x1 * d + m);
+                }
+            }
+        } else { /* q8_0: {d, int8 qs[32]} */
+            for (int j = 0; j < 32; ++j) y[j] = f2h((float)(int8_t)b[2 + j] * d);
+        }
+    }
+}
+
+/* test hook: the loader's dequantisation of nel weights of ggml type t */
+int or_dequant(int t, const uint8_t *src, int64_t nel, uint16_t *dst) {
+    if (!qblock_bytes(t) || nel % 32) return WMI_E_INVALID_ARG;
+    dequant_row_f16(t, src, nel, dst);
+    return WMI_OK;
+}
+
 /* special token ids (main.rs:557-575) with the multilingual shift
  * (main.rs:433-440); large-v3 (n_vocab 51866, one more language) uses the
  * shift of later whisper.cpp. */
@@ -288,7 +356,8 @@ int or_load(const char *path, or_model **out, char *err, size_t errcap) {
         const int32_t *hp = m->hp;
         const int64_t n = hp[HP_N_AUDIO_STATE], nt = hp[HP_N_TEXT_STATE];
         const int64_t La = hp[HP_N_AUDIO_LAYER], Lt = hp[HP_N_TEXT_LAYER];
-        const int W = hp[HP_F16] == 1 ? 1 : 0;
+        const int file_ftype = hp[HP_F16] % 1000; /* ggml ftype + 1000 * quantisation version */
+        const int W = file_ftype == 0 ? 0 : 1;    /* matrices land as f16 (quantised ones dequantised) */
         const int cap = 16 + 15 * La + 24 * Lt;
         reg = calloc(cap, sizeof(reg_entry));
         int nr = 0;
@@ -405,20 +474,37 @@ int or_load(const char *path, or_model **out, char *err, size_t errcap) {
                     rc = WMI_E_WRONG_SHAPE;
                     goto fail;
                 }
-            const int64_t bpe = ftype == 0 ? 4 : 2;
+            const int qb = (e->dtype == 1 && e->n_dims == 2 && ne[0] % 32 == 0) ? qblock_bytes(ftype) : 0;
+            const int64_t file_bytes = qb ? nel / 32 * qb : nel * (ftype == 0 ? 4 : 2);
             const int64_t nbytes = want * (e->dtype ? 2 : 4);
-            if (nel * bpe != nbytes) {
+            if (qb ? 0 : file_bytes != nbytes) {
                 set_err(err, errcap, "tensor %s has wrong bytes in model file, got:%lld, expected:%lld", name,
-                        (long long)nbytes, (long long)(nel * bpe));
+                        (long long)nbytes, (long long)file_bytes);
                 rc = WMI_E_WRONG_BYTES;
                 goto fail;
             }
-            RD(*e->dst, nbytes);
+            if (qb) {
+                uint8_t *raw = malloc((size_t)file_bytes);
+                if (fread(raw, 1, (size_t)file_bytes, f) != (size_t)file_bytes) {
+                    free(raw);
+                    set_err(err, errcap, "Unexpected IO: short read");
+                    rc = WMI_E_IO;
+                    goto fail;
+                }
+                dequant_row_f16(ftype, raw, nel, (uint16_t *)*e->dst);
+                free(raw);
+            } else {
+                RD(*e->dst, nbytes);
+            }
         }
-        if (hp[HP_F16] != 1) {
-            set_err(err, errcap, "f32 matrices (hparams.f16 = %d) are not supported by this build", hp[HP_F16]);
-            rc = WMI_E_UNSUPPORTED;
-            goto fail;
+        {
+            const int ft = hp[HP_F16] % 1000, qv = hp[HP_F16] / 1000;
+            const int ok = ft == 1 || ((ft == 2 || ft == 3 || ft == 7 || ft == 8 || ft == 9) && qv == 2);
+            if (!ok) {
+                set_err(err, errcap, "model ftype %d (hparams.f16 = %d) is not supported by this build", ft, hp[HP_F16]);
+                rc = WMI_E_UNSUPPORTED;
+                goto fail;
+            }
         }
     }
     free(reg);

@@ -316,3 +316,56 @@ def test_large_v3(wmi, model_cache):
     finally:
         ctx.close()
         om.close()
+
+
+# --- ggml quantised weights (config C3; semantics in tests/test_quant.py) ----
+@pytest.mark.parametrize("qtype", ["q4_0", "q4_1", "q5_0", "q5_1", "q8_0"])
+def test_quantised_micro(wmi, model_cache, qtype):
+    import os
+    path = os.path.join(model_cache, f"ggml-synth-micro-{qtype}.bin")
+    if not os.path.exists(path):
+        synth.write_ggml(path, "micro", quant=qtype)
+    om = pyoracle.OracleModel(path)
+    ctx = wmi.WhisperContext.new(path, 0, max_clips=1)
+    try:
+        _, ck_ref, cv_ref = _check_encoder(ctx, om, synth.synth_pcm_f32(2.0, 1234), 64)
+        toks = np.array(om.prompt() + [1000, 2000, 3000], np.int32)
+        ref = om.decode_logits(ck_ref, cv_ref, toks, n_threads=threads())
+        assert np.abs(ctx.decode_logits(toks, 0) - ref).max() <= 2e-3
+    finally:
+        ctx.close()
+        om.close()
+
+
+def test_small_q5_1(wmi, model_cache):
+    """C3: whisper small with q5_1 weights.  The decoder GEMVs stream the q5_1
+    blocks and dequantise in registers; the result must equal, bit for bit,
+    the same decoder reading the loader's dequantised f16 copies
+    (WMI_NO_Q5=1), which the oracle pins."""
+    import os
+    path = synth.model_path("small-q5_1", model_cache)
+    om = pyoracle.OracleModel(path)
+    ctx = wmi.WhisperContext.new(path, 0, max_clips=1)
+    os.environ["WMI_NO_Q5"] = "1"
+    try:
+        ctx16 = wmi.WhisperContext.new(path, 0, max_clips=1)
+    finally:
+        del os.environ["WMI_NO_Q5"]
+    try:
+        pcm = synth.synth_pcm_f32(30.0, 1234)
+        _, ck_ref, cv_ref = _check_encoder(ctx, om, pcm, 1500)
+        ref, margins = om.decode_greedy(ck_ref, cv_ref, 16, suppress_eot=True, n_threads=threads())
+        got = ctx.decode_greedy(16, suppress_eot=True)[0]
+        near = np.nonzero(margins < 1e-3)[0]
+        upto = near[0] + 1 if near.size else len(ref)
+        np.testing.assert_array_equal(got[:upto], ref[:upto])
+        ctx16.set_audio_ctx(1500)
+        ctx16.pcm_to_mel_batch([pcm])
+        ctx16.encode(1, 0)
+        np.testing.assert_array_equal(ctx16.decode_greedy(16, suppress_eot=True)[0], got)
+        toks = np.array(om.prompt() + list(got[:6]), np.int32)
+        np.testing.assert_array_equal(ctx16.decode_logits(toks, 0), ctx.decode_logits(toks, 0))
+    finally:
+        ctx16.close()
+        ctx.close()
+        om.close()

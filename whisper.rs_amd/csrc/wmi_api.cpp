@@ -108,7 +108,9 @@ void build_mel_tables(MelTables &t) {
 }
 
 struct HostTensor {
-    int dtype = 0;  // 0 f32, 1 f16
+    int dtype = 0;  // 0 f32, 1 f16 (quantised matrices are dequantised to f16)
+    int qtype = 0;  // ggml type of a quantised matrix in the file (7 = q5_1), else 0
+    std::vector<uint8_t> qraw;  // its blocks as read (q5_1 only: the decoder GEMVs read them)
     int n_dims = 0;
     int64_t ne[3] = {1, 1, 1};
     std::vector<uint8_t> data;
@@ -136,6 +138,8 @@ struct DecLayerDev {
     float *ln2_w, *ln2_b;
     uint16_t *w0; float *b0;
     uint16_t *w1; float *b1;
+    // q5_1 copies for the decoder GEMVs (null unless every decoder matrix is q5_1)
+    const uint8_t *wqkv5, *wo5, *wco5, *w05, *w15;
 };
 
 int64_t up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
@@ -162,6 +166,8 @@ struct wmi_context {
     uint16_t *wckv = nullptr;
     float *bckv = nullptr;
     uint16_t *te = nullptr;
+    const uint8_t *te5 = nullptr;  // q5_1 token embedding for the logits GEMV (q5_1 models)
+    bool use_q5 = true;            // WMI_NO_Q5=1: decoder GEMVs read the dequantised f16 copies
     float *d_pe = nullptr, *dln_w = nullptr, *dln_b = nullptr;
     std::vector<DecLayerDev> dec;
     // workspace
@@ -277,6 +283,59 @@ struct ParsedModel {
     std::map<std::string, HostTensor> tensors;
 };
 
+// ggml quantised blocks (QNT version 2).  The
+// reference loader rejects them (main.rs:1423-1434); this build dequantises
+// every matrix to f16, w = f16(q * d (+ m)) with an unfused f32 multiply and
+// add, and keeps q5_1 blocks as well for the bandwidth-bound decoder GEMVs,
+// which dequantise on the fly to the same f16 values.
+int qblock_bytes(int t) {
+    switch (t) {
+        case 2: return 18;  // q4_0 {d, qs[16]}
+        case 3: return 20;  // q4_1 {d, m, qs[16]}
+        case 6: return 22;  // q5_0 {d, qh, qs[16]}
+        case 7: return 24;  // q5_1 {d, m, qh, qs[16]}
+        case 8: return 34;  // q8_0 {d, qs[32]}
+        default: return 0;
+    }
+}
+
+void dequant_f16(int t, const uint8_t *src, int64_t nel, uint16_t *dst) {
+    const int bs = qblock_bytes(t);
+    for (int64_t ib = 0; ib < nel / 32; ++ib) {
+        const uint8_t *b = src + ib * bs;
+        uint16_t *y = dst + ib * 32;
+        uint16_t hd, hm = 0;
+        memcpy(&hd, b, 2);
+        const float d = f16_to_f32(hd);
+        float m = 0.0f;
+        if (t == 3 || t == 7) {
+            memcpy(&hm, b + 2, 2);
+            m = f16_to_f32(hm);
+        }
+        int q[32];
+        if (t == 2 || t == 3) {
+            const uint8_t *qs = b + (t == 2 ? 2 : 4);
+            for (int j = 0; j < 16; ++j) { q[j] = qs[j] & 15; q[j + 16] = qs[j] >> 4; }
+        } else if (t == 6 || t == 7) {
+            const int o = t == 6 ? 2 : 4;
+            uint32_t qh;
+            memcpy(&qh, b + o, 4);
+            const uint8_t *qs = b + o + 4;
+            for (int j = 0; j < 16; ++j) {
+                q[j] = (qs[j] & 15) | (int)(((qh >> j) & 1u) << 4);
+                q[j + 16] = (qs[j] >> 4) | (int)(((qh >> (j + 16)) & 1u) << 4);
+            }
+        } else {
+            for (int j = 0; j < 32; ++j) q[j] = (int8_t)b[2 + j];
+        }
+        const int off = t == 2 ? 8 : t == 6 ? 16 : 0;
+        for (int j = 0; j < 32; ++j) {
+            const float pr = (float)(q[j] - off) * d;  // -ffp-contract=off: no FMA with the add
+            y[j] = f32_to_f16((t == 3 || t == 7) ? pr + m : pr);
+        }
+    }
+}
+
 int parse_file(const char *path, ParsedModel &pm, std::string &err) {
     FILE *f = fopen(path, "rb");
     if (!f) { err = std::string("Unexpected IO: cannot open '") + path + "'"; return WMI_E_IO; }
@@ -319,7 +378,8 @@ int parse_file(const char *path, ParsedModel &pm, std::string &err) {
     // expected tensors (main.rs:947-1334)
     std::map<std::string, Expected> exp;
     const int64_t n = hp.n_audio_state, nt = hp.n_text_state;
-    const int W = hp.f16 == 1 ? 1 : 0;
+    const int file_ftype = hp.f16 % 1000;  // ggml ftype + 1000 * quantisation version
+    const int W = file_ftype == 0 ? 0 : 1;  // matrices land as f16 (quantised ones dequantised)
     exp["encoder.positional_embedding"] = {0, 2, {n, hp.n_audio_ctx, 1}};
     exp["encoder.conv1.weight"] = {W, 3, {3, hp.n_mels, n}};
     exp["encoder.conv1.bias"] = {0, 2, {1, n, 1}};
@@ -420,18 +480,35 @@ int parse_file(const char *path, ParsedModel &pm, std::string &err) {
                 err = b;
                 return WMI_E_WRONG_SHAPE;
             }
-        const int64_t bpe = ftype == 0 ? 4 : 2;
-        if (nel * bpe != (int64_t)t.data.size()) {
+        const int qb = (t.dtype == 1 && t.n_dims == 2 && ne[0] % 32 == 0) ? qblock_bytes(ftype) : 0;
+        const int64_t file_bytes = qb ? nel / 32 * qb : nel * (ftype == 0 ? 4 : 2);
+        if (!qb && file_bytes != (int64_t)t.data.size()) {
             snprintf(b, sizeof b, "tensor %s has wrong bytes in model file, got:%lld, expected:%lld", name.c_str(),
-                     (long long)t.data.size(), (long long)(nel * bpe));
+                     (long long)t.data.size(), (long long)file_bytes);
             err = b;
             return WMI_E_WRONG_BYTES;
         }
-        if (!rd(t.data.data(), t.data.size())) { err = "Unexpected IO: short read (tensor data)"; return WMI_E_IO; }
+        if (qb) {
+            std::vector<uint8_t> raw((size_t)file_bytes);
+            if (!rd(raw.data(), raw.size())) { err = "Unexpected IO: short read (tensor data)"; return WMI_E_IO; }
+            dequant_f16(ftype, raw.data(), nel, (uint16_t *)t.data.data());
+            t.qtype = ftype;
+            if (ftype == 7) t.qraw = std::move(raw);
+        } else {
+            t.qtype = 0;
+            t.qraw.clear();
+            if (!rd(t.data.data(), t.data.size())) { err = "Unexpected IO: short read (tensor data)"; return WMI_E_IO; }
+        }
     }
-    if (hp.f16 != 1) {
-        err = "f32 matrices (hparams.f16 != 1) are not supported by this build";
-        return WMI_E_UNSUPPORTED;
+    {
+        const int ft = hp.f16 % 1000, qv = hp.f16 / 1000;
+        const bool ok = ft == 1 || ((ft == 2 || ft == 3 || ft == 7 || ft == 8 || ft == 9) && qv == 2);
+        if (!ok) {
+            char b[160];
+            snprintf(b, sizeof b, "model ftype %d (hparams.f16 = %d) is not supported by this build", ft, hp.f16);
+            err = b;
+            return WMI_E_UNSUPPORTED;
+        }
     }
     return WMI_OK;
 }
@@ -475,6 +552,48 @@ struct Arena {
         return o;
     }
 };
+
+// q5_1 rows of one or more [rows][K] matrices, concatenated, in the decoder
+// GEMV layout: nibbles [N][K/2] in natural order (byte i of a block = weights
+// 2i, 2i+1), then 5th bits [N][K/32] (u32, bit j = weight j), then {f16 d,
+// f16 m} [N][K/32]
+std::vector<uint8_t> repack_q5(const std::vector<const HostTensor *> &mats, int64_t K) {
+    int64_t N = 0;
+    for (const HostTensor *t : mats) N += t->nel() / K;
+    const int64_t nb = K / 32;
+    std::vector<uint8_t> out((size_t)(N * K / 2 + N * nb * 8));
+    uint8_t *qn = out.data();
+    uint32_t *qh = (uint32_t *)(out.data() + N * K / 2);
+    uint32_t *dm = qh + N * nb;
+    int64_t r0 = 0;
+    for (const HostTensor *t : mats) {
+        const int64_t rows = t->nel() / K;
+        for (int64_t r = 0; r < rows; ++r)
+            for (int64_t ib = 0; ib < nb; ++ib) {
+                const uint8_t *b = t->qraw.data() + (r * nb + ib) * 24;
+                uint32_t h;
+                memcpy(&h, b + 4, 4);
+                const uint8_t *qs = b + 8;
+                int q[32];
+                for (int j = 0; j < 16; ++j) {
+                    q[j] = (qs[j] & 15) | (int)(((h >> j) & 1u) << 4);
+                    q[j + 16] = (qs[j] >> 4) | (int)(((h >> (j + 16)) & 1u) << 4);
+                }
+                const int64_t R = r0 + r;
+                uint32_t bits = 0;
+                for (int j = 0; j < 32; ++j) bits |= (uint32_t)(q[j] >> 4) << j;
+                for (int i = 0; i < 16; ++i)
+                    qn[R * K / 2 + ib * 16 + i] = (uint8_t)((q[2 * i] & 15) | ((q[2 * i + 1] & 15) << 4));
+                qh[R * nb + ib] = bits;
+                uint16_t d, m;
+                memcpy(&d, b, 2);
+                memcpy(&m, b + 2, 2);
+                dm[R * nb + ib] = (uint32_t)d | ((uint32_t)m << 16);
+            }
+        r0 += rows;
+    }
+    return out;
+}
 
 int upload_model(wmi_context *ctx, ParsedModel &pm) {
     const wmi_hparams &hp = ctx->hp;
@@ -603,6 +722,32 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
         d.w1 = add(T(p + "mlp.2.weight").f16(), 4 * nt * nt * 2);
         d.b1 = add(T(p + "mlp.2.bias").f32(), nt * 4);
     }
+    // q5_1 decoder: the GEMVs stream the blocks (0.75 B/weight instead of 2)
+    bool q5 = T("decoder.token_embedding.weight").qtype == 7;
+    for (int i = 0; i < Lt && q5; ++i) {
+        snprintf(nm, sizeof nm, "decoder.blocks.%d.", i);
+        const std::string p(nm);
+        for (const char *w : {"attn.query.weight", "attn.key.weight", "attn.value.weight", "attn.out.weight",
+                              "cross_attn.out.weight", "mlp.0.weight", "mlp.2.weight"})
+            q5 = q5 && T(p + w).qtype == 7;
+    }
+    struct DecQ5 { size_t wqkv, wo, wco, w0, w1; };
+    std::vector<DecQ5> dq5(Lt);
+    size_t o_te5 = 0;
+    if (q5) {
+        auto addv = [&](const std::vector<uint8_t> &v) { return add(v.data(), v.size()); };
+        o_te5 = addv(repack_q5({&T("decoder.token_embedding.weight")}, nt));
+        for (int i = 0; i < Lt; ++i) {
+            snprintf(nm, sizeof nm, "decoder.blocks.%d.", i);
+            const std::string p(nm);
+            dq5[i].wqkv = addv(repack_q5({&T(p + "attn.query.weight"), &T(p + "attn.key.weight"),
+                                          &T(p + "attn.value.weight")}, nt));
+            dq5[i].wo = addv(repack_q5({&T(p + "attn.out.weight")}, nt));
+            dq5[i].wco = addv(repack_q5({&T(p + "cross_attn.out.weight")}, nt));
+            dq5[i].w0 = addv(repack_q5({&T(p + "mlp.0.weight")}, nt));
+            dq5[i].w1 = addv(repack_q5({&T(p + "mlp.2.weight")}, 4 * nt));
+        }
+    }
     // upload everything in one copy
     ctx->model_bytes = A.off;
     HIPCHK(ctx, hipMalloc(&ctx->d_model, ctx->model_bytes));
@@ -633,9 +778,12 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
     ctx->dec.resize(Lt);
     for (int i = 0; i < Lt; ++i) {
         const DecOff &d = dof[i];
+        auto Q = [&](size_t o) { return q5 ? (const uint8_t *)(base + o) : nullptr; };
         ctx->dec[i] = {F(d.l1w), F(d.l1b), H(d.wqkv), F(d.bqkv), H(d.wo), F(d.bo), F(d.lcw), F(d.lcb),
-                       H(d.wcq), F(d.bcq), H(d.wco), F(d.bco), F(d.l2w), F(d.l2b), H(d.w0), F(d.b0), H(d.w1), F(d.b1)};
+                       H(d.wcq), F(d.bcq), H(d.wco), F(d.bco), F(d.l2w), F(d.l2b), H(d.w0), F(d.b0), H(d.w1), F(d.b1),
+                       Q(dq5[i].wqkv), Q(dq5[i].wo), Q(dq5[i].wco), Q(dq5[i].w0), Q(dq5[i].w1)};
     }
+    ctx->te5 = q5 ? (const uint8_t *)(base + o_te5) : nullptr;
     return WMI_OK;
 }
 
@@ -927,7 +1075,9 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         uint16_t *kc = ctx->kcache + (size_t)l * DEC_ROWS * hp.n_text_ctx * n;
         uint16_t *vc = ctx->vcache + (size_t)l * DEC_ROWS * hp.n_text_ctx * n;
         DecGemvArgs g{};
+        const bool q5 = ctx->use_q5;
         g.x = ctx->dx; g.ln_w = d.ln1_w; g.ln_b = d.ln1_b; g.W = d.wqkv; g.bias = d.bqkv; g.N = 3 * n; g.K = n; g.B = B;
+        g.Wq5 = q5 ? d.wqkv5 : nullptr;
         g.qscale = qs; g.out16 = ctx->dq16; g.ldo = n; g.kcache = kc; g.vcache = vc; g.n_text_ctx = hp.n_text_ctx;
         g.st = ctx->dstate;
         if (l == 0) {
@@ -956,6 +1106,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         HIPCHK(ctx, launch_dec_attn(s, at));
         g = DecGemvArgs{};
         g.parts = ctx->dopart; g.n_parts = 1; g.W = d.wo; g.bias = d.bo; g.N = n; g.K = n; g.B = B;
+        g.Wq5 = q5 ? d.wo5 : nullptr;
         g.out32 = ctx->dx;
         g.trace = tslot(ctx, "wo", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
@@ -975,21 +1126,25 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         HIPCHK(ctx, launch_dec_attn(s, at));
         g = DecGemvArgs{};
         g.parts = ctx->dopart; g.n_parts = c_cross; g.W = d.wco; g.bias = d.bco; g.N = n; g.K = n; g.B = B;
+        g.Wq5 = q5 ? d.wco5 : nullptr;
         g.out32 = ctx->dx;
         g.trace = tslot(ctx, "wco", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
         g = DecGemvArgs{};
         g.x = ctx->dx; g.ln_w = d.ln2_w; g.ln_b = d.ln2_b; g.W = d.w0; g.bias = d.b0; g.N = 4 * n; g.K = n; g.B = B;
+        g.Wq5 = q5 ? d.w05 : nullptr;
         g.out16 = ctx->dhid16; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
         g.trace = tslot(ctx, "mlp0", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_GELU, g));
         g = DecGemvArgs{};
         g.xin16 = ctx->dhid16; g.W = d.w1; g.bias = d.b1; g.N = n; g.K = 4 * n; g.B = B; g.out32 = ctx->dx;
+        g.Wq5 = q5 ? d.w15 : nullptr;
         g.trace = tslot(ctx, "mlp1", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
     }
     DecGemvArgs g{};
     g.x = ctx->dx; g.ln_w = ctx->dln_w; g.ln_b = ctx->dln_b; g.W = ctx->te; g.N = hp.n_vocab; g.K = n; g.B = B;
+    g.Wq5 = ctx->use_q5 ? ctx->te5 : nullptr;
     g.out32 = ctx->dlogits; g.amax = ctx->damax; g.suppress_id = suppress_eot ? ctx->sp.eot : -1;
     g.st_advance = ctx->dstate;
     g.trace = tslot(ctx, "logits", 0);
@@ -1307,6 +1462,7 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (rc) { g_last_error = ctx->last_error; wmi_free(ctx.release()); return rc; }
     if (getenv("WMI_NO_GRAPH")) ctx->use_graph = false;
     if (getenv("WMI_NO_COOP")) ctx->use_coop = false;
+    if (getenv("WMI_NO_Q5")) ctx->use_q5 = false;
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_trace, TRACE_SLOTS * 16 + 64 * 16 * 8));
@@ -1587,6 +1743,7 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
         if (which == 0) {
             DecGemvArgs g{};
             g.x = ctx->dx; g.ln_w = ctx->dln_w; g.ln_b = ctx->dln_b; g.W = ctx->te; g.N = hp.n_vocab;
+            g.Wq5 = ctx->use_q5 ? ctx->te5 : nullptr;
             g.K = hp.n_text_state; g.B = B < 8 ? B : 8;
             g.out32 = ctx->dlogits; g.amax = ctx->damax; g.suppress_id = ctx->sp.eot; g.st_advance = ctx->dstate;
             HIPCHK(ctx, launch_dec_gemv(s, DEC_LOGITS, g));
@@ -1634,9 +1791,10 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
     const double nt = hp.n_text_state, V = hp.n_vocab;
     if (which == 0) {
         const double b = B < 8 ? B : 8;
-        out->alg_bytes = V * nt * 2 + b * nt * 4 + b * V * 4 + 2 * nt * 4;
+        const bool q5 = ctx->use_q5 && ctx->te5;
+        out->alg_bytes = V * nt * (q5 ? 0.75 : 2.0) + b * nt * 4 + b * V * 4 + 2 * nt * 4;
         out->alg_flops = 2.0 * V * nt * b;
-        snprintf(out->name, sizeof out->name, "k_dec_gemv<DEC_LOGITS,LN>");
+        snprintf(out->name, sizeof out->name, q5 ? "k_dec_gemv<DEC_LOGITS,LN,q5_1>" : "k_dec_gemv<DEC_LOGITS,LN>");
     } else if (which == 1) {
         out->alg_flops = 2.0 * M * (4.0 * n) * n;
         out->alg_bytes = (double)M * n * 2 + 4.0 * n * n * 2 + (double)M * 4 * n * 2;

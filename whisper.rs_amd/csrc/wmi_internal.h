@@ -102,6 +102,7 @@ struct DecGemvArgs {
     const float *parts;      // or: split-key attention partials [B][n_parts][K] f32, summed in order
     int n_parts;
     const uint16_t *W;       // [N][K]
+    const uint8_t *Wq5;      // or q5_1 blocks repacked (nibbles [N][K/2], 5th bits and {d, m} [N][K/32])
     const float *bias;       // [N] (null for logits)
     int N, K, B;
     float qscale;            // (n/h)^-0.25

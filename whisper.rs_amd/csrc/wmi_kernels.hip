@@ -828,7 +828,23 @@ __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K
 
 // NC = 128-element K chunks a lane prefetches per row (8 for K <= 1024, 16 for
 // the MLP-down GEMV at K = 4n <= 2048); longer rows loop.
-template <int EPI, int IN, int G, int NC>
+// q5_1 weights (repacked at load: per row K/2 bytes of nibbles in natural
+// order, then per 32-block a u32 of 5th bits and a u32 {f16 d, f16 m}):
+// eight weights starting at block offset sh, dequantised exactly as the host
+// loader does, w = f16(q * d + m) (unfused)
+__device__ __forceinline__ half8 q5_half8(uint32_t qn, uint32_t qh, uint32_t dm, int sh) {
+    const float d = h2f_bits((uint16_t)(dm & 0xffffu)), m = h2f_bits((uint16_t)(dm >> 16));
+    const uint32_t hb = qh >> sh;
+    half8 w;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const uint32_t qv = ((qn >> (4 * e)) & 15u) | (((hb >> e) & 1u) << 4);
+        w[e] = (f16)((float)qv * d + m);
+    }
+    return w;
+}
+
+template <int EPI, int IN, int G, int NC, int WQ>
 __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
     trace_begin(a.trace);
     constexpr int DG_NC = NC, DG_KB = NC * 128;
@@ -845,7 +861,11 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
     int rg = blockIdx.x;
     int rowbase = (rg * 4 + w) * 4 * G;
     const f16 *W = (const f16 *)a.W;
-    half8 wv[G][DG_NC];
+    half8 wv[G][WQ ? 1 : DG_NC];
+    uint32_t wqn[G][WQ ? DG_NC : 1], wqh[G][WQ ? DG_NC : 1], wdm[G][WQ ? DG_NC : 1];
+    const uint8_t *q5n = a.Wq5;
+    const uint32_t *q5h = (const uint32_t *)(a.Wq5 + (int64_t)N * K / 2);
+    const uint32_t *q5d = q5h + (int64_t)N * (K / 32);
     auto load_chunk = [&](int k0) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -853,10 +873,21 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
 #pragma unroll
             for (int c = 0; c < DG_NC; ++c) {
                 const int k = k0 + c * 128 + l16 * 8;
-                if (row < N && k < K) wv[g][c] = *(const half8 *)(W + (int64_t)row * K + k);
-                else
+                if constexpr (WQ) {
+                    if (row < N && k < K) {
+                        const int64_t e = (int64_t)row * K + k;
+                        wqn[g][c] = *(const uint32_t *)(q5n + e / 2);
+                        wqh[g][c] = q5h[e / 32];
+                        wdm[g][c] = q5d[e / 32];
+                    } else {
+                        wqn[g][c] = 0u; wqh[g][c] = 0u; wdm[g][c] = 0u;
+                    }
+                } else {
+                    if (row < N && k < K) wv[g][c] = *(const half8 *)(W + (int64_t)row * K + k);
+                    else
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) wv[g][c][e] = (f16)0.0f;
+                        for (int e = 0; e < 8; ++e) wv[g][c][e] = (f16)0.0f;
+                }
             }
         }
     };
@@ -948,12 +979,18 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
             for (int c = 0; c < DG_NC; ++c) {
                 const int k = k0 + c * 128 + l16 * 8;
                 if (k0 + c * 128 < K) {
+                    half8 wc[G];
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        if constexpr (WQ) wc[g] = q5_half8(wqn[g][c], wqh[g][c], wdm[g][c], k & 31);
+                        else wc[g] = wv[g][c];
+                    }
 #pragma unroll
                     for (int bb = 0; bb < DG_MAXB; ++bb) {
                         if (bb < B) {
                             const half8 xv = *(const half8 *)(xs + bb * K + k);
 #pragma unroll
-                            for (int g = 0; g < G; ++g) acc[g][bb] = dot8(wv[g][c], xv, acc[g][bb]);
+                            for (int g = 0; g < G; ++g) acc[g][bb] = dot8(wc[g], xv, acc[g][bb]);
                         }
                     }
                 }
@@ -1030,9 +1067,8 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
     trace_end(a.trace);
 }
 
-template <int EPI, int IN>
-static hipError_t dec_gemv_g(hipStream_t s, int G, const DecGemvArgs &a) {
-    (void)G;
+template <int EPI, int IN, int WQ>
+static hipError_t dec_gemv_g(hipStream_t s, const DecGemvArgs &a) {
     const size_t lds = (size_t)a.B * a.K * 2;
     dim3 block(256);
     // the vocabulary GEMV runs persistent: 4 workgroups per CU walk the row groups
@@ -1040,36 +1076,33 @@ static hipError_t dec_gemv_g(hipStream_t s, int G, const DecGemvArgs &a) {
     const int nrg = cdiv(a.N, 16);
     const dim3 grid(nrg < cap ? nrg : cap);
     if (a.K > 1024) {
-        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 16>, lds);
+        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 16, WQ>, lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 16>), grid, block, lds, s, a);
+        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 16, WQ>), grid, block, lds, s, a);
     } else {
-        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 8>, lds);
+        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 8, WQ>, lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 8>), grid, block, lds, s, a);
+        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 8, WQ>), grid, block, lds, s, a);
     }
     return hipGetLastError();
 }
 
+template <int EPI, int IN>
+static hipError_t dec_gemv_w(hipStream_t s, const DecGemvArgs &a) {
+    return a.Wq5 ? dec_gemv_g<EPI, IN, 1>(s, a) : dec_gemv_g<EPI, IN, 0>(s, a);
+}
+
+// (epilogue, input) pairs the decoder step uses
 hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a) {
     if (a.B < 1 || a.B > DG_MAXB || a.K % 128) return hipErrorInvalidValue;
     const int in = a.te ? 3 : (a.ln_w ? 0 : (a.parts ? 2 : 1));
-    const int G = 1;
-#define DGC(E)                                                     \
-    case E:                                                        \
-        if (in == 0) return dec_gemv_g<E, 0>(s, G, a);             \
-        if (in == 1) return dec_gemv_g<E, 1>(s, G, a);             \
-        if (in == 3) return dec_gemv_g<E, 3>(s, G, a);             \
-        return dec_gemv_g<E, 2>(s, G, a);
-    switch (epi) {
-        DGC(DEC_QKV)
-        DGC(DEC_Q)
-        DGC(DEC_GELU)
-        DGC(DEC_RESID)
-        DGC(DEC_LOGITS)
-        default: return hipErrorInvalidValue;
-    }
-#undef DGC
+    if (epi == DEC_QKV && in == 3) return dec_gemv_w<DEC_QKV, 3>(s, a);
+    if (epi == DEC_QKV && in == 0) return dec_gemv_w<DEC_QKV, 0>(s, a);
+    if (epi == DEC_GELU && in == 0) return dec_gemv_w<DEC_GELU, 0>(s, a);
+    if (epi == DEC_RESID && in == 1) return dec_gemv_w<DEC_RESID, 1>(s, a);
+    if (epi == DEC_RESID && in == 2) return dec_gemv_w<DEC_RESID, 2>(s, a);
+    if (epi == DEC_LOGITS && in == 0) return dec_gemv_w<DEC_LOGITS, 0>(s, a);
+    return hipErrorInvalidValue;
 }
 
 // ---- decoder attention, split over 128-key chunks --------------------------

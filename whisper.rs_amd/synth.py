@@ -181,12 +181,103 @@ def _vocab_tokens(n: int):
         yield (f" w{i}" if i < 50256 else f"<|special{i}|>").encode()
 
 
+# ----------------------------------------------------------------------------
+# ggml quantisation (QNT version 2 block layouts)
+# ----------------------------------------------------------------------------
+GGML_QNT_VERSION = 2
+QUANT_TYPES = {"q4_0": (2, 2), "q4_1": (3, 3), "q5_0": (6, 8), "q5_1": (7, 9), "q8_0": (8, 7)}  # -> (ttype, ftype)
+
+
+def _absmax_signed(x):
+    """ggml's 'max by absolute value, keeping the sign' per row of 32."""
+    i = np.abs(x).argmax(axis=1)
+    return x[np.arange(x.shape[0]), i]
+
+
+def _inv(d):
+    with np.errstate(divide="ignore"):
+        return np.where(d != 0, np.float32(1.0) / np.where(d != 0, d, np.float32(1.0)), np.float32(0.0)).astype(np.float32)
+
+
+def _qh_bits(q):
+    bits = np.arange(32, dtype=np.uint64)
+    return ((((q & 0x10) >> 4).astype(np.uint64) << bits).sum(axis=1)).astype("<u4")
+
+
+def quantize(w: np.ndarray, qtype: str) -> bytes:
+    """ggml quantize_row_<type>_ref (QNT v2 layouts) over rows of 32 weights."""
+    if qtype == "q5_1":
+        return quantize_q5_1(w)
+    x = np.ascontiguousarray(w, dtype=np.float32).reshape(-1, 32)
+    nb = x.shape[0]
+    if qtype == "q8_0":
+        d = np.abs(x).max(axis=1) / np.float32(127.0)
+        q = np.round(x * _inv(d)[:, None])  # roundf: half away from zero
+        q = np.where(np.abs(x * _inv(d)[:, None] - np.trunc(x * _inv(d)[:, None])) == 0.5,
+                     np.trunc(x * _inv(d)[:, None]) + np.sign(x), q)
+        blk = np.zeros(nb, dtype=[("d", "<f2"), ("qs", "i1", 32)])
+        blk["d"] = d.astype(np.float16)
+        blk["qs"] = q.astype(np.int8)
+        return blk.tobytes()
+    if qtype in ("q4_0", "q5_0"):
+        lv = 8 if qtype == "q4_0" else 16
+        d = _absmax_signed(x) / np.float32(-lv)
+        q = np.minimum(2 * lv - 1, (x * _inv(d)[:, None] + np.float32(lv + 0.5)).astype(np.int8).astype(np.int64))
+    else:  # q4_1
+        mn = x.min(axis=1)
+        d = (x.max(axis=1) - mn) / np.float32(15.0)
+        q = np.minimum(15, ((x - mn[:, None]) * _inv(d)[:, None] + np.float32(0.5)).astype(np.int8).astype(np.int64))
+    q &= 0xFF
+    qs = ((q[:, :16] & 0x0F) | ((q[:, 16:] & 0x0F) << 4)).astype(np.uint8)
+    if qtype == "q4_0":
+        blk = np.zeros(nb, dtype=[("d", "<f2"), ("qs", "u1", 16)])
+    elif qtype == "q4_1":
+        blk = np.zeros(nb, dtype=[("d", "<f2"), ("m", "<f2"), ("qs", "u1", 16)])
+        blk["m"] = mn.astype(np.float16)
+    else:
+        blk = np.zeros(nb, dtype=[("d", "<f2"), ("qh", "<u4"), ("qs", "u1", 16)])
+        blk["qh"] = _qh_bits(np.concatenate([q[:, :16], q[:, 16:]], axis=1))
+    blk["d"] = d.astype(np.float16)
+    blk["qs"] = qs
+    return blk.tobytes()
+
+
+def quantize_q5_1(w: np.ndarray) -> bytes:
+    """ggml quantize_row_q5_1_ref over rows of 32: {f16 d, f16 m, u32 qh, u8 qs[16]}.
+    f32 arithmetic as in ggml: d = (max - min) / 31, q = (int)((x - min) * (1/d) + 0.5);
+    element j < 16 in the low nibble of qs[j], element j + 16 in its high nibble,
+    bit 4 of element j in bit j of qh."""
+    x = np.ascontiguousarray(w, dtype=np.float32).reshape(-1, 32)
+    mn = x.min(axis=1)
+    mx = x.max(axis=1)
+    d = (mx - mn) / np.float32(31.0)
+    with np.errstate(divide="ignore"):
+        idv = np.where(d != 0, np.float32(1.0) / np.where(d != 0, d, np.float32(1.0)), np.float32(0.0)).astype(np.float32)
+    q = (((x - mn[:, None]) * idv[:, None]) + np.float32(0.5)).astype(np.int64) & 0xFF  # (uint8_t) cast
+    lo, hi = q[:, :16], q[:, 16:]
+    qs = ((lo & 0x0F) | ((hi & 0x0F) << 4)).astype(np.uint8)
+    bits = np.arange(16, dtype=np.uint64)
+    qh = ((((lo & 0x10) >> 4).astype(np.uint64) << bits).sum(axis=1) +
+          (((hi & 0x10) >> 4).astype(np.uint64) << (bits + 16)).sum(axis=1)).astype("<u4")
+    blk = np.zeros(x.shape[0], dtype=[("d", "<f2"), ("m", "<f2"), ("qh", "<u4"), ("qs", "u1", 16)])
+    blk["d"] = d.astype(np.float16)
+    blk["m"] = mn.astype(np.float16)
+    blk["qh"] = qh
+    blk["qs"] = qs
+    return blk.tobytes()
+
+
 def write_ggml(path: str, model: str = "base", hp_override: dict | None = None,
-               wscale: float = 0.02, n_vocab_file: int | None = None, tensor_hook=None) -> dict:
+               wscale: float = 0.02, n_vocab_file: int | None = None, tensor_hook=None,
+               quant: str | None = None) -> dict:
     """Write a synthetic ggml-v1 Whisper file; returns the hparams used.
-    tensor_hook(name, array) -> array may edit tensors before they are written."""
+    tensor_hook(name, array) -> array may edit tensors before they are written.
+    quant ("q5_1", "q8_0", ...) stores every 2-D weight matrix in that ggml block format,
+    as whisper.cpp's quantize tool does (conv kernels, biases, LN parameters
+    and positional embeddings keep their type); hparams.f16 then carries the
+    file ftype + 1000 * GGML_QNT_VERSION."""
     hp = dict(MODEL_DIMS[model])
-    hp["f16"] = 1
+    hp["f16"] = 1 if quant is None else QUANT_TYPES[quant][1] + 1000 * GGML_QNT_VERSION
     if hp_override:
         hp.update(hp_override)
     n_vocab_file = 50257 if n_vocab_file is None else n_vocab_file
@@ -208,10 +299,15 @@ def write_ggml(path: str, model: str = "base", hp_override: dict | None = None,
             ftype = 1 if arr.dtype == np.float16 else 0
             ne = tuple(reversed(shape))
             nb = name.encode()
+            if quant is not None and kind == "w" and len(shape) == 2:
+                ftype = QUANT_TYPES[quant][0]
+                payload = quantize(arr.astype(np.float32), quant)
+            else:
+                payload = arr.astype("<f2" if ftype else "<f4").tobytes()
             f.write(struct.pack("<iii", len(ne), len(nb), ftype))
             f.write(struct.pack(f"<{len(ne)}i", *ne))
             f.write(nb)
-            f.write(arr.astype("<f2" if ftype else "<f4").tobytes())
+            f.write(payload)
     os.replace(tmp, path)
     return hp
 
@@ -222,7 +318,11 @@ def model_path(model: str, cache_dir: str | None = None) -> str:
     os.makedirs(cache_dir, exist_ok=True)
     p = os.path.join(cache_dir, f"ggml-synth-{model}.bin")
     if not os.path.exists(p):
-        write_ggml(p, model)
+        base, _, quant = model.partition("-q")
+        if quant:  # e.g. "small-q5_1": the small model's weights in ggml q5_1
+            write_ggml(p, base, quant="q" + quant)
+        else:
+            write_ggml(p, model)
     return p
 
 
