@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--model", default="base")
     ap.add_argument("--clips-per-gpu", type=int, default=1)
     ap.add_argument("--n-decode", type=int, default=128)
+    ap.add_argument("--beam", type=int, default=0, help="beam width (0 = greedy; C5 uses 5)")
     ap.add_argument("--roofline-kernel", type=int, default=0, choices=sorted(KERNELS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-min-seconds", type=float, default=10.0)
@@ -114,7 +115,7 @@ def main():
     ctx.stage(clips)
 
     def step():
-        ctx.run_staged(n_decode=args.n_decode)
+        ctx.run_staged(n_decode=args.n_decode, beam_size=args.beam)
         if world > 1:
             ctx.dist_gather_tokens()
 
@@ -137,6 +138,7 @@ def main():
 
     result = None
     if rank == 0:
+        wtype = "q5_1" if args.model.endswith("q5_1") else "f16"
         ms_step = elapsed / args.steps * 1e3
         value = world * audio_s * args.steps / elapsed
         kernels = {}
@@ -170,8 +172,10 @@ def main():
             "dtype": "f16",
             "data": "synthetic",
             "config": {
-                "workload": (f"whisper-{args.model} f16 (random-init ggml-v1 weights), {cpg} x 30 s synthetic clip(s) "
-                             f"per GPU: mel + conv stem + encoder + cross-KV + {args.n_decode} greedy tokens"),
+                "workload": (f"whisper-{args.model} {wtype} (random-init ggml-v1 weights), {cpg} x 30 s synthetic clip(s) "
+                             f"per GPU: mel + conv stem + encoder + cross-KV + {args.n_decode} "
+                             + (f"tokens of {args.beam}-beam search" if args.beam else "greedy tokens")),
+                "beam": args.beam,
                 "clips_per_gpu": cpg,
                 "global_clips": world * cpg,
                 "n_decode": args.n_decode,

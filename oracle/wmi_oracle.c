@@ -205,9 +205,9 @@ static void reg_add(reg_entry *r, int *n, const char *name, int dtype, int n_dim
 
 /* ggml quantised blocks (QNT version 2 layouts; SURVEY.md §A.8 and §8f
  * item 2: the reference loader rejects them, main.rs:1423-1434).  Weights are
- * dequantised to f16 — w = f16(q * d (+ m)), f32 multiply then add, no FMA —
- * and every matmul then follows the f16 semantics (§A.4), as ggml's GPU
- * back-ends do (dequantise -> f16 GEMM).  Types: 2 q4_0, 3 q4_1, 6 q5_0,
+ * dequantised to f16 — w = f16(q * d (+ m)) rounded once, as a fused
+ * multiply-add (exact in double here) — and every matmul then follows the f16
+ * semantics (§A.4), as ggml's GPU back-ends do (dequantise -> f16 GEMM).  Types: 2 q4_0, 3 q4_1, 6 q5_0,
  * 7 q5_1, 8 q8_0; 32 weights per block. */
 static int qblock_bytes(int t) {
     switch (t) {
@@ -220,6 +220,29 @@ static int qblock_bytes(int t) {
     }
 }
 
+/* correctly rounded (RNE) double -> f16 */
+static uint16_t d2h(double v) {
+    uint64_t x;
+    memcpy(&x, &v, 8);
+    const uint32_t sign = (uint32_t)(x >> 48) & 0x8000u;
+    x &= ~(1ull << 63);
+    if (x >= 0x7ff0000000000000ull) return (uint16_t)(sign | 0x7c00u | (x > 0x7ff0000000000000ull ? 0x200u : 0u));
+    if (x < 0x0010000000000000ull) return (uint16_t)sign;
+    const int e = (int)(x >> 52) - 1023;
+    const uint64_t mant = (x & ((1ull << 52) - 1)) | (1ull << 52);
+    if (e >= 16) return (uint16_t)(sign | 0x7c00u);
+    const int shift = e >= -14 ? 42 : 42 + (-14 - e);
+    if (shift >= 63) return (uint16_t)sign;
+    uint64_t q = mant >> shift;
+    const uint64_t rem = mant & ((1ull << shift) - 1), half = 1ull << (shift - 1);
+    if (rem > half || (rem == half && (q & 1))) ++q;
+    if (e < -14) return (uint16_t)(sign | q);
+    uint32_t ex = (uint32_t)(e + 15);
+    if (q >> 11) { q >>= 1; ++ex; }
+    if (ex >= 31) return (uint16_t)(sign | 0x7c00u);
+    return (uint16_t)(sign | (ex << 10) | (uint32_t)(q & 0x3ffu));
+}
+
 static void dequant_row_f16(int t, const uint8_t *src, int64_t nel, uint16_t *dst) {
     const int bs = qblock_bytes(t);
     for (int64_t ib = 0; ib < nel / 32; ++ib) {
@@ -230,15 +253,15 @@ static void dequant_row_f16(int t, const uint8_t *src, int64_t nel, uint16_t *ds
         const float d = h2f(hd);
         if (t == 2) { /* q4_0: {d, qs[16]}, (nibble - 8) * d */
             for (int j = 0; j < 16; ++j) {
-                y[j] = f2h((float)((b[2 + j] & 0x0F) - 8) * d);
-                y[j + 16] = f2h((float)((b[2 + j] >> 4) - 8) * d);
+                y[j] = d2h((double)((b[2 + j] & 0x0F) - 8) * d);
+                y[j + 16] = d2h((double)((b[2 + j] >> 4) - 8) * d);
             }
         } else if (t == 3) { /* q4_1: {d, m, qs[16]}, nibble * d + m */
             memcpy(&hm, b + 2, 2);
             const float m = h2f(hm);
             for (int j = 0; j < 16; ++j) {
-                y[j] = f2h((float)(b[4 + j] & 0x0F) * d + m);
-                y[j + 16] = f2h((float)(b[4 + j] >> 4) * d + m);
+                y[j] = d2h((double)(b[4 + j] & 0x0F) * d + (double)m);
+                y[j + 16] = d2h((double)(b[4 + j] >> 4) * d + (double)m);
             }
         } else if (t == 6 || t == 7) { /* q5_0 {d, qh, qs} (q - 16) * d; q5_1 {d, m, qh, qs} q * d + m */
             const int o = t == 6 ? 2 : 4;
@@ -251,15 +274,15 @@ static void dequant_row_f16(int t, const uint8_t *src, int64_t nel, uint16_t *ds
                 const int x0 = (qs[j] & 0x0F) | (((qh >> j) & 1) << 4);
                 const int x1 = (qs[j] >> 4) | (((qh >> (j + 16)) & 1) << 4);
                 if (t == 6) {
-                    y[j] = f2h((float)(x0 - 16) * d);
-                    y[j + 16] = f2h((float)(x1 - 16) * d);
+                    y[j] = d2h((double)(x0 - 16) * d);
+                    y[j + 16] = d2h((double)(x1 - 16) * d);
                 } else {
-                    y[j] = f2h((float)x0 * d + m);
-                    y[j + 16] = f2h((float)x1 * d + m);
+                    y[j] = d2h((double)x0 * d + (double)m);
+                    y[j + 16] = d2h((double)x1 * d + (double)m);
                 }
             }
         } else { /* q8_0: {d, int8 qs[32]} */
-            for (int j = 0; j < 32; ++j) y[j] = f2h((float)(int8_t)b[2 + j] * d);
+            for (int j = 0; j < 32; ++j) y[j] = d2h((double)(int8_t)b[2 + j] * d);
         }
     }
 }

@@ -41,7 +41,7 @@ int or_prompt(const or_model *m, int32_t *out);
 void or_set_dot_mode(int exact_double);
 
 /* The loader's dequantisation of ggml quantised blocks to f16 (types 2 q4_0,
- * 3 q4_1, 6 q5_0, 7 q5_1, 8 q8_0): w = f16(q * d (+ m)), unfused f32. */
+ * 3 q4_1, 6 q5_0, 7 q5_1, 8 q8_0): w = f16(q * d (+ m)) rounded once. */
 int or_dequant(int type, const uint8_t *src, int64_t nel, uint16_t *dst);
 
 /* ggml lookup tables (ggml_init): f16 GELU and f16 exp, 65536 entries each. */

@@ -339,9 +339,10 @@ def test_quantised_micro(wmi, model_cache, qtype):
 
 def test_small_q5_1(wmi, model_cache):
     """C3: whisper small with q5_1 weights.  The decoder GEMVs stream the q5_1
-    blocks and dequantise in registers; the result must equal, bit for bit,
-    the same decoder reading the loader's dequantised f16 copies
-    (WMI_NO_Q5=1), which the oracle pins."""
+    blocks and dequantise in registers to exactly the loader's f16 weights
+    (a lane owns a whole 32-weight block, so the f32 summation is grouped
+    differently from the f16 GEMV's); both decoders (q5_1 blocks, and the
+    dequantised f16 copies with WMI_NO_Q5=1) are held to the oracle."""
     import os
     path = synth.model_path("small-q5_1", model_cache)
     om = pyoracle.OracleModel(path)
@@ -362,9 +363,12 @@ def test_small_q5_1(wmi, model_cache):
         ctx16.set_audio_ctx(1500)
         ctx16.pcm_to_mel_batch([pcm])
         ctx16.encode(1, 0)
-        np.testing.assert_array_equal(ctx16.decode_greedy(16, suppress_eot=True)[0], got)
-        toks = np.array(om.prompt() + list(got[:6]), np.int32)
-        np.testing.assert_array_equal(ctx16.decode_logits(toks, 0), ctx.decode_logits(toks, 0))
+        np.testing.assert_array_equal(ctx16.decode_greedy(16, suppress_eot=True)[0][:upto], ref[:upto])
+        toks = np.array(om.prompt() + list(ref[:6]), np.int32)
+        lref = om.decode_logits(ck_ref, cv_ref, toks, n_threads=threads())
+        e5 = np.abs(ctx.decode_logits(toks, 0) - lref).max()
+        e16 = np.abs(ctx16.decode_logits(toks, 0) - lref).max()
+        assert e5 <= 5e-3 and e16 <= 5e-3, (e5, e16)
     finally:
         ctx16.close()
         ctx.close()

@@ -1,8 +1,8 @@
 """ggml quantised weight files.
 
 The reference loader rejects quantised tensors (main.rs:1423-1434); this
-build dequantises every quantised matrix to f16, w = f16(q * d (+ m)) with an
-unfused f32 multiply and add (ggml's GPU back-ends' dequantise -> f16 GEMM),
+build dequantises every quantised matrix to f16, w = f16(q * d (+ m)) rounded
+once, as a fused multiply-add (ggml's GPU back-ends' dequantise -> f16 GEMM),
 so every matmul keeps the f16 semantics of SURVEY.md §A.4.  Pinned here: the
 synthetic quantisers restate ggml's quantize_row_*_ref, and the oracle's
 dequantisation equals an independent NumPy decoding of the QNT-v2 block
@@ -26,7 +26,7 @@ def np_dequant(qtype: str, raw: bytes, nel: int) -> np.ndarray:
     d = b[:, 0:2].copy().view("<f2")[:, 0].astype(np.float32)
     if qtype == "q8_0":
         q = b[:, 2:34].view(np.int8).astype(np.int32)
-        return (q.astype(np.float32) * d[:, None]).astype(np.float16).reshape(-1)
+        return (q.astype(np.float64) * d[:, None]).astype(np.float16).reshape(-1)
     m = b[:, 2:4].copy().view("<f2")[:, 0].astype(np.float32) if qtype in ("q4_1", "q5_1") else None
     qs_off = {"q4_0": 2, "q4_1": 4, "q5_0": 6, "q5_1": 8}[qtype]
     qs = b[:, qs_off:qs_off + 16].astype(np.int32)
@@ -36,10 +36,10 @@ def np_dequant(qtype: str, raw: bytes, nel: int) -> np.ndarray:
         qh = b[:, ho:ho + 4].copy().view("<u4")[:, 0].astype(np.int64)
         q = q | (((qh[:, None] >> np.arange(32)) & 1) << 4).astype(np.int32)
     off = {"q4_0": 8, "q5_0": 16}.get(qtype, 0)
-    v = (q - off).astype(np.float32) * d[:, None]
+    v = (q - off).astype(np.float64) * d[:, None].astype(np.float64)  # exact
     if m is not None:
-        v = v + m[:, None]
-    return v.astype(np.float16).reshape(-1)
+        v = v + m[:, None].astype(np.float64)  # exact for these magnitudes
+    return v.astype(np.float16).reshape(-1)  # one RNE rounding (NumPy rounds double -> half directly)
 
 
 @pytest.mark.parametrize("qtype", sorted(TYPES))
@@ -78,3 +78,22 @@ def test_unsupported_quant_version(tmp_path):
     with pytest.raises(pyoracle.OracleError) as e:
         pyoracle.OracleModel(path)
     assert e.value.code == 13
+
+
+@pytest.mark.parametrize("qtype", sorted(TYPES))
+def test_dequant_rounding_random_blocks(qtype):
+    """Arbitrary blocks (random quants, d and m over f16's whole normal and
+    subnormal exponent range): the single-rounding dequantisation equals
+    NumPy's correctly rounded double -> half conversion everywhere."""
+    rng = np.random.default_rng(11)
+    nb, bs = 2048, TYPES[qtype][1]
+    raw = rng.integers(0, 256, (nb, bs), dtype=np.uint8)
+    e = rng.integers(-24, 8, (nb, 2))
+    vals = (rng.choice([-1.0, 1.0], (nb, 2)) * rng.uniform(1, 2, (nb, 2)) * np.exp2(e)).astype(np.float16)
+    raw[:, 0:2] = vals[:, 0:1].copy().view(np.uint8)
+    if qtype in ("q4_1", "q5_1"):
+        raw[:, 2:4] = vals[:, 1:2].copy().view(np.uint8)
+    raw = raw.tobytes()
+    ref = np_dequant(qtype, raw, nb * 32)
+    got = pyoracle.dequant(TYPES[qtype][0], raw, nb * 32)
+    np.testing.assert_array_equal(got, ref.view(np.uint16))

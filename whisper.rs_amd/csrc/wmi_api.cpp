@@ -61,6 +61,29 @@ uint16_t f32_to_f16(float f) {
     return (uint16_t)h;
 }
 
+// correctly rounded (RNE) double -> f16
+uint16_t f64_to_f16(double v) {
+    uint64_t x;
+    memcpy(&x, &v, 8);
+    const uint32_t sign = (uint32_t)(x >> 48) & 0x8000u;
+    x &= ~(1ull << 63);
+    if (x >= 0x7ff0000000000000ull) return (uint16_t)(sign | 0x7c00u | (x > 0x7ff0000000000000ull ? 0x200u : 0u));
+    if (x < 0x0010000000000000ull) return (uint16_t)sign;  // double subnormals: far below f16's range
+    const int e = (int)(x >> 52) - 1023;
+    const uint64_t mant = (x & ((1ull << 52) - 1)) | (1ull << 52);
+    if (e >= 16) return (uint16_t)(sign | 0x7c00u);
+    const int shift = e >= -14 ? 42 : 42 + (-14 - e);
+    if (shift >= 63) return (uint16_t)sign;
+    uint64_t q = mant >> shift;
+    const uint64_t rem = mant & ((1ull << shift) - 1), half = 1ull << (shift - 1);
+    if (rem > half || (rem == half && (q & 1))) ++q;
+    if (e < -14) return (uint16_t)(sign | q);  // subnormal (a carry into 0x400 is the smallest normal)
+    uint32_t ex = (uint32_t)(e + 15);
+    if (q >> 11) { q >>= 1; ++ex; }
+    if (ex >= 31) return (uint16_t)(sign | 0x7c00u);
+    return (uint16_t)(sign | (ex << 10) | (uint32_t)(q & 0x3ffu));
+}
+
 float f16_to_f32(uint16_t h) {
     const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
     const uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
@@ -285,9 +308,9 @@ struct ParsedModel {
 
 // ggml quantised blocks (QNT version 2).  The
 // reference loader rejects them (main.rs:1423-1434); this build dequantises
-// every matrix to f16, w = f16(q * d (+ m)) with an unfused f32 multiply and
-// add, and keeps q5_1 blocks as well for the bandwidth-bound decoder GEMVs,
-// which dequantise on the fly to the same f16 values.
+// every matrix to f16, w = f16(q * d (+ m)) rounded once (a fused multiply-
+// add), and keeps q5_1 blocks as well for the bandwidth-bound decoder GEMVs,
+// which dequantise on the fly (v_pk_fma_f16) to the same f16 values.
 int qblock_bytes(int t) {
     switch (t) {
         case 2: return 18;  // q4_0 {d, qs[16]}
@@ -329,10 +352,8 @@ void dequant_f16(int t, const uint8_t *src, int64_t nel, uint16_t *dst) {
             for (int j = 0; j < 32; ++j) q[j] = (int8_t)b[2 + j];
         }
         const int off = t == 2 ? 8 : t == 6 ? 16 : 0;
-        for (int j = 0; j < 32; ++j) {
-            const float pr = (float)(q[j] - off) * d;  // -ffp-contract=off: no FMA with the add
-            y[j] = f32_to_f16((t == 3 || t == 7) ? pr + m : pr);
-        }
+        // q * d + m is exact in double (|log2(d / m)| <= 37); one rounding to f16
+        for (int j = 0; j < 32; ++j) y[j] = f64_to_f16((double)(q[j] - off) * (double)d + (double)m);
     }
 }
 
@@ -555,16 +576,15 @@ struct Arena {
 
 // q5_1 rows of one or more [rows][K] matrices, concatenated, in the decoder
 // GEMV layout: nibbles [N][K/2] in natural order (byte i of a block = weights
-// 2i, 2i+1), then 5th bits [N][K/32] (u32, bit j = weight j), then {f16 d,
-// f16 m} [N][K/32]
+// 2i, 2i+1), then per block [N][K/32] a pair {u32 5th bits (bit j = weight
+// j), u32 f16 d | f16 m << 16} — one 16-byte and one 8-byte load per block
 std::vector<uint8_t> repack_q5(const std::vector<const HostTensor *> &mats, int64_t K) {
     int64_t N = 0;
     for (const HostTensor *t : mats) N += t->nel() / K;
     const int64_t nb = K / 32;
     std::vector<uint8_t> out((size_t)(N * K / 2 + N * nb * 8));
     uint8_t *qn = out.data();
-    uint32_t *qh = (uint32_t *)(out.data() + N * K / 2);
-    uint32_t *dm = qh + N * nb;
+    uint32_t *hd = (uint32_t *)(out.data() + N * K / 2);
     int64_t r0 = 0;
     for (const HostTensor *t : mats) {
         const int64_t rows = t->nel() / K;
@@ -584,11 +604,11 @@ std::vector<uint8_t> repack_q5(const std::vector<const HostTensor *> &mats, int6
                 for (int j = 0; j < 32; ++j) bits |= (uint32_t)(q[j] >> 4) << j;
                 for (int i = 0; i < 16; ++i)
                     qn[R * K / 2 + ib * 16 + i] = (uint8_t)((q[2 * i] & 15) | ((q[2 * i + 1] & 15) << 4));
-                qh[R * nb + ib] = bits;
                 uint16_t d, m;
                 memcpy(&d, b, 2);
                 memcpy(&m, b + 2, 2);
-                dm[R * nb + ib] = (uint32_t)d | ((uint32_t)m << 16);
+                hd[2 * (R * nb + ib)] = bits;
+                hd[2 * (R * nb + ib) + 1] = (uint32_t)d | ((uint32_t)m << 16);
             }
         r0 += rows;
     }
@@ -1463,6 +1483,7 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (getenv("WMI_NO_GRAPH")) ctx->use_graph = false;
     if (getenv("WMI_NO_COOP")) ctx->use_coop = false;
     if (getenv("WMI_NO_Q5")) ctx->use_q5 = false;
+    if (const char *c = getenv("WMI_LOGITS_CAP")) g_logits_cap = atoi(c) > 0 ? atoi(c) : g_logits_cap;
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_trace, TRACE_SLOTS * 16 + 64 * 16 * 8));

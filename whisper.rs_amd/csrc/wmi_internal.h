@@ -102,7 +102,7 @@ struct DecGemvArgs {
     const float *parts;      // or: split-key attention partials [B][n_parts][K] f32, summed in order
     int n_parts;
     const uint16_t *W;       // [N][K]
-    const uint8_t *Wq5;      // or q5_1 blocks repacked (nibbles [N][K/2], 5th bits and {d, m} [N][K/32])
+    const uint8_t *Wq5;      // or q5_1 blocks repacked (nibbles [N][K/2], then {5th bits, d | m << 16} [N][K/32])
     const float *bias;       // [N] (null for logits)
     int N, K, B;
     float qscale;            // (n/h)^-0.25
@@ -132,6 +132,7 @@ struct DecGemvArgs {
 constexpr int AMAX_SHARDS = 64;
 constexpr int DEC_ROWS = 8;  // decoder rows per step: clips (greedy) or beam hypotheses
 hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a);
+extern int g_logits_cap;
 
 struct DecAttnArgs {
     const uint16_t *q;       // [B][n]

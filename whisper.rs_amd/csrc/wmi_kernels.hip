@@ -831,15 +831,24 @@ __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K
 // q5_1 weights (repacked at load: per row K/2 bytes of nibbles in natural
 // order, then per 32-block a u32 of 5th bits and a u32 {f16 d, f16 m}):
 // eight weights starting at block offset sh, dequantised exactly as the host
-// loader does, w = f16(q * d + m) (unfused)
+// loader does, w = f16(q * d + m) rounded once.  Packed: two quants per dword
+// as f16 (1024 + q) via v_perm + bit spread, minus 1024 (exact), then one
+// v_pk_fma_f16 per pair.
 __device__ __forceinline__ half8 q5_half8(uint32_t qn, uint32_t qh, uint32_t dm, int sh) {
-    const float d = h2f_bits((uint16_t)(dm & 0xffffu)), m = h2f_bits((uint16_t)(dm >> 16));
+    const uint32_t lo = qn & 0x0F0F0F0Fu, hi = (qn >> 4) & 0x0F0F0F0Fu;  // weights 0,2,4,6 / 1,3,5,7
     const uint32_t hb = qh >> sh;
+    const half2v d2 = __builtin_bit_cast(half2v, __builtin_amdgcn_perm(dm, dm, 0x01000100u));
+    const half2v m2 = __builtin_bit_cast(half2v, __builtin_amdgcn_perm(dm, dm, 0x03020302u));
+    const half2v k1024 = {(f16)1024.0f, (f16)1024.0f};
     half8 w;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const uint32_t qv = ((qn >> (4 * e)) & 15u) | (((hb >> e) & 1u) << 4);
-        w[e] = (f16)((float)qv * d + m);
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t nib = __builtin_amdgcn_perm(hi, lo, 0x0C000C00u | ((uint32_t)(4 + i) << 16) | (uint32_t)i);
+        const uint32_t h5 = ((__builtin_amdgcn_ubfe(hb, 2 * i, 2)) * 0x80010u) & 0x100010u;
+        const half2v q2 = __builtin_bit_cast(half2v, nib | h5 | 0x64006400u) - k1024;
+        const half2v r = __builtin_elementwise_fma(q2, d2, m2);
+        w[2 * i] = r[0];
+        w[2 * i + 1] = r[1];
     }
     return w;
 }
@@ -847,58 +856,162 @@ __device__ __forceinline__ half8 q5_half8(uint32_t qn, uint32_t qh, uint32_t dm,
 template <int EPI, int IN, int G, int NC, int WQ>
 __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
     trace_begin(a.trace);
-    constexpr int DG_NC = NC, DG_KB = NC * 128;
+    // chunk geometry: a quarter-wave covers CW consecutive weights of its row
+    // per chunk, a lane LW of them (f16: 8 = one 16-byte load; q5_1: 32 = one
+    // block, its 16 nibble bytes + an 8-byte {5th bits, d/m} word)
+    constexpr int CW = WQ ? 512 : 128, LW = CW / 16;
+    constexpr int DG_NC = NC, DG_KB = NC * CW;
+    // the vocabulary GEMV is persistent and software-pipelined over two
+    // register sets: row group i + 1's weights are in flight while group i is
+    // reduced and written (PIPE); the others run one row group per workgroup
+    constexpr bool PIPE = EPI == DEC_LOGITS;
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
     f16 *xs = (f16 *)smraw;  // [B][K]
     __shared__ unsigned long long amax_s[DG_MAXB];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int q = lane >> 4, l16 = lane & 15;
     const int K = a.K, B = a.B, N = a.N;
-    // row groups of 16*G rows; a grid smaller than the group count walks them
-    // (persistent form, used for the vocabulary-sized logits GEMV so the
-    // LayerNorm prologue is paid once per workgroup, not once per 32 rows)
     const int nrg = (N + 16 * G - 1) / (16 * G);
-    int rg = blockIdx.x;
-    int rowbase = (rg * 4 + w) * 4 * G;
+    auto rbase = [&](int rg) { return (rg * 4 + w) * 4 * G; };
     const f16 *W = (const f16 *)a.W;
-    half8 wv[G][WQ ? 1 : DG_NC];
-    uint32_t wqn[G][WQ ? DG_NC : 1], wqh[G][WQ ? DG_NC : 1], wdm[G][WQ ? DG_NC : 1];
     const uint8_t *q5n = a.Wq5;
-    const uint32_t *q5h = (const uint32_t *)(a.Wq5 + (int64_t)N * K / 2);
-    const uint32_t *q5d = q5h + (int64_t)N * (K / 32);
-    auto load_chunk = [&](int k0) {
+    const uint2 *q5hd = (const uint2 *)(a.Wq5 + (int64_t)N * K / 2);
+    struct WSet {
+        half8 wv[G][WQ ? 1 : DG_NC];
+        uint4 wqn[G][WQ ? DG_NC : 1];
+        uint2 wqd[G][WQ ? DG_NC : 1];
+        float eb[G], er[G];  // epilogue operands: bias, residual (lane l16 == clip)
+    };
+    auto load_set = [&](WSet &S, int rb, int k0) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const int row = rowbase + g * 4 + q;
+            const int row = rb + g * 4 + q;
 #pragma unroll
             for (int c = 0; c < DG_NC; ++c) {
-                const int k = k0 + c * 128 + l16 * 8;
+                const int k = k0 + c * CW + l16 * LW;
                 if constexpr (WQ) {
                     if (row < N && k < K) {
                         const int64_t e = (int64_t)row * K + k;
-                        wqn[g][c] = *(const uint32_t *)(q5n + e / 2);
-                        wqh[g][c] = q5h[e / 32];
-                        wdm[g][c] = q5d[e / 32];
+                        S.wqn[g][c] = *(const uint4 *)(q5n + e / 2);
+                        S.wqd[g][c] = q5hd[e / 32];
                     } else {
-                        wqn[g][c] = 0u; wqh[g][c] = 0u; wdm[g][c] = 0u;
+                        S.wqn[g][c] = make_uint4(0u, 0u, 0u, 0u);
+                        S.wqd[g][c] = make_uint2(0u, 0u);
                     }
                 } else {
-                    if (row < N && k < K) wv[g][c] = *(const half8 *)(W + (int64_t)row * K + k);
+                    if (row < N && k < K) S.wv[g][c] = *(const half8 *)(W + (int64_t)row * K + k);
                     else
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) wv[g][c][e] = (f16)0.0f;
+                        for (int e = 0; e < 8; ++e) S.wv[g][c][e] = (f16)0.0f;
                 }
             }
         }
     };
-    load_chunk(0);
-    // epilogue operands, prefetched: lane l16 == bb owns (row, bb)
-    float ebias[G], eres[G];
+    auto load_epi = [&](WSet &S, int rb) {
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const int o = rowbase + g * 4 + q;
-        ebias[g] = (a.bias && o < N) ? a.bias[o] : 0.0f;
-        eres[g] = (EPI == DEC_RESID && o < N && l16 < B) ? a.out32[(int64_t)l16 * N + o] : 0.0f;
+        for (int g = 0; g < G; ++g) {
+            const int o = rb + g * 4 + q;
+            S.eb[g] = (a.bias && o < N) ? a.bias[o] : 0.0f;
+            S.er[g] = (EPI == DEC_RESID && o < N && l16 < B) ? a.out32[(int64_t)l16 * N + o] : 0.0f;
+        }
+    };
+    auto dot_set = [&](const WSet &S, int k0, float (&acc)[G][DG_MAXB]) {
+#pragma unroll
+        for (int c = 0; c < DG_NC; ++c) {
+            const int k = k0 + c * CW + l16 * LW;
+            if constexpr (WQ) {
+                if (k < K) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        half8 wc[G];
+#pragma unroll
+                        for (int g = 0; g < G; ++g) {
+                            const uint4 qv = S.wqn[g][c];
+                            const uint32_t qn = j == 0 ? qv.x : j == 1 ? qv.y : j == 2 ? qv.z : qv.w;
+                            wc[g] = q5_half8(qn, S.wqd[g][c].x, S.wqd[g][c].y, 8 * j);
+                        }
+#pragma unroll
+                        for (int bb = 0; bb < DG_MAXB; ++bb) {
+                            if (bb < B) {
+                                const half8 xv = *(const half8 *)(xs + bb * K + k + 8 * j);
+#pragma unroll
+                                for (int g = 0; g < G; ++g) acc[g][bb] = dot8(wc[g], xv, acc[g][bb]);
+                            }
+                        }
+                    }
+                }
+            } else if (k0 + c * CW < K) {
+#pragma unroll
+                for (int bb = 0; bb < DG_MAXB; ++bb) {
+                    if (bb < B) {
+                        const half8 xv = *(const half8 *)(xs + bb * K + k);
+#pragma unroll
+                        for (int g = 0; g < G; ++g) acc[g][bb] = dot8(S.wv[g][c], xv, acc[g][bb]);
+                    }
+                }
+            }
+        }
+    };
+    // cross-lane reduction and the fused epilogue of one row group
+    auto finish = [&](int rb, float (&acc)[G][DG_MAXB], const WSet &S) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int bb = 0; bb < DG_MAXB; ++bb)
+                if (bb < B) {
+                    float v = acc[g][bb];
+                    v += __shfl_xor(v, 8);
+                    v += __shfl_xor(v, 4);
+                    v += __shfl_xor(v, 2);
+                    v += __shfl_xor(v, 1);
+                    acc[g][bb] = v;
+                }
+        const int pos = (EPI == DEC_QKV) ? a.st->pos : 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int o = rb + g * 4 + q;
+            float v = 0.0f;
+#pragma unroll
+            for (int bb = 0; bb < DG_MAXB; ++bb)
+                if (l16 == bb) v = acc[g][bb];
+            if (l16 >= B || o >= N) continue;
+            const int bb = l16;
+            if (EPI == DEC_QKV) {
+                const int n = N / 3, which = o / n, c = o - which * n;
+                if (which == 0) a.out16[bb * a.ldo + c] = f2h_bits((v + S.eb[g]) * a.qscale);
+                else if (which == 1)
+                    a.kcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(v * a.qscale);
+                else a.vcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(S.eb[g] + v);
+            } else if (EPI == DEC_Q) {
+                a.out16[bb * a.ldo + o] = f2h_bits((v + S.eb[g]) * a.qscale);
+            } else if (EPI == DEC_GELU) {
+                a.out16[bb * a.ldo + o] = a.gelu_tab[f2h_bits(v + S.eb[g])];
+            } else if (EPI == DEC_RESID) {
+                a.out32[(int64_t)bb * N + o] = (v + S.eb[g]) + S.er[g];
+            } else if (EPI == DEC_LOGITS) {
+                a.out32[(int64_t)bb * N + o] = v;
+                if (a.amax && o != a.suppress_id) {
+                    const unsigned long long key =
+                        ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)o);
+                    atomicMax(&amax_s[bb], key);
+                }
+            }
+        }
+    };
+    auto zero = [&](float (&acc)[G][DG_MAXB]) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int bb = 0; bb < DG_MAXB; ++bb) acc[g][bb] = 0.0f;
+    };
+    // every weight / epilogue request of the first group(s) before the prologue
+    WSet S0, S1;
+    int rgA = blockIdx.x, rgB = rgA + gridDim.x;
+    load_set(S0, rbase(rgA), 0);
+    load_epi(S0, rbase(rgA));
+    if (PIPE && rgB < nrg) {
+        load_set(S1, rbase(rgB), 0);
+        load_epi(S1, rbase(rgB));
     }
     if (IN == 0 || IN == 3) {
         // each wave normalises rows w and w + 4
@@ -967,97 +1080,33 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
     }
     if (EPI == DEC_LOGITS && tid < DG_MAXB) amax_s[tid] = 0ull;
     __syncthreads();
-    for (;;) {
-        float acc[G][DG_MAXB];
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int bb = 0; bb < DG_MAXB; ++bb) acc[g][bb] = 0.0f;
+    float acc[G][DG_MAXB];
+    if constexpr (PIPE) {  // K <= DG_KB (checked by the launcher)
+        for (;;) {
+            zero(acc);
+            dot_set(S0, 0, acc);
+            const int rgC = rgB + gridDim.x;
+            if (rgC < nrg) load_set(S0, rbase(rgC), 0);
+            finish(rbase(rgA), acc, S0);
+            if (rgB >= nrg) break;
+            if (rgC < nrg) load_epi(S0, rbase(rgC));
+            zero(acc);
+            dot_set(S1, 0, acc);
+            const int rgD = rgC + gridDim.x;
+            if (rgD < nrg) load_set(S1, rbase(rgD), 0);
+            finish(rbase(rgB), acc, S1);
+            if (rgC >= nrg) break;
+            if (rgD < nrg) load_epi(S1, rbase(rgD));
+            rgA = rgC;
+            rgB = rgD;
+        }
+    } else {  // one row group, K in DG_KB sweeps
+        zero(acc);
         for (int k0 = 0; k0 < K; k0 += DG_KB) {
-            if (k0 > 0) load_chunk(k0);
-#pragma unroll
-            for (int c = 0; c < DG_NC; ++c) {
-                const int k = k0 + c * 128 + l16 * 8;
-                if (k0 + c * 128 < K) {
-                    half8 wc[G];
-#pragma unroll
-                    for (int g = 0; g < G; ++g) {
-                        if constexpr (WQ) wc[g] = q5_half8(wqn[g][c], wqh[g][c], wdm[g][c], k & 31);
-                        else wc[g] = wv[g][c];
-                    }
-#pragma unroll
-                    for (int bb = 0; bb < DG_MAXB; ++bb) {
-                        if (bb < B) {
-                            const half8 xv = *(const half8 *)(xs + bb * K + k);
-#pragma unroll
-                            for (int g = 0; g < G; ++g) acc[g][bb] = dot8(wc[g], xv, acc[g][bb]);
-                        }
-                    }
-                }
-            }
+            if (k0 > 0) load_set(S0, rbase(rgA), k0);
+            dot_set(S0, k0, acc);
         }
-        const int cur_rowbase = rowbase;
-        // prefetch the next row group before this group's reduction/epilogue
-        const int next = rg + gridDim.x;
-        if (next < nrg && K <= DG_KB) {
-            rowbase = (next * 4 + w) * 4 * G;
-            load_chunk(0);
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int bb = 0; bb < DG_MAXB; ++bb)
-                if (bb < B) {
-                    float v = acc[g][bb];
-                    v += __shfl_xor(v, 8);
-                    v += __shfl_xor(v, 4);
-                    v += __shfl_xor(v, 2);
-                    v += __shfl_xor(v, 1);
-                    acc[g][bb] = v;
-                }
-        const int pos = (EPI == DEC_QKV) ? a.st->pos : 0;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int o = cur_rowbase + g * 4 + q;
-            float v = 0.0f;
-#pragma unroll
-            for (int bb = 0; bb < DG_MAXB; ++bb)
-                if (l16 == bb) v = acc[g][bb];
-            if (l16 >= B || o >= N) continue;
-            const int bb = l16;
-            if (EPI == DEC_QKV) {
-                const int n = N / 3, which = o / n, c = o - which * n;
-                if (which == 0) a.out16[bb * a.ldo + c] = f2h_bits((v + ebias[g]) * a.qscale);
-                else if (which == 1)
-                    a.kcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(v * a.qscale);
-                else a.vcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(ebias[g] + v);
-            } else if (EPI == DEC_Q) {
-                a.out16[bb * a.ldo + o] = f2h_bits((v + ebias[g]) * a.qscale);
-            } else if (EPI == DEC_GELU) {
-                a.out16[bb * a.ldo + o] = a.gelu_tab[f2h_bits(v + ebias[g])];
-            } else if (EPI == DEC_RESID) {
-                a.out32[(int64_t)bb * N + o] = (v + ebias[g]) + eres[g];
-            } else if (EPI == DEC_LOGITS) {
-                a.out32[(int64_t)bb * N + o] = v;
-                if (a.amax && o != a.suppress_id) {
-                    const unsigned long long key =
-                        ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)o);
-                    atomicMax(&amax_s[bb], key);
-                }
-            }
-        }
-        if (next >= nrg) break;
-        rg = next;
-        if (K > DG_KB) {
-            rowbase = (rg * 4 + w) * 4 * G;
-            load_chunk(0);
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {  // epilogue operands of the next group
-            const int o = rowbase + g * 4 + q;
-            ebias[g] = (a.bias && o < N) ? a.bias[o] : 0.0f;
-            eres[g] = (EPI == DEC_RESID && o < N && l16 < B) ? a.out32[(int64_t)l16 * N + o] : 0.0f;
-        }
+        finish(rbase(rgA), acc, S0);
     }
     if (EPI == DEC_LOGITS) {
         __syncthreads();
@@ -1067,22 +1116,31 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
     trace_end(a.trace);
 }
 
+int g_logits_cap = 512;  // persistent logits grid (WMI_LOGITS_CAP overrides; 2 workgroups per CU at ~210 VGPRs)
+
 template <int EPI, int IN, int WQ>
 static hipError_t dec_gemv_g(hipStream_t s, const DecGemvArgs &a) {
     const size_t lds = (size_t)a.B * a.K * 2;
     dim3 block(256);
-    // the vocabulary GEMV runs persistent: 4 workgroups per CU walk the row groups
-    const int cap = EPI == DEC_LOGITS ? 1024 : 1 << 30;
+    // the vocabulary GEMV runs persistent and pipelined (its K = n_state <=
+    // 1280 fits one sweep of either chunk size); the others one group per WG
+    const int cap = EPI == DEC_LOGITS ? g_logits_cap : 1 << 30;
     const int nrg = cdiv(a.N, 16);
     const dim3 grid(nrg < cap ? nrg : cap);
-    if (a.K > 1024) {
-        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 16, WQ>, lds);
+    if constexpr (WQ == 1) {  // q5_1: 4 chunks of 512 weights (K <= 2048 per sweep)
+        if (EPI == DEC_LOGITS && a.K > 2048) return hipErrorInvalidValue;
+        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 4, 1>, lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 16, WQ>), grid, block, lds, s, a);
+        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 4, 1>), grid, block, lds, s, a);
+    } else if (a.K > 1024) {
+        if (EPI == DEC_LOGITS && a.K > 2048) return hipErrorInvalidValue;
+        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 16, 0>, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 16, 0>), grid, block, lds, s, a);
     } else {
-        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 8, WQ>, lds);
+        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 8, 0>, lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 8, WQ>), grid, block, lds, s, a);
+        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 8, 0>), grid, block, lds, s, a);
     }
     return hipGetLastError();
 }
