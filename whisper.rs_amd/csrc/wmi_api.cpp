@@ -206,6 +206,9 @@ struct wmi_context {
     uint16_t *dq16 = nullptr, *datt16 = nullptr, *dhid16 = nullptr;
     float *dS = nullptr, *dcmax = nullptr, *dopart = nullptr;
     XSync *dsync = nullptr;     // [n_text_layer][8][n_text_head]
+    float *dwoparts = nullptr;  // [8][n_text_head][n_text_state] per-head output-projection partials
+    float *dx2 = nullptr;       // second residual-stream buffer (ping-pong with dx when fused)
+    bool fuse_wo = true;        // WMI_NO_FUSE=1: separate output-projection GEMV
     // beam search (config C5)
     BeamPart *dbparts = nullptr;
     BeamState *dbstate = nullptr;
@@ -244,9 +247,16 @@ struct wmi_context {
     hipEvent_t ev[8] = {};
     wmi_timings timings{};
     // decode graph cache
-    hipGraphExec_t g_exec = nullptr;
-    hipGraph_t g_graph = nullptr;
-    std::string g_key;
+    struct Graph { hipGraph_t graph = nullptr; hipGraphExec_t exec = nullptr; };
+    std::map<std::string, Graph> graphs;  // captured decoder steps by configuration
+    int self_mk = 512;                    // key capacity of the self-attention launch being enqueued
+    void clear_graphs() {
+        for (auto &kv : graphs) {
+            if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+            if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
+        }
+        graphs.clear();
+    }
     bool use_graph = true;
     bool use_coop = true;
     // WMI_TRACE=1: per-launch device timeline of the last decoder step
@@ -846,6 +856,8 @@ int alloc_workspace(wmi_context *ctx) {
     const size_t o_S = A.take(Bd * Hd * Smax * 4);
     const size_t o_cmax = A.take(Bd * Hd * Cmax * 4);
     const size_t o_opart = A.take(Bd * Cmax * nt * 4);
+    const size_t o_woparts = A.take(R * Hd * nt * 4);
+    const size_t o_dx2 = A.take(R * nt * 4);
     const size_t sync_bytes = (size_t)Lt * 8 * Hd * sizeof(XSync);
     const size_t o_sync = A.take(sync_bytes + 256);
     const size_t o_amax = A.take(8 * AMAX_SHARDS * 8);
@@ -890,6 +902,8 @@ int alloc_workspace(wmi_context *ctx) {
     for (int64_t r = 0; r < R; ++r)
         for (int j = 0; j < hp.n_text_ctx; ++j) ctx->kvsrc_init[(size_t)r * hp.n_text_ctx + j] = (int32_t)r;
     ctx->dsync = (XSync *)(b + o_sync);
+    ctx->dwoparts = (float *)(b + o_woparts);
+    ctx->dx2 = (float *)(b + o_dx2);
     ctx->derr = (uint32_t *)(b + o_sync + sync_bytes);
     ctx->sync_bytes = sync_bytes + 256;
     ctx->s_stride = (int)Smax;
@@ -1090,20 +1104,25 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     const bool beam = ctx->beam_k > 0;
     // per layer: [LN+QKV (+embed at l=0)] [self-attn] [Wo+res] [LN+Wcq+cross scores]
     //            [cross softmax+PV] [Wco+res] [LN+W0+GELU] [W1+res]; then LN+logits+argmax
+    // residual stream: dx, or with the fused output projection alternating
+    // dx / dx2 (the cross-attention prologue writes the updated stream to the
+    // other buffer while its sibling workgroups still read this one)
+    float *X[2] = {ctx->dx, ctx->dx2};
+    int cur = 0;
     for (int l = 0; l < hp.n_text_layer; ++l) {
         const DecLayerDev &d = ctx->dec[l];
         uint16_t *kc = ctx->kcache + (size_t)l * DEC_ROWS * hp.n_text_ctx * n;
         uint16_t *vc = ctx->vcache + (size_t)l * DEC_ROWS * hp.n_text_ctx * n;
         DecGemvArgs g{};
         const bool q5 = ctx->use_q5;
-        g.x = ctx->dx; g.ln_w = d.ln1_w; g.ln_b = d.ln1_b; g.W = d.wqkv; g.bias = d.bqkv; g.N = 3 * n; g.K = n; g.B = B;
+        g.x = X[cur]; g.ln_w = d.ln1_w; g.ln_b = d.ln1_b; g.W = d.wqkv; g.bias = d.bqkv; g.N = 3 * n; g.K = n; g.B = B;
         g.Wq5 = q5 ? d.wqkv5 : nullptr;
         g.qscale = qs; g.out16 = ctx->dq16; g.ldo = n; g.kcache = kc; g.vcache = vc; g.n_text_ctx = hp.n_text_ctx;
         g.st = ctx->dstate;
         if (l == 0) {
             g.te = ctx->te; g.pe = ctx->d_pe; g.feed = ctx->dfeed; g.feed_len = feed_len; g.feed_stride = feed_stride;
             g.amax = ctx->damax; g.tokens_out = ctx->dtokens + (size_t)b0 * out_stride; g.out_stride = out_stride;
-            g.x_out = ctx->dx;
+            g.x_out = X[cur];
             if (beam) {
                 g.tokens_out = nullptr;
                 g.beam_tok = ctx->dbstate->tok;
@@ -1113,6 +1132,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         HIPCHK(ctx, launch_dec_gemv(s, DEC_QKV, g));
         DecAttnArgs at{};
         at.q = ctx->dq16; at.K = kc; at.V = vc; at.clip_stride = (int64_t)hp.n_text_ctx * n; at.M_fixed = 0;
+        at.mk = ctx->self_mk; at.err = ctx->derr;
         at.st = ctx->dstate; at.S = ctx->dS; at.s_stride = ctx->s_stride; at.cmax = ctx->dcmax;
         at.opart = ctx->dopart; at.n_chunks = 1; at.exp_tab = ctx->exp_tab; at.n_exp = ctx->n_exp;
         at.H = H; at.n = n; at.B = B;
@@ -1122,14 +1142,20 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
             at.kv_src = ctx->dkvsrc;
             at.kv_src_stride = hp.n_text_ctx;
         }
+        if (ctx->fuse_wo) {  // per-head output-projection partials; residual in the next kernel
+            at.Wo = d.wo;
+            at.wo_parts = ctx->dwoparts;
+        }
         at.trace = tslot(ctx, "self_attn", l);
         HIPCHK(ctx, launch_dec_attn(s, at));
-        g = DecGemvArgs{};
-        g.parts = ctx->dopart; g.n_parts = 1; g.W = d.wo; g.bias = d.bo; g.N = n; g.K = n; g.B = B;
-        g.Wq5 = q5 ? d.wo5 : nullptr;
-        g.out32 = ctx->dx;
-        g.trace = tslot(ctx, "wo", l);
-        HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
+        if (!ctx->fuse_wo) {
+            g = DecGemvArgs{};
+            g.parts = ctx->dopart; g.n_parts = 1; g.W = d.wo; g.bias = d.bo; g.N = n; g.K = n; g.B = B;
+            g.Wq5 = q5 ? d.wo5 : nullptr;
+            g.out32 = X[cur];
+            g.trace = tslot(ctx, "wo", l);
+            HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
+        }
         const int c_cross = (T + 127) / 128;
         at = DecAttnArgs{};
         at.K = ctx->ck + ((size_t)l * Bt + b0) * T * n;
@@ -1137,33 +1163,37 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         at.clip_stride = (int64_t)T * n; at.M_fixed = T; at.st = ctx->dstate;
         at.S = ctx->dS; at.s_stride = ctx->s_stride; at.cmax = ctx->dcmax; at.opart = ctx->dopart;
         at.n_chunks = c_cross; at.exp_tab = ctx->exp_tab; at.n_exp = ctx->n_exp; at.H = H; at.n = n; at.B = B;
-        at.x = ctx->dx; at.ln_w = d.lnc_w; at.ln_b = d.lnc_b; at.Wq = d.wcq; at.bq = d.bcq; at.qscale = qs;
+        at.x = X[cur]; at.ln_w = d.lnc_w; at.ln_b = d.lnc_b; at.Wq = d.wcq; at.bq = d.bcq; at.qscale = qs;
         at.sync = ctx->use_coop ? ctx->dsync + (size_t)l * 8 * H : nullptr;
         at.err = ctx->derr;
         at.clip_div = beam ? B : 1;  // beam rows all read clip b0's cross K/V
+        if (ctx->fuse_wo) {
+            at.res_parts = ctx->dwoparts; at.res_bias = d.bo; at.x_out = X[cur ^ 1];
+            cur ^= 1;
+        }
         at.trace = tslot(ctx, "cross_attn", l);
         at.phase = ctx->trace_on ? ctx->d_trace + 2 * TRACE_SLOTS + 16 * l : nullptr;
         HIPCHK(ctx, launch_dec_attn(s, at));
         g = DecGemvArgs{};
         g.parts = ctx->dopart; g.n_parts = c_cross; g.W = d.wco; g.bias = d.bco; g.N = n; g.K = n; g.B = B;
         g.Wq5 = q5 ? d.wco5 : nullptr;
-        g.out32 = ctx->dx;
+        g.out32 = X[cur];
         g.trace = tslot(ctx, "wco", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
         g = DecGemvArgs{};
-        g.x = ctx->dx; g.ln_w = d.ln2_w; g.ln_b = d.ln2_b; g.W = d.w0; g.bias = d.b0; g.N = 4 * n; g.K = n; g.B = B;
+        g.x = X[cur]; g.ln_w = d.ln2_w; g.ln_b = d.ln2_b; g.W = d.w0; g.bias = d.b0; g.N = 4 * n; g.K = n; g.B = B;
         g.Wq5 = q5 ? d.w05 : nullptr;
         g.out16 = ctx->dhid16; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
         g.trace = tslot(ctx, "mlp0", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_GELU, g));
         g = DecGemvArgs{};
-        g.xin16 = ctx->dhid16; g.W = d.w1; g.bias = d.b1; g.N = n; g.K = 4 * n; g.B = B; g.out32 = ctx->dx;
+        g.xin16 = ctx->dhid16; g.W = d.w1; g.bias = d.b1; g.N = n; g.K = 4 * n; g.B = B; g.out32 = X[cur];
         g.Wq5 = q5 ? d.w15 : nullptr;
         g.trace = tslot(ctx, "mlp1", l);
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
     }
     DecGemvArgs g{};
-    g.x = ctx->dx; g.ln_w = ctx->dln_w; g.ln_b = ctx->dln_b; g.W = ctx->te; g.N = hp.n_vocab; g.K = n; g.B = B;
+    g.x = X[cur]; g.ln_w = ctx->dln_w; g.ln_b = ctx->dln_b; g.W = ctx->te; g.N = hp.n_vocab; g.K = n; g.B = B;
     g.Wq5 = ctx->use_q5 ? ctx->te5 : nullptr;
     g.out32 = ctx->dlogits; g.amax = ctx->damax; g.suppress_id = suppress_eot ? ctx->sp.eot : -1;
     g.st_advance = ctx->dstate;
@@ -1187,49 +1217,71 @@ int ensure_decode_buffers(wmi_context *ctx, int feed_elems, size_t token_elems) 
         if (ctx->dfeed) HIPCHK(ctx, hipFree(ctx->dfeed));
         HIPCHK(ctx, hipMalloc(&ctx->dfeed, (size_t)feed_elems * 4));
         ctx->feed_cap = feed_elems;
-        ctx->g_key.clear();
+        ctx->clear_graphs();
     }
     if (token_elems > ctx->tokens_cap) {
         if (ctx->dtokens) HIPCHK(ctx, hipFree(ctx->dtokens));
         HIPCHK(ctx, hipMalloc(&ctx->dtokens, token_elems * 4));
         HIPCHK(ctx, hipMemset(ctx->dtokens, 0, token_elems * 4));
         ctx->tokens_cap = token_elems;
-        ctx->g_key.clear();
+        ctx->clear_graphs();
     }
     return WMI_OK;
 }
 
-// run `steps` decoder steps for clips [b0, b0+B), via a captured hipGraph
+// device error word of a decode run: bit 0 cross-attention exchange timeout,
+// bit 1 self-attention launched with too small a key capacity
+int dec_err(wmi_context *ctx, uint32_t err) {
+    if (err & 1u) return set_err(ctx, WMI_E_HIP, "cross-attention exchange timed out (workgroups not co-resident)");
+    return set_err(ctx, WMI_E_HIP, "internal: self-attention key capacity below pos + 1 (err word %u)", err);
+}
+
+// self-attention key capacity for M = pos + 1 keys
+int self_mk_for(int M) { return M <= 64 ? 64 : M <= 128 ? 128 : M <= 256 ? 256 : 512; }
+
+// run `steps` decoder steps for clips [b0, b0+B), the first at position pos0,
+// via captured hipGraphs: one per configuration and self-attention key
+// capacity, so a chunk is split where pos + 1 crosses 64 / 128 / 256
 int run_dec_steps(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride, int suppress_eot, int out_stride,
-                  int steps) {
-    if (!ctx->use_graph) {
-        for (int i = 0; i < steps; ++i) {
-            if (ctx->trace_on) HIPCHK(ctx, hipMemsetAsync(ctx->d_trace, 0xff, TRACE_SLOTS * 16, ctx->stream));
-            int rc = enqueue_dec_step(ctx, b0, B, feed_len, feed_stride, suppress_eot, out_stride);
-            if (rc) return rc;
+                  int pos0, int steps) {
+    for (int done = 0; done < steps;) {
+        const int mk = self_mk_for(pos0 + done + 1);
+        int n = steps - done;
+        if (mk < 512 && pos0 + done + n > mk) n = mk - (pos0 + done);
+        ctx->self_mk = mk;
+        if (!ctx->use_graph) {
+            for (int i = 0; i < n; ++i) {
+                if (ctx->trace_on) HIPCHK(ctx, hipMemsetAsync(ctx->d_trace, 0xff, TRACE_SLOTS * 16, ctx->stream));
+                int rc = enqueue_dec_step(ctx, b0, B, feed_len, feed_stride, suppress_eot, out_stride);
+                if (rc) return rc;
+            }
+            done += n;
+            continue;
         }
-        return WMI_OK;
-    }
-    char key[160];
-    snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%p/%p/%d/%d", b0, B, feed_len, feed_stride, suppress_eot,
-             out_stride, ctx->enc_T, ctx->enc_clips, (void *)ctx->dfeed, (void *)ctx->dtokens, ctx->beam_k,
-             ctx->beam_max_tokens);
-    if (ctx->g_key != key) {
-        if (ctx->g_exec) { (void)hipGraphExecDestroy(ctx->g_exec); ctx->g_exec = nullptr; }
-        if (ctx->g_graph) { (void)hipGraphDestroy(ctx->g_graph); ctx->g_graph = nullptr; }
-        HIPCHK(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-        int rc = enqueue_dec_step(ctx, b0, B, feed_len, feed_stride, suppress_eot, out_stride);
-        hipGraph_t graph = nullptr;
-        hipError_t ce = hipStreamEndCapture(ctx->stream, &graph);
-        if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
-        HIPCHK(ctx, ce);
-        ctx->g_graph = graph;
-        HIPCHK(ctx, hipGraphInstantiate(&ctx->g_exec, graph, nullptr, nullptr, 0));
-        ctx->g_key = key;
-    }
-    for (int i = 0; i < steps; ++i) {
-        if (ctx->trace_on) HIPCHK(ctx, hipMemsetAsync(ctx->d_trace, 0xff, TRACE_SLOTS * 16, ctx->stream));
-        HIPCHK(ctx, hipGraphLaunch(ctx->g_exec, ctx->stream));
+        char key[192];
+        snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%p/%p/%d/%d/%d", b0, B, feed_len, feed_stride, suppress_eot,
+                 out_stride, ctx->enc_T, ctx->enc_clips, (void *)ctx->dfeed, (void *)ctx->dtokens, ctx->beam_k,
+                 ctx->beam_max_tokens, mk);
+        auto it = ctx->graphs.find(key);
+        if (it == ctx->graphs.end()) {
+            if (ctx->graphs.size() >= 32) ctx->clear_graphs();
+            HIPCHK(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+            int rc = enqueue_dec_step(ctx, b0, B, feed_len, feed_stride, suppress_eot, out_stride);
+            hipGraph_t graph = nullptr;
+            hipError_t ce = hipStreamEndCapture(ctx->stream, &graph);
+            if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
+            HIPCHK(ctx, ce);
+            wmi_context::Graph g;
+            g.graph = graph;
+            hipError_t ie = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+            if (ie != hipSuccess) { (void)hipGraphDestroy(graph); HIPCHK(ctx, ie); }
+            it = ctx->graphs.emplace(key, g).first;
+        }
+        for (int i = 0; i < n; ++i) {
+            if (ctx->trace_on) HIPCHK(ctx, hipMemsetAsync(ctx->d_trace, 0xff, TRACE_SLOTS * 16, ctx->stream));
+            HIPCHK(ctx, hipGraphLaunch(it->second.exec, ctx->stream));
+        }
+        done += n;
     }
     return WMI_OK;
 }
@@ -1263,7 +1315,7 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
         while (done_steps < total_steps) {
             int chunk = total_steps - done_steps;
             if (early_stop && chunk > 32) chunk = 32;
-            rc = run_dec_steps(ctx, b0, B, np, np, suppress_eot, n_gen, chunk);
+            rc = run_dec_steps(ctx, b0, B, np, np, suppress_eot, n_gen, done_steps, chunk);
             if (rc) return rc;
             done_steps += chunk;
             if (early_stop && done_steps < total_steps && done_steps >= np) {
@@ -1294,7 +1346,7 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
         uint32_t err = 0;
         HIPCHK(ctx, hipMemcpyAsync(&err, ctx->derr, 4, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        if (err) return set_err(ctx, WMI_E_HIP, "cross-attention exchange timed out (workgroups not co-resident)");
+        if (err) return dec_err(ctx, err);
     }
     if (ctx->trace_on) {
         const int rc2 = trace_dump(ctx);
@@ -1355,7 +1407,7 @@ int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_st
         while (done_steps < total_steps) {
             int chunk = total_steps - done_steps;
             if (early_stop && chunk > 32) chunk = 32;
-            rc = run_dec_steps(ctx, clip, K, np, np, suppress_eot, 1, chunk);
+            rc = run_dec_steps(ctx, clip, K, np, np, suppress_eot, 1, done_steps, chunk);
             if (rc) return rc;
             done_steps += chunk;
             if (early_stop && done_steps < total_steps) {
@@ -1408,7 +1460,7 @@ int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_st
     }
     uint32_t err = 0;
     HIPCHK(ctx, hipMemcpy(&err, ctx->derr, 4, hipMemcpyDeviceToHost));
-    if (err) return set_err(ctx, WMI_E_HIP, "cross-attention exchange timed out (workgroups not co-resident)");
+    if (err) return dec_err(ctx, err);
     return WMI_OK;
 }
 
@@ -1483,6 +1535,7 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (getenv("WMI_NO_GRAPH")) ctx->use_graph = false;
     if (getenv("WMI_NO_COOP")) ctx->use_coop = false;
     if (getenv("WMI_NO_Q5")) ctx->use_q5 = false;
+    if (getenv("WMI_NO_FUSE")) ctx->fuse_wo = false;
     if (const char *c = getenv("WMI_LOGITS_CAP")) g_logits_cap = atoi(c) > 0 ? atoi(c) : g_logits_cap;
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;
@@ -1497,8 +1550,7 @@ void wmi_free(wmi_context *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
-    if (ctx->g_exec) (void)hipGraphExecDestroy(ctx->g_exec);
-    if (ctx->g_graph) (void)hipGraphDestroy(ctx->g_graph);
+    ctx->clear_graphs();
     for (float *p : ctx->pcm_dev) if (p) (void)hipFree(p);
     if (ctx->d_mel) (void)hipFree(ctx->d_mel);
     if (ctx->dfeed) (void)hipFree(ctx->dfeed);
@@ -1612,11 +1664,14 @@ int wmi_decode_logits(wmi_context *ctx, int clip, const int32_t *tokens, int n_t
     HIPCHK(ctx, hipMemsetAsync(ctx->dsync, 0, ctx->sync_bytes, ctx->stream));
     const size_t V = ctx->hp.n_vocab;
     for (int i = 0; i < n_tokens; ++i) {
-        rc = run_dec_steps(ctx, clip, 1, n_tokens, n_tokens, 0, 1, 1);
+        rc = run_dec_steps(ctx, clip, 1, n_tokens, n_tokens, 0, 1, i, 1);
         if (rc) return rc;
         HIPCHK(ctx, hipMemcpyAsync(logits + (size_t)i * V, ctx->dlogits, V * 4, hipMemcpyDeviceToHost, ctx->stream));
     }
+    uint32_t err = 0;
+    HIPCHK(ctx, hipMemcpyAsync(&err, ctx->derr, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (err) return dec_err(ctx, err);
     return WMI_OK;
 }
 

@@ -139,6 +139,7 @@ struct DecAttnArgs {
     const uint16_t *K, *V;   // per clip: rows of n (clip_stride elements apart)
     int64_t clip_stride;     // elements between clips in K/V
     int M_fixed;             // >0: fixed key count (cross); 0: pos + 1 (self)
+    int mk;                  // self-attention: key capacity of this launch (64/128/256/512 >= pos + 1)
     const DecState *st;
     float *S;                // scores [B][H][s_stride]
     int s_stride;
@@ -163,6 +164,15 @@ struct DecAttnArgs {
     const int32_t *kv_src;
     int kv_src_stride;
     int clip_div;
+    // self-attention with the output projection fused (Wo null: o_h -> opart):
+    // head h writes Wo[:, h*64:(h+1)*64] . f16(o_h) to wo_parts[b][h][n]
+    const uint16_t *Wo;
+    float *wo_parts;
+    // cross-attention prologue (res_parts non-null): x_out = (res_bias +
+    // sum_h res_parts[b][h]) + x, the fused self-attention's residual update,
+    // then LN(x_out); block (0, 0, b) stores x_out[b] (x_out != x: ping-pong)
+    const float *res_parts, *res_bias;
+    float *x_out;
     unsigned long long *trace;  // WMI_TRACE slot (see DecGemvArgs)
     unsigned long long *phase;  // WMI_TRACE: [2][8] phase times of the first and last chunk of (head 0, clip 0)
 };

@@ -828,6 +828,27 @@ __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K
 
 // NC = 128-element K chunks a lane prefetches per row (8 for K <= 1024, 16 for
 // the MLP-down GEMV at K = 4n <= 2048); longer rows loop.
+// decoder weight stream loads: WMI_NT builds use the non-temporal policy
+// (weights each CU reads once per step; MI355X_MICROARCH.md nt-weights)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ T wload(const T *p) {
+#ifdef WMI_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ uint4 wload(const uint4 *p) {
+    const u32x4 v = wload((const u32x4 *)p);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ uint2 wload(const uint2 *p) {
+    const u32x2 v = wload((const u32x2 *)p);
+    return make_uint2(v[0], v[1]);
+}
+
 // q5_1 weights (repacked at load: per row K/2 bytes of nibbles in natural
 // order, then per 32-block a u32 of 5th bits and a u32 {f16 d, f16 m}):
 // eight weights starting at block offset sh, dequantised exactly as the host
@@ -892,14 +913,14 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
                 if constexpr (WQ) {
                     if (row < N && k < K) {
                         const int64_t e = (int64_t)row * K + k;
-                        S.wqn[g][c] = *(const uint4 *)(q5n + e / 2);
-                        S.wqd[g][c] = q5hd[e / 32];
+                        S.wqn[g][c] = wload((const uint4 *)(q5n + e / 2));
+                        S.wqd[g][c] = wload(q5hd + e / 32);
                     } else {
                         S.wqn[g][c] = make_uint4(0u, 0u, 0u, 0u);
                         S.wqd[g][c] = make_uint2(0u, 0u);
                     }
                 } else {
-                    if (row < N && k < K) S.wv[g][c] = *(const half8 *)(W + (int64_t)row * K + k);
+                    if (row < N && k < K) S.wv[g][c] = wload((const half8 *)(W + (int64_t)row * K + k));
                     else
 #pragma unroll
                         for (int e = 0; e < 8; ++e) S.wv[g][c][e] = (f16)0.0f;
@@ -1353,7 +1374,37 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
         for (int kc = 0; kc < KC; ++kc) wq[i][kc] = *(const half8 *)(wr + kc * 128);
         bqr[i] = a.bq[r];
     }
-    if (w == 0) {
+    if (a.res_parts) {
+        // the fused self-attention's residual update: x + (bo + sum over the
+        // H = 2 KC heads of its output-projection partials), in head order;
+        // block (0, 0, b) stores it for the rest of the layer (ping-pong buffer)
+        __shared__ __attribute__((aligned(16))) float xnew[KC * 128];
+        constexpr int H2 = 2 * KC;
+        for (int j = tid; j < n / 4; j += 256) {
+            const float *pp = a.res_parts + (int64_t)b * H2 * n + 4 * j;
+            float4 t[H2];
+#pragma unroll
+            for (int hh = 0; hh < H2; ++hh) t[hh] = *(const float4 *)(pp + (int64_t)hh * n);
+            const float4 bo = *(const float4 *)(a.res_bias + 4 * j);
+            const float4 x0 = *(const float4 *)(a.x + (int64_t)b * n + 4 * j);
+            float4 sm = t[0];
+#pragma unroll
+            for (int hh = 1; hh < H2; ++hh) {
+                sm.x = sm.x + t[hh].x; sm.y = sm.y + t[hh].y; sm.z = sm.z + t[hh].z; sm.w = sm.w + t[hh].w;
+            }
+            float4 v;
+            v.x = (bo.x + sm.x) + x0.x; v.y = (bo.y + sm.y) + x0.y;
+            v.z = (bo.z + sm.z) + x0.z; v.w = (bo.w + sm.w) + x0.w;
+            *(float4 *)(xnew + 4 * j) = v;
+            if (c == 0 && h == 0) *(float4 *)(a.x_out + (int64_t)b * n + 4 * j) = v;
+        }
+        __syncthreads();
+        if (w == 0) {
+            float4 xv[DG_LNV];
+            ln_load_row(xnew, n, lane, xv);
+            ln_regs_to_lds(xv, n, a.ln_w, a.ln_b, xs, lane);
+        }
+    } else if (w == 0) {
         float4 xv[DG_LNV];
         ln_load_row(a.x + (int64_t)b * n, n, lane, xv);
         ln_regs_to_lds(xv, n, a.ln_w, a.ln_b, xs, lane);
@@ -1419,7 +1470,9 @@ __global__ __launch_bounds__(256) void k_dec_attn_pv(DecAttnArgs a) {
 // self-attention over the KV cache (M = pos + 1 <= 512 keys): one workgroup
 // per (clip, head), every K and V load issued up front.  Output goes to
 // opart[b][0][n] (n_parts = 1 for the consumer).
+template <int MK>  // keys covered: M = pos + 1 <= MK (64, 128, 256 or 512)
 __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
+    constexpr int RK = MK > 256 ? 2 : 1, NVI = MK / 32;
     trace_begin(a.trace);
     const int h = blockIdx.x, b = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1427,7 +1480,8 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     const int n = a.n;
     __shared__ float redf[4];
     __shared__ double redd[4];
-    __shared__ __attribute__((aligned(16))) uint16_t P[512];
+    __shared__ __attribute__((aligned(16))) uint16_t P[MK];
+    if (M > MK && tid == 0 && a.err) atomicOr(a.err, 2u);  // host bucketing error: flagged, never silent
     __shared__ float ored[32][64];
     const f16 *qr = (const f16 *)a.q + (int64_t)b * n + h * 64;
     if (a.reset_amax && h == 0 && b == 0)
@@ -1437,46 +1491,57 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     // Scores: thread t owns keys t and t + 256; PV: thread owns d-octet
     // (tid & 7) and keys (tid >> 3) + 32 i.
     const int doct = tid & 7, jg = tid >> 3;
-    int jk[2], jv[16];
-    int64_t sk[2], sv[16];
+    int jk[RK], jv[NVI];
+    int64_t sk[RK], sv[NVI];
 #pragma unroll
-    for (int r = 0; r < 2; ++r) jk[r] = min(tid + 256 * r, M - 1);
+    for (int r = 0; r < RK; ++r) jk[r] = min(tid + 256 * r, M - 1);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) jv[i] = min(jg + 32 * i, M - 1);
+    for (int i = 0; i < NVI; ++i) jv[i] = min(jg + 32 * i, M - 1);
 #pragma unroll
-    for (int r = 0; r < 2; ++r) sk[r] = b;
+    for (int r = 0; r < RK; ++r) sk[r] = b;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) sv[i] = b;
+    for (int i = 0; i < NVI; ++i) sv[i] = b;
     if (a.kv_src) {  // every table load first, then every cache load
         const int32_t *src = a.kv_src + (int64_t)b * a.kv_src_stride;
-        int tk[2], tv[16];
+        int tk[RK], tv[NVI];
 #pragma unroll
-        for (int r = 0; r < 2; ++r) tk[r] = src[jk[r]];
+        for (int r = 0; r < RK; ++r) tk[r] = src[jk[r]];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) tv[i] = src[jv[i]];
+        for (int i = 0; i < NVI; ++i) tv[i] = src[jv[i]];
 #pragma unroll
-        for (int r = 0; r < 2; ++r) sk[r] = jk[r] < M - 1 ? tk[r] : b;
+        for (int r = 0; r < RK; ++r) sk[r] = jk[r] < M - 1 ? tk[r] : b;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sv[i] = jv[i] < M - 1 ? tv[i] : b;
+        for (int i = 0; i < NVI; ++i) sv[i] = jv[i] < M - 1 ? tv[i] : b;
     }
-    half8 kv[2][8];
+    half8 kv[RK][8];
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < RK; ++r) {
         const f16 *kr = (const f16 *)a.K + sk[r] * a.clip_stride + (int64_t)jk[r] * n + h * 64;
 #pragma unroll
         for (int i = 0; i < 8; ++i) kv[r][i] = *(const half8 *)(kr + 8 * i);
     }
-    half8 vv[16];
+    half8 vv[NVI];
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
+    for (int i = 0; i < NVI; ++i)
         vv[i] = *(const half8 *)((const f16 *)a.V + sv[i] * a.clip_stride + (int64_t)jv[i] * n + h * 64 + doct * 8);
     half8 qv[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) qv[i] = *(const half8 *)(qr + 8 * i);
-    float sc[2];
+    // fused output projection: this head's 64 Wo columns for output rows
+    // tid + 256 r (the first two prefetched now, independent of the attention)
+    constexpr int WOR = 2;
+    half8 wov[WOR][8];
+    if (a.Wo)
+#pragma unroll
+        for (int r = 0; r < WOR; ++r) {
+            const int orow = min(tid + 256 * r, n - 1);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wov[r][i] = wload((const half8 *)(a.Wo + (int64_t)orow * n + h * 64 + 8 * i));
+        }
+    float sc[RK];
     float mx = -INFINITY;
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < RK; ++r) {
         float s = 0.0f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) s = dot8(kv[r][i], qv[i], s);
@@ -1488,9 +1553,9 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     __syncthreads();
     mx = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
     double sum = 0.0;
-    float p[2];
+    float p[RK];
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < RK; ++r) {
         p[r] = 0.0f;
         if (tid + 256 * r < M) {
             p[r] = exp_f16_exact(sc[r] - mx);
@@ -1502,11 +1567,12 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     __syncthreads();
     const float inv = (float)(1.0 / (((redd[0] + redd[1]) + redd[2]) + redd[3]));
 #pragma unroll
-    for (int r = 0; r < 2; ++r) P[tid + 256 * r] = f2h_bits(tid + 256 * r < M ? p[r] * inv : 0.0f);
+    for (int r = 0; r < RK; ++r)
+        if (tid + 256 * r < MK) P[tid + 256 * r] = f2h_bits(tid + 256 * r < M ? p[r] * inv : 0.0f);
     __syncthreads();
     float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < NVI; ++i) {
         const float pj = h2f_bits(P[jg + 32 * i]);
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vv[i][e];
@@ -1514,10 +1580,41 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) ored[jg][doct * 8 + e] = o[e];
     __syncthreads();
+    if (!a.Wo) {
+        if (tid < 64) {
+            float v = ored[0][tid];
+            for (int g = 1; g < 32; ++g) v = v + ored[g][tid];
+            a.opart[(int64_t)b * n + h * 64 + tid] = v;
+        }
+        trace_end(a.trace);
+        return;
+    }
+    __shared__ __attribute__((aligned(16))) f16 oh[64];
     if (tid < 64) {
         float v = ored[0][tid];
         for (int g = 1; g < 32; ++g) v = v + ored[g][tid];
-        a.opart[(int64_t)b * n + h * 64 + tid] = v;
+        oh[tid] = (f16)v;  // the f16 input of the output projection
+    }
+    __syncthreads();
+    half8 ov[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ov[i] = *(const half8 *)(oh + 8 * i);
+    float *dst = a.wo_parts + ((int64_t)b * a.H + h) * n;
+    for (int r = 0; r * 256 < n; ++r) {
+        const int orow = tid + 256 * r;
+        half8 wr[8];
+        if (r < WOR) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wr[i] = r == 0 ? wov[0][i] : wov[1][i];
+        } else {
+            const int oc = min(orow, n - 1);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wr[i] = wload((const half8 *)(a.Wo + (int64_t)oc * n + h * 64 + 8 * i));
+        }
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc = dot8(wr[i], ov[i], acc);
+        if (orow < n) dst[orow] = acc;  // summed by the next kernel's prologue
     }
     trace_end(a.trace);
 }
@@ -1525,11 +1622,19 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
 
 hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
     if (a.M_fixed == 0) {  // self-attention: M = pos + 1 <= 512
-        if (a.n_chunks != 1) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_dec_self_attn, dim3(a.H, a.B), dim3(256), 0, s, a);
+        if (a.n_chunks != 1 || (a.Wo && !a.wo_parts)) return hipErrorInvalidValue;
+        switch (a.mk) {
+            case 64: hipLaunchKernelGGL(k_dec_self_attn<64>, dim3(a.H, a.B), dim3(256), 0, s, a); break;
+            case 128: hipLaunchKernelGGL(k_dec_self_attn<128>, dim3(a.H, a.B), dim3(256), 0, s, a); break;
+            case 256: hipLaunchKernelGGL(k_dec_self_attn<256>, dim3(a.H, a.B), dim3(256), 0, s, a); break;
+            case 512: hipLaunchKernelGGL(k_dec_self_attn<512>, dim3(a.H, a.B), dim3(256), 0, s, a); break;
+            default: return hipErrorInvalidValue;
+        }
         return hipGetLastError();
     }
-    if (a.M_fixed > 2048 || a.n_chunks > 16 || a.n_chunks * DA_CK < a.M_fixed || a.n % 128) return hipErrorInvalidValue;
+    if (a.M_fixed > 2048 || a.n_chunks > 16 || a.n_chunks * DA_CK < a.M_fixed || a.n % 128 ||
+        (a.res_parts && (a.H * 64 != a.n || !a.res_bias || !a.x_out || a.x_out == a.x)))
+        return hipErrorInvalidValue;
     dim3 grid(a.n_chunks, a.H, a.B);
     // cooperative single kernel while the grid stays far inside residency
     // (<= 2 workgroups per CU) and the Wq rows fit the register budget;

@@ -21,7 +21,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libwhisper_mi355x.so")
+LIB_PATH = os.environ.get("WMI_LIB") or os.path.join(HERE, "libwhisper_mi355x.so")
 
 WMI_OK = 0
 
