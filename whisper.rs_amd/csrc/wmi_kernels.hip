@@ -783,17 +783,20 @@ __device__ __forceinline__ void ln_load_row(const float *x, int K, int lane, flo
     }
 }
 
-// LayerNorm of one K-row held as float4 registers (ggml norm semantics)
-__device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K, const float *lw, const float *lb,
-                                               f16 *dst, int lane) {
-    // gain/bias requested before the two reductions so their latency hides
-    float4 gw[DG_LNV], gb[DG_LNV];
+// LayerNorm gain / bias as float4 registers
+__device__ __forceinline__ void ln_load_params(const float *lw, const float *lb, int K, int lane, float4 (&gw)[DG_LNV],
+                                               float4 (&gb)[DG_LNV]) {
 #pragma unroll
     for (int i = 0; i < DG_LNV; ++i) {
         const int e = (lane + 64 * i) * 4, ec = e < K ? e : 0;
         gw[i] = keep4(*(const float4 *)(lw + ec), e < K);
         gb[i] = keep4(*(const float4 *)(lb + ec), e < K);
     }
+}
+
+// LayerNorm of one K-row held as float4 registers (ggml norm semantics)
+__device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K, const float4 (&gw)[DG_LNV],
+                                               const float4 (&gb)[DG_LNV], f16 *dst, int lane) {
     double s1 = 0.0;
 #pragma unroll
     for (int i = 0; i < DG_LNV; ++i)
@@ -823,6 +826,14 @@ __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K
             }
         }
     }
+}
+
+// the same with the gain / bias requested here (before the two reductions)
+__device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K, const float *lw, const float *lb,
+                                               f16 *dst, int lane) {
+    float4 gw[DG_LNV], gb[DG_LNV];
+    ln_load_params(lw, lb, K, lane, gw, gb);
+    ln_regs_to_lds(xv, K, gw, gb, dst, lane);
 }
 
 
@@ -1025,6 +1036,13 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
 #pragma unroll
             for (int bb = 0; bb < DG_MAXB; ++bb) acc[g][bb] = 0.0f;
     };
+    // LayerNorm operands of row w first: the LN below then waits for them
+    // while the weight stream issued after them is still in flight
+    float4 xv0[DG_LNV], gw0[DG_LNV], gb0[DG_LNV];
+    if (IN == 0 && w < B) {
+        ln_load_row(a.x + (int64_t)w * K, K, lane, xv0);
+        ln_load_params(a.ln_w, a.ln_b, K, lane, gw0, gb0);
+    }
     // every weight / epilogue request of the first group(s) before the prologue
     WSet S0, S1;
     int rgA = blockIdx.x, rgB = rgA + gridDim.x;
@@ -1042,6 +1060,10 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
             const int rb = w + 4 * rr;
             if (rb < B) {
                 float4 xv[DG_LNV];
+                if (IN == 0 && rr == 0) {
+                    ln_regs_to_lds(xv0, K, gw0, gb0, xs + rb * K, lane);
+                    continue;
+                }
                 if (IN == 0) {
                     ln_load_row(a.x + (int64_t)rb * K, K, lane, xv);
                 } else {
@@ -1353,7 +1375,24 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
     __shared__ __attribute__((aligned(16))) f16 xs[KC * 128];
     __shared__ __attribute__((aligned(16))) f16 qh[64];
     __shared__ float red[4];
-    // ---- every independent load first (all unconditional) ----
+    // ---- every independent load first (all unconditional); the LayerNorm
+    // operands (and the fused self-attention's partials) lead, so the LN
+    // waits for them while the K / V / Wq requests are still in flight ----
+    constexpr int H2 = 2 * KC;  // heads: n / 64
+    float4 rp[H2], rbo, rx;
+    const bool rpart = a.res_parts != nullptr && tid < n / 4;
+    if (rpart) {
+        const float *pp = a.res_parts + (int64_t)b * H2 * n + 4 * tid;
+#pragma unroll
+        for (int hh = 0; hh < H2; ++hh) rp[hh] = *(const float4 *)(pp + (int64_t)hh * n);
+        rbo = *(const float4 *)(a.res_bias + 4 * tid);
+        rx = *(const float4 *)(a.x + (int64_t)b * n + 4 * tid);
+    }
+    float4 xv[DG_LNV], gw[DG_LNV], gb[DG_LNV];
+    if (w == 0) {
+        ln_load_params(a.ln_w, a.ln_b, n, lane, gw, gb);
+        if (!a.res_parts) ln_load_row(a.x + (int64_t)b * n, n, lane, xv);
+    }
     const int key = c * DA_CK + (tid >> 1), half = tid & 1;
     half8 kf[4];
     {
@@ -1376,38 +1415,35 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
     }
     if (a.res_parts) {
         // the fused self-attention's residual update: x + (bo + sum over the
-        // H = 2 KC heads of its output-projection partials), in head order;
-        // block (0, 0, b) stores it for the rest of the layer (ping-pong buffer)
+        // H heads of its output-projection partials), in head order; block
+        // (0, 0, b) stores it for the rest of the layer (ping-pong buffer)
         __shared__ __attribute__((aligned(16))) float xnew[KC * 128];
-        constexpr int H2 = 2 * KC;
         for (int j = tid; j < n / 4; j += 256) {
-            const float *pp = a.res_parts + (int64_t)b * H2 * n + 4 * j;
-            float4 t[H2];
+            if (j != tid) {  // second pass (n > 1024): operands not prefetched
+                const float *pp = a.res_parts + (int64_t)b * H2 * n + 4 * j;
 #pragma unroll
-            for (int hh = 0; hh < H2; ++hh) t[hh] = *(const float4 *)(pp + (int64_t)hh * n);
-            const float4 bo = *(const float4 *)(a.res_bias + 4 * j);
-            const float4 x0 = *(const float4 *)(a.x + (int64_t)b * n + 4 * j);
-            float4 sm = t[0];
+                for (int hh = 0; hh < H2; ++hh) rp[hh] = *(const float4 *)(pp + (int64_t)hh * n);
+                rbo = *(const float4 *)(a.res_bias + 4 * j);
+                rx = *(const float4 *)(a.x + (int64_t)b * n + 4 * j);
+            }
+            float4 sm = rp[0];
 #pragma unroll
             for (int hh = 1; hh < H2; ++hh) {
-                sm.x = sm.x + t[hh].x; sm.y = sm.y + t[hh].y; sm.z = sm.z + t[hh].z; sm.w = sm.w + t[hh].w;
+                sm.x = sm.x + rp[hh].x; sm.y = sm.y + rp[hh].y; sm.z = sm.z + rp[hh].z; sm.w = sm.w + rp[hh].w;
             }
             float4 v;
-            v.x = (bo.x + sm.x) + x0.x; v.y = (bo.y + sm.y) + x0.y;
-            v.z = (bo.z + sm.z) + x0.z; v.w = (bo.w + sm.w) + x0.w;
+            v.x = (rbo.x + sm.x) + rx.x; v.y = (rbo.y + sm.y) + rx.y;
+            v.z = (rbo.z + sm.z) + rx.z; v.w = (rbo.w + sm.w) + rx.w;
             *(float4 *)(xnew + 4 * j) = v;
             if (c == 0 && h == 0) *(float4 *)(a.x_out + (int64_t)b * n + 4 * j) = v;
         }
         __syncthreads();
         if (w == 0) {
-            float4 xv[DG_LNV];
             ln_load_row(xnew, n, lane, xv);
-            ln_regs_to_lds(xv, n, a.ln_w, a.ln_b, xs, lane);
+            ln_regs_to_lds(xv, n, gw, gb, xs, lane);
         }
     } else if (w == 0) {
-        float4 xv[DG_LNV];
-        ln_load_row(a.x + (int64_t)b * n, n, lane, xv);
-        ln_regs_to_lds(xv, n, a.ln_w, a.ln_b, xs, lane);
+        ln_regs_to_lds(xv, n, gw, gb, xs, lane);
     }
     __syncthreads();
     trace_phase(a.phase, 1);
