@@ -33,6 +33,10 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense FP16
 KERNELS = {0: ("hbm", "dec_logits"), 1: ("mfma", "enc_mlp0"), 2: ("mfma", "enc_attn"), 3: ("mfma", "cross_kv"),
            4: ("hbm", "probe_empty"), 5: ("hbm", "probe_copy_1MiB")}
+# roofline.traffic: per-launch HBM bytes of the roofline kernel measured with
+# rocprofv3 PMC counters (scripts/pmc_pass.sh + scripts/pmc_summary.py; the
+# profiler cannot run inside this process), keyed by (model, kernel id)
+PMC_TRAFFIC = {("base", 0): "profiles/r01_pmc_logits_base.json"}
 
 
 def log(msg):
@@ -141,9 +145,10 @@ def main():
         wtype = "q5_1" if args.model.endswith("q5_1") else "f16"
         ms_step = elapsed / args.steps * 1e3
         value = world * audio_s * args.steps / elapsed
-        kernels = {}
+        kernels, kb_alg_bytes = {}, {}
         for k, (bound, name) in KERNELS.items():
             kb = ctx.bench_kernel(k, 50)
+            kb_alg_bytes[name] = kb["alg_bytes"]
             secs = kb["avg_us"] * 1e-6
             kernels[name] = {"kernel": kb["name"], "avg_us": round(kb["avg_us"], 3),
                              "GB/s": round(kb["alg_bytes"] / secs / 1e9, 1),
@@ -156,6 +161,13 @@ def main():
             roof = {"bound": "mfma", "achieved": kd["TFLOP/s"], "peak": MFMA_F16_PEAK_TFS, "unit": "TFLOP/s"}
         roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
         roof["traffic"] = None
+        pmc = PMC_TRAFFIC.get((args.model, args.roofline_kernel))
+        if pmc and os.path.exists(os.path.join(ROOT, pmc)):
+            with open(os.path.join(ROOT, pmc)) as fh:
+                pm = json.load(fh)
+            roof["traffic"] = pm["traffic_bytes"]  # HBM bytes per launch, rocprofv3 PMC (corrected)
+            roof["traffic_source"] = pmc
+            roof["alg_bytes"] = kb_alg_bytes[name]
         roof["kernel"] = kd["kernel"]
         roof["avg_us"] = kd["avg_us"]
         result = {

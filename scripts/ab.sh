@@ -1,8 +1,13 @@
 #!/bin/bash
-# A/B timing of decoder variants on the gpurun box: bench.py base, 3 steps
+# A/B timing of decoder variants on the gpurun box: bench.py (base unless
+# MODEL is set), 3 steps each; each line "<env> value decode_ms logits_us".
+# Usage: bash scripts/ab.sh "ENV=1 ENV2=0" "ENV=0" ...
 set -o pipefail
 mkdir -p gpurun_out
-run() { timeout -k 10 200 env "$@" python bench.py --steps 3 --warmup 1 --no-cpu-baseline 2>/dev/null | python -c "
-import json,sys; d=json.load(sys.stdin); print('$*', d['value'], d['stage_ms']['decode_ms'], d['roofline']['avg_us'])"; }
-run WMI_X=0 && run WMI_NO_FUSE=1 && run WMI_LIB=$PWD/whisper.rs_amd/libwhisper_mi355x_nt.so && \
-run WMI_LIB=$PWD/whisper.rs_amd/libwhisper_mi355x_nt.so WMI_NO_FUSE=1
+export WMI_MODEL_CACHE=/tmp/wmi_models
+MODEL=${MODEL:-base}
+for v in "$@"; do
+  timeout -k 10 200 env $v python bench.py --model $MODEL --steps 3 --warmup 1 --no-cpu-baseline 2>/dev/null | python -c "
+import json,sys; d=json.load(sys.stdin); print('$v', d['value'], d['stage_ms']['decode_ms'], d['encoder_ms'], d['roofline']['avg_us'])" || exit 1
+done
+echo "AB EXIT 0"

@@ -263,6 +263,7 @@ struct wmi_context {
     bool trace_on = false;
     unsigned long long *d_trace = nullptr;
     std::vector<std::string> trace_names;
+    std::vector<std::string> phase_names = std::vector<std::string>(32);  // phase slots 32.. (layer 0 GEMVs, logits)
     // dist
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
@@ -1055,6 +1056,13 @@ int run_encode(wmi_context *ctx, int mel_offset) {
 
 constexpr int TRACE_SLOTS = 512;
 
+// phase slot (first / last workgroup timeline inside one launch) for WMI_TRACE
+unsigned long long *pslot(wmi_context *ctx, int i, const char *name) {
+    if (!ctx->trace_on || i < 0 || i >= 32) return nullptr;
+    ctx->phase_names[i] = name;
+    return ctx->d_trace + 2 * 512 + 16 * (32 + i);
+}
+
 unsigned long long *tslot(wmi_context *ctx, const char *name, int l) {
     if (!ctx->trace_on || ctx->trace_names.size() >= (size_t)TRACE_SLOTS) return nullptr;
     char buf[64];
@@ -1069,11 +1077,19 @@ int trace_dump(wmi_context *ctx) {
     std::vector<unsigned long long> t(2 * TRACE_SLOTS + 64 * 16);
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     HIPCHK(ctx, hipMemcpy(t.data(), ctx->d_trace, t.size() * 8, hipMemcpyDeviceToHost));
-    for (int l = 0; l < ctx->hp.n_text_layer && ctx->use_coop; ++l) {
-        const unsigned long long *ph = t.data() + 2 * TRACE_SLOTS + 16 * l;
+    for (int sl = 0; sl < 64; ++sl) {
+        const unsigned long long *ph = t.data() + 2 * TRACE_SLOTS + 16 * sl;
+        std::string nm;
+        if (sl < ctx->hp.n_text_layer && ctx->use_coop) nm = "cross_attn[" + std::to_string(sl) + "]";
+        else if (sl >= 32 && !ctx->phase_names[sl - 32].empty() && ph[0]) nm = ctx->phase_names[sl - 32];
+        if (nm.empty()) continue;
         for (int wg = 0; wg < 2; ++wg) {
-            fprintf(stderr, "[wmi trace] cross_attn[%d] %s chunk phases:", l, wg ? "last " : "first");
-            for (int i = 1; i < 8; ++i) fprintf(stderr, " %7.2f", ((double)ph[8 * wg + i] - (double)ph[0]) * 0.01);
+            fprintf(stderr, "[wmi trace] %-14s %s WG phases:", nm.c_str(), wg ? "last " : "first");
+            for (int i = 1; i < 8; ++i) {
+                const unsigned long long v = ph[8 * wg + i];
+                if (v) fprintf(stderr, " %7.2f", ((double)v - (double)ph[0]) * 0.01);
+                else fprintf(stderr, "       -");
+            }
             fprintf(stderr, "\n");
         }
     }
@@ -1129,6 +1145,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
             }
         }
         g.trace = tslot(ctx, "qkv", l);
+        if (l == 0) g.phase = pslot(ctx, 0, "qkv[0]");
         HIPCHK(ctx, launch_dec_gemv(s, DEC_QKV, g));
         DecAttnArgs at{};
         at.q = ctx->dq16; at.K = kc; at.V = vc; at.clip_stride = (int64_t)hp.n_text_ctx * n; at.M_fixed = 0;
@@ -1147,6 +1164,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
             at.wo_parts = ctx->dwoparts;
         }
         at.trace = tslot(ctx, "self_attn", l);
+        if (l == 0) at.phase = pslot(ctx, 1, "self_attn[0]");
         HIPCHK(ctx, launch_dec_attn(s, at));
         if (!ctx->fuse_wo) {
             g = DecGemvArgs{};
@@ -1179,17 +1197,20 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         g.Wq5 = q5 ? d.wco5 : nullptr;
         g.out32 = X[cur];
         g.trace = tslot(ctx, "wco", l);
+        if (l == 0) g.phase = pslot(ctx, 2, "wco[0]");
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
         g = DecGemvArgs{};
         g.x = X[cur]; g.ln_w = d.ln2_w; g.ln_b = d.ln2_b; g.W = d.w0; g.bias = d.b0; g.N = 4 * n; g.K = n; g.B = B;
         g.Wq5 = q5 ? d.w05 : nullptr;
         g.out16 = ctx->dhid16; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
         g.trace = tslot(ctx, "mlp0", l);
+        if (l == 0) g.phase = pslot(ctx, 3, "mlp0[0]");
         HIPCHK(ctx, launch_dec_gemv(s, DEC_GELU, g));
         g = DecGemvArgs{};
         g.xin16 = ctx->dhid16; g.W = d.w1; g.bias = d.b1; g.N = n; g.K = 4 * n; g.B = B; g.out32 = X[cur];
         g.Wq5 = q5 ? d.w15 : nullptr;
         g.trace = tslot(ctx, "mlp1", l);
+        if (l == 0) g.phase = pslot(ctx, 4, "mlp1[0]");
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
     }
     DecGemvArgs g{};
@@ -1198,6 +1219,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     g.out32 = ctx->dlogits; g.amax = ctx->damax; g.suppress_id = suppress_eot ? ctx->sp.eot : -1;
     g.st_advance = ctx->dstate;
     g.trace = tslot(ctx, "logits", 0);
+    g.phase = pslot(ctx, 5, "logits");
     if (beam) g.amax = nullptr;
     HIPCHK(ctx, launch_dec_gemv(s, DEC_LOGITS, g));
     if (beam) {
@@ -1537,9 +1559,12 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (getenv("WMI_NO_Q5")) ctx->use_q5 = false;
     if (getenv("WMI_NO_FUSE")) ctx->fuse_wo = false;
     if (const char *c = getenv("WMI_LOGITS_CAP")) g_logits_cap = atoi(c) > 0 ? atoi(c) : g_logits_cap;
+    if (const char *c = getenv("WMI_GEMV_NW")) g_gemv_nw = atoi(c) == 1 ? 1 : atoi(c) == 0 ? 0 : 4;
+    if (const char *c = getenv("WMI_SELF_SPLIT")) g_self_split = atoi(c) >= 0 ? atoi(c) : g_self_split;
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_trace, TRACE_SLOTS * 16 + 64 * 16 * 8));
+        HIPCHK(ctx.get(), hipMemset(ctx->d_trace, 0, TRACE_SLOTS * 16 + 64 * 16 * 8));
     }
     *out = ctx.release();
     return WMI_OK;

@@ -128,11 +128,14 @@ struct DecGemvArgs {
     float *x_out;               // residual stream written by block 0
     const int32_t *beam_tok;    // beam search: token of row b past the prompt (BeamState::tok), else null
     unsigned long long *trace;  // WMI_TRACE: {min start, ~max end} s_memrealtime of this launch
+    unsigned long long *phase;  // WMI_TRACE: [2][8] phase times of the first and last workgroup
 };
 constexpr int AMAX_SHARDS = 64;
 constexpr int DEC_ROWS = 8;  // decoder rows per step: clips (greedy) or beam hypotheses
 hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a);
 extern int g_logits_cap;
+extern int g_gemv_nw;
+extern int g_self_split;
 
 struct DecAttnArgs {
     const uint16_t *q;       // [B][n]

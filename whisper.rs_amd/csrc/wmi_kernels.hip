@@ -885,9 +885,14 @@ __device__ __forceinline__ half8 q5_half8(uint32_t qn, uint32_t qh, uint32_t dm,
     return w;
 }
 
-template <int EPI, int IN, int G, int NC, int WQ>
-__global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
+// NW = waves per workgroup: 4 (16 rows per workgroup) for the vocabulary GEMV
+// and batched rows; 1 (4 rows) for the small per-layer GEMVs at B <= 2, so
+// their 0.5-2 MiB weight streams spread over 4x the CUs (per-CU bytes, not
+// chip bandwidth, bound a 2 MiB GEMV spread over 32-128 workgroups)
+template <int EPI, int IN, int G, int NC, int WQ, int NW>
+__global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
     trace_begin(a.trace);
+    trace_phase(a.phase, 0);
     // chunk geometry: a quarter-wave covers CW consecutive weights of its row
     // per chunk, a lane LW of them (f16: 8 = one 16-byte load; q5_1: 32 = one
     // block, its 16 nibble bytes + an 8-byte {5th bits, d/m} word)
@@ -903,8 +908,8 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int q = lane >> 4, l16 = lane & 15;
     const int K = a.K, B = a.B, N = a.N;
-    const int nrg = (N + 16 * G - 1) / (16 * G);
-    auto rbase = [&](int rg) { return (rg * 4 + w) * 4 * G; };
+    const int nrg = (N + 4 * NW * G - 1) / (4 * NW * G);
+    auto rbase = [&](int rg) { return (rg * NW + w) * 4 * G; };
     const f16 *W = (const f16 *)a.W;
     const uint8_t *q5n = a.Wq5;
     const uint2 *q5hd = (const uint2 *)(a.Wq5 + (int64_t)N * K / 2);
@@ -1052,12 +1057,13 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
         load_set(S1, rbase(rgB), 0);
         load_epi(S1, rbase(rgB));
     }
+    trace_phase(a.phase, 1);
     if (IN == 0 || IN == 3) {
-        // each wave normalises rows w and w + 4
+        // each wave normalises rows w, w + NW, ...
         const int pos = (IN == 3) ? a.st->pos : 0;
 #pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            const int rb = w + 4 * rr;
+        for (int rr = 0; rr < DG_MAXB / NW; ++rr) {
+            const int rb = w + NW * rr;
             if (rb < B) {
                 float4 xv[DG_LNV];
                 if (IN == 0 && rr == 0) {
@@ -1098,11 +1104,11 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
     } else if (IN == 1) {
         const uint4 *src = (const uint4 *)a.xin16;
         uint4 *dst = (uint4 *)xs;
-        for (int i = tid; i < B * K / 8; i += 256) dst[i] = src[i];
+        for (int i = tid; i < B * K / 8; i += 64 * NW) dst[i] = src[i];
     } else {
         // partial sums: thread owns 4 consecutive inputs; all chunk loads issued first
         constexpr int CMAXP = 16;
-        for (int i4 = tid; i4 < B * K / 4; i4 += 256) {
+        for (int i4 = tid; i4 < B * K / 4; i4 += 64 * NW) {
             const int bb = (i4 * 4) / K, k = i4 * 4 - bb * K;
             const float *p = a.parts + ((int64_t)bb * a.n_parts) * K + k;
             float4 v[CMAXP];
@@ -1123,6 +1129,7 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
     }
     if (EPI == DEC_LOGITS && tid < DG_MAXB) amax_s[tid] = 0ull;
     __syncthreads();
+    trace_phase(a.phase, 2);
     float acc[G][DG_MAXB];
     if constexpr (PIPE) {  // K <= DG_KB (checked by the launcher)
         for (;;) {
@@ -1149,43 +1156,63 @@ __global__ __launch_bounds__(256) void k_dec_gemv(DecGemvArgs a) {
             if (k0 > 0) load_set(S0, rbase(rgA), k0);
             dot_set(S0, k0, acc);
         }
+        trace_phase(a.phase, 3);
         finish(rbase(rgA), acc, S0);
+        trace_phase(a.phase, 4);
     }
     if (EPI == DEC_LOGITS) {
         __syncthreads();
         if (a.amax && tid < B && amax_s[tid]) atomicMax(&a.amax[tid * AMAX_SHARDS + (blockIdx.x & (AMAX_SHARDS - 1))], amax_s[tid]);
         if (blockIdx.x == 0 && tid == 0) a.st_advance->pos += 1;
     }
+    trace_phase(a.phase, 7);
     trace_end(a.trace);
 }
 
 int g_logits_cap = 512;  // persistent logits grid (WMI_LOGITS_CAP overrides; 2 workgroups per CU at ~210 VGPRs)
+// waves per workgroup of the per-layer GEMVs (WMI_GEMV_NW=1 / 0 = one wave /
+// one wave at B <= 2): 4 measured fastest at base, B = 1 (one wave per
+// workgroup: mlp0 4.6 -> 10 us, every workgroup repeating the LayerNorm)
+int g_gemv_nw = 4;
+int g_self_split = 1;    // self-attention output projection over n / 128 workgroups per head (WMI_SELF_SPLIT=0: one)
 
-template <int EPI, int IN, int WQ>
-static hipError_t dec_gemv_g(hipStream_t s, const DecGemvArgs &a) {
+template <int EPI, int IN, int WQ, int NW>
+static hipError_t dec_gemv_nw(hipStream_t s, const DecGemvArgs &a) {
     const size_t lds = (size_t)a.B * a.K * 2;
-    dim3 block(256);
+    dim3 block(64 * NW);
     // the vocabulary GEMV runs persistent and pipelined (its K = n_state <=
     // 1280 fits one sweep of either chunk size); the others one group per WG
     const int cap = EPI == DEC_LOGITS ? g_logits_cap : 1 << 30;
-    const int nrg = cdiv(a.N, 16);
+    const int nrg = cdiv(a.N, 4 * NW);
     const dim3 grid(nrg < cap ? nrg : cap);
     if constexpr (WQ == 1) {  // q5_1: 4 chunks of 512 weights (K <= 2048 per sweep)
         if (EPI == DEC_LOGITS && a.K > 2048) return hipErrorInvalidValue;
-        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 4, 1>, lds);
+        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 4, 1, NW>, lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 4, 1>), grid, block, lds, s, a);
+        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 4, 1, NW>), grid, block, lds, s, a);
     } else if (a.K > 1024) {
         if (EPI == DEC_LOGITS && a.K > 2048) return hipErrorInvalidValue;
-        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 16, 0>, lds);
+        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 16, 0, NW>, lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 16, 0>), grid, block, lds, s, a);
+        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 16, 0, NW>), grid, block, lds, s, a);
     } else {
-        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 8, 0>, lds);
+        hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 8, 0, NW>, lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 8, 0>), grid, block, lds, s, a);
+        hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 8, 0, NW>), grid, block, lds, s, a);
     }
     return hipGetLastError();
+}
+
+template <int EPI, int IN, int WQ>
+static hipError_t dec_gemv_g(hipStream_t s, const DecGemvArgs &a) {
+    // one wave per workgroup spreads a per-layer GEMV over 4x the CUs; with
+    // more rows each wave would normalise B / NW LayerNorm rows serially
+    if constexpr (EPI == DEC_LOGITS) {
+        return dec_gemv_nw<EPI, IN, WQ, 4>(s, a);
+    } else {
+        const bool one = g_gemv_nw == 1 || (g_gemv_nw == 0 && a.B <= 2);
+        return one ? dec_gemv_nw<EPI, IN, WQ, 1>(s, a) : dec_gemv_nw<EPI, IN, WQ, 4>(s, a);
+    }
 }
 
 template <int EPI, int IN>
@@ -1510,6 +1537,7 @@ template <int MK>  // keys covered: M = pos + 1 <= MK (64, 128, 256 or 512)
 __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     constexpr int RK = MK > 256 ? 2 : 1, NVI = MK / 32;
     trace_begin(a.trace);
+    trace_phase(a.phase, 0);
     const int h = blockIdx.x, b = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int M = a.st->pos + 1;
@@ -1520,7 +1548,7 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     if (M > MK && tid == 0 && a.err) atomicOr(a.err, 2u);  // host bucketing error: flagged, never silent
     __shared__ float ored[32][64];
     const f16 *qr = (const f16 *)a.q + (int64_t)b * n + h * 64;
-    if (a.reset_amax && h == 0 && b == 0)
+    if (a.reset_amax && h == 0 && b == 0 && blockIdx.z == 0)
         for (int i = tid; i < a.B * AMAX_SHARDS; i += 256) a.reset_amax[i] = 0ull;
     // cache row of key j: slot b, or (beam search) the slot holding the
     // hypothesis' history; keys past M load row M - 1 (finite, masked below).
@@ -1565,15 +1593,26 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     for (int i = 0; i < 8; ++i) qv[i] = *(const half8 *)(qr + 8 * i);
     // fused output projection: this head's 64 Wo columns for output rows
     // tid + 256 r (the first two prefetched now, independent of the attention)
+    // Split form (gridDim.z = n / 128 > 1): workgroup z owns output rows
+    // [128 z, 128 z + 128), two threads per row (32 columns each); the
+    // attention itself is recomputed by each of the head's workgroups
     constexpr int WOR = 2;
+    const bool wsplit = gridDim.z > 1;
     half8 wov[WOR][8];
-    if (a.Wo)
+    if (a.Wo && wsplit) {
+        const int orow = blockIdx.z * 128 + (tid >> 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            wov[0][i] = wload((const half8 *)(a.Wo + (int64_t)orow * n + h * 64 + 32 * (tid & 1) + 8 * i));
+    } else if (a.Wo) {
 #pragma unroll
         for (int r = 0; r < WOR; ++r) {
             const int orow = min(tid + 256 * r, n - 1);
 #pragma unroll
             for (int i = 0; i < 8; ++i) wov[r][i] = wload((const half8 *)(a.Wo + (int64_t)orow * n + h * 64 + 8 * i));
         }
+    }
+    trace_phase(a.phase, 1);
     float sc[RK];
     float mx = -INFINITY;
 #pragma unroll
@@ -1606,6 +1645,7 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     for (int r = 0; r < RK; ++r)
         if (tid + 256 * r < MK) P[tid + 256 * r] = f2h_bits(tid + 256 * r < M ? p[r] * inv : 0.0f);
     __syncthreads();
+    trace_phase(a.phase, 2);
     float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < NVI; ++i) {
@@ -1616,6 +1656,7 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) ored[jg][doct * 8 + e] = o[e];
     __syncthreads();
+    trace_phase(a.phase, 3);
     if (!a.Wo) {
         if (tid < 64) {
             float v = ored[0][tid];
@@ -1636,6 +1677,17 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) ov[i] = *(const half8 *)(oh + 8 * i);
     float *dst = a.wo_parts + ((int64_t)b * a.H + h) * n;
+    if (wsplit) {
+        const int part = tid & 1;
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc = dot8(wov[0][i], part ? ov[4 + i] : ov[i], acc);
+        const float other = __shfl_xor(acc, 1);
+        if (part == 0) dst[blockIdx.z * 128 + (tid >> 1)] = acc + other;  // summed by the next kernel's prologue
+        trace_phase(a.phase, 7);
+        trace_end(a.trace);
+        return;
+    }
     for (int r = 0; r * 256 < n; ++r) {
         const int orow = tid + 256 * r;
         half8 wr[8];
@@ -1659,11 +1711,14 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
 hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
     if (a.M_fixed == 0) {  // self-attention: M = pos + 1 <= 512
         if (a.n_chunks != 1 || (a.Wo && !a.wo_parts)) return hipErrorInvalidValue;
+        // fused output projection split over n / 128 workgroups per head
+        const int S = (g_self_split && a.Wo && a.n % 128 == 0) ? a.n / 128 : 1;
+        const dim3 grid(a.H, a.B, S);
         switch (a.mk) {
-            case 64: hipLaunchKernelGGL(k_dec_self_attn<64>, dim3(a.H, a.B), dim3(256), 0, s, a); break;
-            case 128: hipLaunchKernelGGL(k_dec_self_attn<128>, dim3(a.H, a.B), dim3(256), 0, s, a); break;
-            case 256: hipLaunchKernelGGL(k_dec_self_attn<256>, dim3(a.H, a.B), dim3(256), 0, s, a); break;
-            case 512: hipLaunchKernelGGL(k_dec_self_attn<512>, dim3(a.H, a.B), dim3(256), 0, s, a); break;
+            case 64: hipLaunchKernelGGL(k_dec_self_attn<64>, grid, dim3(256), 0, s, a); break;
+            case 128: hipLaunchKernelGGL(k_dec_self_attn<128>, grid, dim3(256), 0, s, a); break;
+            case 256: hipLaunchKernelGGL(k_dec_self_attn<256>, grid, dim3(256), 0, s, a); break;
+            case 512: hipLaunchKernelGGL(k_dec_self_attn<512>, grid, dim3(256), 0, s, a); break;
             default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
