@@ -169,17 +169,9 @@ int64_t up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace
 
-constexpr int N_LINKS = 256;    // chained-launch arrival counters (64 B apart; >= launches per step)
-constexpr int N_JOIN_EV = 512;  // events for the decoder step's stream joins
-
 struct wmi_context {
     int device = 0;
     hipStream_t stream = nullptr;
-    // decoder step chain (DecLink): launches alternate between stream and stream2
-    hipStream_t stream2 = nullptr;
-    hipEvent_t evj[N_JOIN_EV] = {};
-    uint32_t *dlink = nullptr;
-    bool chain = true;              // WMI_NO_CHAIN=1: every decoder launch in stream order
     wmi_hparams hp{};
     wmi_special_tokens sp{};
     std::vector<std::string> vocab;
@@ -867,10 +859,7 @@ int alloc_workspace(wmi_context *ctx) {
     const size_t o_opart = A.take(Bd * Cmax * nt * 4);
     const size_t o_woparts = A.take(R * Hd * nt * 4);
     const size_t o_dx2 = A.take(R * nt * 4);
-    // polled words, zeroed together at the start of every decode run:
-    // cross-attention exchange counters, chain arrival counters, error word
-    const size_t xsync_bytes = (size_t)Lt * 8 * Hd * sizeof(XSync);
-    const size_t sync_bytes = xsync_bytes + (size_t)N_LINKS * 64;
+    const size_t sync_bytes = (size_t)Lt * 8 * Hd * sizeof(XSync);
     const size_t o_sync = A.take(sync_bytes + 256);
     const size_t o_amax = A.take(8 * AMAX_SHARDS * 8);
     const size_t o_st = A.take(sizeof(DecState));
@@ -914,7 +903,6 @@ int alloc_workspace(wmi_context *ctx) {
     for (int64_t r = 0; r < R; ++r)
         for (int j = 0; j < hp.n_text_ctx; ++j) ctx->kvsrc_init[(size_t)r * hp.n_text_ctx + j] = (int32_t)r;
     ctx->dsync = (XSync *)(b + o_sync);
-    ctx->dlink = (uint32_t *)(b + o_sync + xsync_bytes);
     ctx->dwoparts = (float *)(b + o_woparts);
     ctx->dx2 = (float *)(b + o_dx2);
     ctx->derr = (uint32_t *)(b + o_sync + sync_bytes);
@@ -1122,63 +1110,11 @@ int trace_dump(wmi_context *ctx) {
     return WMI_OK;
 }
 
-// The decoder step's launch chain.  Consecutive launches alternate between
-// the context's two streams and hand off through DecLink arrival counters,
-// so launch k's workgroups start, and request their weights, while launch
-// k - 1 still runs; stream order still keeps k - 2 -> k.  A pair whose grids
-// together might not all be resident at once (a spinning successor must
-// never keep its predecessor's workgroups from being scheduled) is joined
-// instead, as is the step's tail (logits, beam step) on stream 0.
-constexpr int CHAIN_MAX_WG = 480;
-struct Chain {
-    wmi_context *ctx;
-    hipStream_t s[2];
-    bool on;
-    int cur = 0, idx = 0, ev = 0;
-    uint32_t *prev = nullptr;
-    int prev_n = 0;
-    hipError_t err = hipSuccess;
-    explicit Chain(wmi_context *c) : ctx(c), s{c->stream, c->stream2}, on(c->chain && c->stream2 != nullptr) {}
-    // both streams wait for everything enqueued on either
-    void join() {
-        if (!on) return;
-        for (int i = 0; i < 2 && err == hipSuccess; ++i) {
-            if (ev >= N_JOIN_EV) { err = hipErrorInvalidValue; return; }
-            hipEvent_t e = ctx->evj[ev++];
-            err = hipEventRecord(e, s[i]);
-            if (err == hipSuccess) err = hipStreamWaitEvent(s[i ^ 1], e, 0);
-        }
-    }
-    // stream of the next launch (grid workgroups); fills its link
-    hipStream_t next(DecLink &lk, int grid) {
-        lk = DecLink{};
-        if (!on) return s[0];
-        if (prev && prev_n + grid <= CHAIN_MAX_WG) {
-            cur ^= 1;
-            lk.wait = prev;
-            lk.wait_n = (uint32_t)prev_n;
-        } else {
-            join();
-        }
-        if (idx >= N_LINKS) { err = hipErrorInvalidValue; return s[cur]; }
-        lk.signal = ctx->dlink + 16 * idx++;
-        lk.err = ctx->derr;
-        prev = lk.signal;
-        prev_n = grid;
-        return s[cur];
-    }
-    hipStream_t close() {
-        join();
-        prev = nullptr;
-        return s[0];
-    }
-};
-
 // one decoder step for clips [b0, b0 + B) of the encoded batch
 int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride, int suppress_eot, int out_stride) {
     const wmi_hparams &hp = ctx->hp;
     const int n = hp.n_text_state, H = hp.n_text_head, T = ctx->enc_T, Bt = ctx->enc_clips;
-    Chain ch(ctx);
+    hipStream_t s = ctx->stream;
     const float qs = powf((float)n / (float)H, -0.25f);
     ctx->trace_names.clear();
     const bool beam = ctx->beam_k > 0;
@@ -1210,7 +1146,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         }
         g.trace = tslot(ctx, "qkv", l);
         if (l == 0) g.phase = pslot(ctx, 0, "qkv[0]");
-        HIPCHK(ctx, launch_dec_gemv(ch.next(g.link, dec_gemv_grid(DEC_QKV, g)), DEC_QKV, g));
+        HIPCHK(ctx, launch_dec_gemv(s, DEC_QKV, g));
         DecAttnArgs at{};
         at.q = ctx->dq16; at.K = kc; at.V = vc; at.clip_stride = (int64_t)hp.n_text_ctx * n; at.M_fixed = 0;
         at.mk = ctx->self_mk; at.err = ctx->derr;
@@ -1229,14 +1165,14 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         }
         at.trace = tslot(ctx, "self_attn", l);
         if (l == 0) at.phase = pslot(ctx, 1, "self_attn[0]");
-        HIPCHK(ctx, launch_dec_attn(ch.next(at.link, dec_attn_grid(at)), at));
+        HIPCHK(ctx, launch_dec_attn(s, at));
         if (!ctx->fuse_wo) {
             g = DecGemvArgs{};
             g.parts = ctx->dopart; g.n_parts = 1; g.W = d.wo; g.bias = d.bo; g.N = n; g.K = n; g.B = B;
             g.Wq5 = q5 ? d.wo5 : nullptr;
-            g.out32 = X[cur]; g.st = ctx->dstate;
+            g.out32 = X[cur];
             g.trace = tslot(ctx, "wo", l);
-            HIPCHK(ctx, launch_dec_gemv(ch.next(g.link, dec_gemv_grid(DEC_RESID, g)), DEC_RESID, g));
+            HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
         }
         const int c_cross = (T + 127) / 128;
         at = DecAttnArgs{};
@@ -1255,32 +1191,28 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         }
         at.trace = tslot(ctx, "cross_attn", l);
         at.phase = ctx->trace_on ? ctx->d_trace + 2 * TRACE_SLOTS + 16 * l : nullptr;
-        HIPCHK(ctx, launch_dec_attn(ch.next(at.link, dec_attn_grid(at)), at));
+        HIPCHK(ctx, launch_dec_attn(s, at));
         g = DecGemvArgs{};
         g.parts = ctx->dopart; g.n_parts = c_cross; g.W = d.wco; g.bias = d.bco; g.N = n; g.K = n; g.B = B;
         g.Wq5 = q5 ? d.wco5 : nullptr;
-        g.out32 = X[cur]; g.st = ctx->dstate;
+        g.out32 = X[cur];
         g.trace = tslot(ctx, "wco", l);
         if (l == 0) g.phase = pslot(ctx, 2, "wco[0]");
-        HIPCHK(ctx, launch_dec_gemv(ch.next(g.link, dec_gemv_grid(DEC_RESID, g)), DEC_RESID, g));
+        HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
         g = DecGemvArgs{};
         g.x = X[cur]; g.ln_w = d.ln2_w; g.ln_b = d.ln2_b; g.W = d.w0; g.bias = d.b0; g.N = 4 * n; g.K = n; g.B = B;
         g.Wq5 = q5 ? d.w05 : nullptr;
-        g.out16 = ctx->dhid16; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab; g.st = ctx->dstate;
+        g.out16 = ctx->dhid16; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
         g.trace = tslot(ctx, "mlp0", l);
         if (l == 0) g.phase = pslot(ctx, 3, "mlp0[0]");
-        HIPCHK(ctx, launch_dec_gemv(ch.next(g.link, dec_gemv_grid(DEC_GELU, g)), DEC_GELU, g));
+        HIPCHK(ctx, launch_dec_gemv(s, DEC_GELU, g));
         g = DecGemvArgs{};
         g.xin16 = ctx->dhid16; g.W = d.w1; g.bias = d.b1; g.N = n; g.K = 4 * n; g.B = B; g.out32 = X[cur];
         g.Wq5 = q5 ? d.w15 : nullptr;
-        g.st = ctx->dstate;
         g.trace = tslot(ctx, "mlp1", l);
         if (l == 0) g.phase = pslot(ctx, 4, "mlp1[0]");
-        HIPCHK(ctx, launch_dec_gemv(ch.next(g.link, dec_gemv_grid(DEC_RESID, g)), DEC_RESID, g));
+        HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
     }
-    // the step's tail in stream order behind everything
-    hipStream_t s = ch.close();
-    HIPCHK(ctx, ch.err);
     DecGemvArgs g{};
     g.x = X[cur]; g.ln_w = ctx->dln_w; g.ln_b = ctx->dln_b; g.W = ctx->te; g.N = hp.n_vocab; g.K = n; g.B = B;
     g.Wq5 = ctx->use_q5 ? ctx->te5 : nullptr;
@@ -1617,8 +1549,6 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     }
     HIPCHK(ctx.get(), hipSetDevice(device));
     HIPCHK(ctx.get(), hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-    HIPCHK(ctx.get(), hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
-    for (int i = 0; i < N_JOIN_EV; ++i) HIPCHK(ctx.get(), hipEventCreateWithFlags(&ctx->evj[i], hipEventDisableTiming));
     rc = upload_model(ctx.get(), pm);
     if (rc) { g_last_error = ctx->last_error; wmi_free(ctx.release()); return rc; }
     pm.tensors.clear();
@@ -1628,7 +1558,6 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (getenv("WMI_NO_COOP")) ctx->use_coop = false;
     if (getenv("WMI_NO_Q5")) ctx->use_q5 = false;
     if (getenv("WMI_NO_FUSE")) ctx->fuse_wo = false;
-    if (getenv("WMI_NO_CHAIN")) ctx->chain = false;
     if (const char *c = getenv("WMI_LOGITS_CAP")) g_logits_cap = atoi(c) > 0 ? atoi(c) : g_logits_cap;
     if (const char *c = getenv("WMI_GEMV_NW")) g_gemv_nw = atoi(c) == 1 ? 1 : atoi(c) == 0 ? 0 : 4;
     if (const char *c = getenv("WMI_SELF_SPLIT")) g_self_split = atoi(c) >= 0 ? atoi(c) : g_self_split;
@@ -1645,7 +1574,6 @@ void wmi_free(wmi_context *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     ctx->clear_graphs();
     for (float *p : ctx->pcm_dev) if (p) (void)hipFree(p);
@@ -1657,8 +1585,6 @@ void wmi_free(wmi_context *ctx) {
     if (ctx->d_trace) (void)hipFree(ctx->d_trace);
     if (ctx->d_model) (void)hipFree(ctx->d_model);
     for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
-    for (auto &e : ctx->evj) if (e) (void)hipEventDestroy(e);
-    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
