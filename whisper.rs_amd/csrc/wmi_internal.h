@@ -95,20 +95,6 @@ struct DecState {          // device-resident, advanced by the kernels
 
 enum DecEpi { DEC_QKV = 0, DEC_Q = 1, DEC_GELU = 2, DEC_RESID = 3, DEC_LOGITS = 4 };
 
-// Chained decoder launches (overlapped step): launch k runs on the other
-// stream than launch k - 1, so it starts while k - 1 still runs; it issues
-// its weight loads, then waits until every workgroup of k - 1 has arrived
-// (monotonic counter, target (pos + 1) * wait_n) before reading k - 1's
-// outputs.  Words handed from k - 1 to k are stored write-through (sc1) and
-// read with sc1 loads (MI355X_MICROARCH.md visibility table, first row);
-// everything older is ordered by the stream (k - 2 -> k).
-struct DecLink {
-    uint32_t *wait;          // predecessor's arrival counter (null: stream order only)
-    uint32_t wait_n;         // predecessor's workgroups
-    uint32_t *signal;        // this launch's arrival counter (null: nobody waits)
-    uint32_t *err;           // bit 0 set on a spin timeout
-};
-
 struct DecGemvArgs {
     const float *x;          // LN input [B][K] f32 (ln != null)
     const float *ln_w, *ln_b;
@@ -143,7 +129,6 @@ struct DecGemvArgs {
     const int32_t *beam_tok;    // beam search: token of row b past the prompt (BeamState::tok), else null
     unsigned long long *trace;  // WMI_TRACE: {min start, ~max end} s_memrealtime of this launch
     unsigned long long *phase;  // WMI_TRACE: [2][8] phase times of the first and last workgroup
-    DecLink link;
 };
 constexpr int AMAX_SHARDS = 64;
 constexpr int DEC_ROWS = 8;  // decoder rows per step: clips (greedy) or beam hypotheses
@@ -193,11 +178,7 @@ struct DecAttnArgs {
     float *x_out;
     unsigned long long *trace;  // WMI_TRACE slot (see DecGemvArgs)
     unsigned long long *phase;  // WMI_TRACE: [2][8] phase times of the first and last chunk of (head 0, clip 0)
-    DecLink link;            // two-kernel cross-attention: the first launch waits, the second (P.V) signals
 };
-// workgroups of each decoder launch (the chained successor's wait count)
-int dec_gemv_grid(int epi, const DecGemvArgs &a);
-int dec_attn_grid(const DecAttnArgs &a);
 // exchange words of one (layer, clip, head) for the cooperative kernel
 struct XSync {
     uint32_t cnt;            // monotonic arrival counter (target (pos + 1) * n_chunks)

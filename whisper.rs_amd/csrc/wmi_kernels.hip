@@ -771,62 +771,6 @@ __device__ __forceinline__ float4 keep4(float4 v, bool ok) {
 }
 __device__ __forceinline__ float keep1(float v, bool ok) { return v * (ok ? 1.0f : 0.0f); }
 
-// ---- hand-offs between chained decoder launches (DecLink) -----------------
-// Words the next launch reads while this one may still run are stored
-// write-through (sc1) and loaded with sc1 loads (L1 bypass); 16-byte loads
-// go through a buffer resource on a wave-uniform base (aux 16 = sc1).
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ uint4 ld1_16(const void *base, uint32_t off) {
-    const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(brsrc(base), off, 0, 16);
-    return make_uint4(v[0], v[1], v[2], v[3]);
-}
-__device__ __forceinline__ float4 ld1_f4(const void *base, uint32_t off) {
-    const uint4 v = ld1_16(base, off);
-    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-__device__ __forceinline__ half8 ld1_h8(const void *base, uint32_t off) { return __builtin_bit_cast(half8, ld1_16(base, off)); }
-__device__ __forceinline__ float ld1_f32(const float *p) {
-    return __uint_as_float(__hip_atomic_load((uint32_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void st1_f32(float *p, float v) {
-    __hip_atomic_store((uint32_t *)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st1_u16(uint16_t *p, uint16_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// 16 B at base + off (base wave-uniform)
-__device__ __forceinline__ void st1_f4(float *base, uint32_t off, float4 v) {
-    const u32x4_t u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-    __builtin_amdgcn_raw_buffer_store_b128(u, brsrc(base), off, 0, 16);
-}
-// wait for every workgroup of the predecessor launch (thread 0 polls, the
-// workgroup barrier releases the others; bounded: sets err bit 0 and goes on)
-__device__ __forceinline__ void link_wait(const DecLink &lk, int pos) {
-    if (!lk.wait) return;
-    if (threadIdx.x == 0) {
-        const uint32_t target = (uint32_t)(pos + 1) * lk.wait_n;
-        for (uint32_t it = 0;; ++it) {
-            if (__hip_atomic_load(lk.wait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
-            if (it > (1u << 22)) {
-                __hip_atomic_store(lk.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    __syncthreads();
-}
-// this workgroup's arrival, after every wave's stores have drained
-__device__ __forceinline__ void link_signal(const DecLink &lk) {
-    if (!lk.signal) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(lk.signal, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // LayerNorm input row as float4 registers: unconditional (clamped) loads so
 // every request is in flight before the first wait
 __device__ __forceinline__ void ln_load_row(const float *x, int K, int lane, float4 (&xv)[DG_LNV]) {
@@ -836,17 +780,6 @@ __device__ __forceinline__ void ln_load_row(const float *x, int K, int lane, flo
         const int idx = lane + 64 * i;
         const bool ok = idx * 4 < K;
         xv[i] = keep4(xr[ok ? idx : 0], ok);
-    }
-}
-
-// the same with sc1 loads (the row may come from the chained predecessor);
-// x must be wave-uniform
-__device__ __forceinline__ void ln_load_row1(const float *x, int K, int lane, float4 (&xv)[DG_LNV]) {
-#pragma unroll
-    for (int i = 0; i < DG_LNV; ++i) {
-        const int idx = lane + 64 * i;
-        const bool ok = idx * 4 < K;
-        xv[i] = keep4(ld1_f4(x, (uint32_t)(ok ? idx : 0) * 16u), ok);
     }
 }
 
@@ -1016,15 +949,7 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
         for (int g = 0; g < G; ++g) {
             const int o = rb + g * 4 + q;
             S.eb[g] = (a.bias && o < N) ? a.bias[o] : 0.0f;
-            S.er[g] = 0.0f;
-        }
-    };
-    // residual operand: the stream the predecessor may have just written
-    auto load_res = [&](WSet &S, int rb) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int o = rb + g * 4 + q;
-            S.er[g] = (EPI == DEC_RESID && o < N && l16 < B) ? ld1_f32(a.out32 + (int64_t)l16 * N + o) : 0.0f;
+            S.er[g] = (EPI == DEC_RESID && o < N && l16 < B) ? a.out32[(int64_t)l16 * N + o] : 0.0f;
         }
     };
     auto dot_set = [&](const WSet &S, int k0, float (&acc)[G][DG_MAXB]) {
@@ -1088,19 +1013,18 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
                 if (l16 == bb) v = acc[g][bb];
             if (l16 >= B || o >= N) continue;
             const int bb = l16;
-            // outputs the next (possibly already running) launch reads: sc1
             if (EPI == DEC_QKV) {
                 const int n = N / 3, which = o / n, c = o - which * n;
-                if (which == 0) st1_u16(a.out16 + bb * a.ldo + c, f2h_bits((v + S.eb[g]) * a.qscale));
+                if (which == 0) a.out16[bb * a.ldo + c] = f2h_bits((v + S.eb[g]) * a.qscale);
                 else if (which == 1)
-                    st1_u16(a.kcache + ((int64_t)bb * a.n_text_ctx + pos) * n + c, f2h_bits(v * a.qscale));
-                else st1_u16(a.vcache + ((int64_t)bb * a.n_text_ctx + pos) * n + c, f2h_bits(S.eb[g] + v));
+                    a.kcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(v * a.qscale);
+                else a.vcache[((int64_t)bb * a.n_text_ctx + pos) * n + c] = f2h_bits(S.eb[g] + v);
             } else if (EPI == DEC_Q) {
-                st1_u16(a.out16 + bb * a.ldo + o, f2h_bits((v + S.eb[g]) * a.qscale));
+                a.out16[bb * a.ldo + o] = f2h_bits((v + S.eb[g]) * a.qscale);
             } else if (EPI == DEC_GELU) {
-                st1_u16(a.out16 + bb * a.ldo + o, a.gelu_tab[f2h_bits(v + S.eb[g])]);
+                a.out16[bb * a.ldo + o] = a.gelu_tab[f2h_bits(v + S.eb[g])];
             } else if (EPI == DEC_RESID) {
-                st1_f32(a.out32 + (int64_t)bb * N + o, (v + S.eb[g]) + S.er[g]);
+                a.out32[(int64_t)bb * N + o] = (v + S.eb[g]) + S.er[g];
             } else if (EPI == DEC_LOGITS) {
                 a.out32[(int64_t)bb * N + o] = v;
                 if (a.amax && o != a.suppress_id) {
@@ -1119,11 +1043,9 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
     };
     // LayerNorm operands of row w first: the LN below then waits for them
     // while the weight stream issued after them is still in flight
-    // (chained: the predecessor writes x, so only the constants go first)
-    const bool linked = a.link.wait != nullptr;
     float4 xv0[DG_LNV], gw0[DG_LNV], gb0[DG_LNV];
     if (IN == 0 && w < B) {
-        if (!linked) ln_load_row1(a.x + (int64_t)w * K, K, lane, xv0);
+        ln_load_row(a.x + (int64_t)w * K, K, lane, xv0);
         ln_load_params(a.ln_w, a.ln_b, K, lane, gw0, gb0);
     }
     // every weight / epilogue request of the first group(s) before the prologue
@@ -1136,10 +1058,6 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
         load_epi(S1, rbase(rgB));
     }
     trace_phase(a.phase, 1);
-    // chained launch: the weights are in flight; now wait for the predecessor
-    link_wait(a.link, linked ? a.st->pos : 0);
-    if (IN == 0 && w < B && linked) ln_load_row1(a.x + (int64_t)w * K, K, lane, xv0);
-    if (!PIPE) load_res(S0, rbase(rgA));
     if (IN == 0 || IN == 3) {
         // each wave normalises rows w, w + NW, ...
         const int pos = (IN == 3) ? a.st->pos : 0;
@@ -1153,7 +1071,7 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
                     continue;
                 }
                 if (IN == 0) {
-                    ln_load_row1(a.x + (int64_t)rb * K, K, lane, xv);
+                    ln_load_row(a.x + (int64_t)rb * K, K, lane, xv);
                 } else {
                     // x = te[tok] + pe[pos] (get_rows f16 -> f32, add)
                     const bool fed = pos < a.feed_len;
@@ -1184,18 +1102,19 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
             }
         }
     } else if (IN == 1) {
+        const uint4 *src = (const uint4 *)a.xin16;
         uint4 *dst = (uint4 *)xs;
-        for (int i = tid; i < B * K / 8; i += 64 * NW) dst[i] = ld1_16(a.xin16, (uint32_t)i * 16u);
+        for (int i = tid; i < B * K / 8; i += 64 * NW) dst[i] = src[i];
     } else {
         // partial sums: thread owns 4 consecutive inputs; all chunk loads issued first
         constexpr int CMAXP = 16;
         for (int i4 = tid; i4 < B * K / 4; i4 += 64 * NW) {
             const int bb = (i4 * 4) / K, k = i4 * 4 - bb * K;
-            const uint32_t p = (uint32_t)(((int64_t)bb * a.n_parts) * K + k) * 4u;  // byte offset in parts
+            const float *p = a.parts + ((int64_t)bb * a.n_parts) * K + k;
             float4 v[CMAXP];
 #pragma unroll
             for (int c = 0; c < CMAXP; ++c)
-                v[c] = c < a.n_parts ? ld1_f4(a.parts, p + (uint32_t)c * K * 4u) : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[c] = c < a.n_parts ? *(const float4 *)(p + (int64_t)c * K) : make_float4(0.f, 0.f, 0.f, 0.f);
             float4 sacc = v[0];
 #pragma unroll
             for (int c = 1; c < CMAXP; ++c)
@@ -1246,7 +1165,6 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
         if (a.amax && tid < B && amax_s[tid]) atomicMax(&a.amax[tid * AMAX_SHARDS + (blockIdx.x & (AMAX_SHARDS - 1))], amax_s[tid]);
         if (blockIdx.x == 0 && tid == 0) a.st_advance->pos += 1;
     }
-    link_signal(a.link);
     trace_phase(a.phase, 7);
     trace_end(a.trace);
 }
@@ -1448,8 +1366,8 @@ __device__ __forceinline__ void xattn_pv(const DecAttnArgs &a, int c, int h, int
         for (int e = 0; e < 8; ++e) ow[w][lane * 8 + e] = o[e];
     __syncthreads();
     if (tid < 64)
-        st1_f32(a.opart + ((int64_t)b * a.n_chunks + c) * n + h * 64 + tid,
-                ((ow[0][tid] + ow[1][tid]) + ow[2][tid]) + ow[3][tid]);
+        a.opart[((int64_t)b * a.n_chunks + c) * n + h * 64 + tid] =
+            ((ow[0][tid] + ow[1][tid]) + ow[2][tid]) + ow[3][tid];
 }
 
 // this chunk's V rows for xattn_pv (clamped rows: every load unconditional)
@@ -1491,11 +1409,17 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
     float4 rp[H2], rbo, rx;
     const bool rpart = a.res_parts != nullptr && tid < n / 4;
     if (rpart) {
+        const float *pp = a.res_parts + (int64_t)b * H2 * n + 4 * tid;
+#pragma unroll
+        for (int hh = 0; hh < H2; ++hh) rp[hh] = *(const float4 *)(pp + (int64_t)hh * n);
         rbo = *(const float4 *)(a.res_bias + 4 * tid);
         rx = *(const float4 *)(a.x + (int64_t)b * n + 4 * tid);
     }
     float4 xv[DG_LNV], gw[DG_LNV], gb[DG_LNV];
-    if (w == 0) ln_load_params(a.ln_w, a.ln_b, n, lane, gw, gb);
+    if (w == 0) {
+        ln_load_params(a.ln_w, a.ln_b, n, lane, gw, gb);
+        if (!a.res_parts) ln_load_row(a.x + (int64_t)b * n, n, lane, xv);
+    }
     const int key = c * DA_CK + (tid >> 1), half = tid & 1;
     half8 kf[4];
     {
@@ -1516,15 +1440,6 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
         for (int kc = 0; kc < KC; ++kc) wq[i][kc] = *(const half8 *)(wr + kc * 128);
         bqr[i] = a.bq[r];
     }
-    // the chained self-attention's outputs (its per-head partials, or with a
-    // separate output projection the updated x): after its arrival, sc1
-    link_wait(a.link, a.st->pos);
-    if (rpart) {
-        const uint32_t pp = (uint32_t)(((int64_t)b * H2 * n + 4 * tid) * 4);
-#pragma unroll
-        for (int hh = 0; hh < H2; ++hh) rp[hh] = ld1_f4(a.res_parts, pp + (uint32_t)hh * n * 4u);
-    }
-    if (w == 0 && !a.res_parts) ln_load_row1(a.x + (int64_t)b * n, n, lane, xv);
     if (a.res_parts) {
         // the fused self-attention's residual update: x + (bo + sum over the
         // H heads of its output-projection partials), in head order; block
@@ -1532,9 +1447,9 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
         __shared__ __attribute__((aligned(16))) float xnew[KC * 128];
         for (int j = tid; j < n / 4; j += 256) {
             if (j != tid) {  // second pass (n > 1024): operands not prefetched
-                const uint32_t pp = (uint32_t)(((int64_t)b * H2 * n + 4 * j) * 4);
+                const float *pp = a.res_parts + (int64_t)b * H2 * n + 4 * j;
 #pragma unroll
-                for (int hh = 0; hh < H2; ++hh) rp[hh] = ld1_f4(a.res_parts, pp + (uint32_t)hh * n * 4u);
+                for (int hh = 0; hh < H2; ++hh) rp[hh] = *(const float4 *)(pp + (int64_t)hh * n);
                 rbo = *(const float4 *)(a.res_bias + 4 * j);
                 rx = *(const float4 *)(a.x + (int64_t)b * n + 4 * j);
             }
@@ -1547,7 +1462,7 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
             v.x = (rbo.x + sm.x) + rx.x; v.y = (rbo.y + sm.y) + rx.y;
             v.z = (rbo.z + sm.z) + rx.z; v.w = (rbo.w + sm.w) + rx.w;
             *(float4 *)(xnew + 4 * j) = v;
-            if (c == 0 && h == 0) st1_f4(a.x_out + (int64_t)b * n, 16u * j, v);  // read by the next launch
+            if (c == 0 && h == 0) *(float4 *)(a.x_out + (int64_t)b * n + 4 * j) = v;
         }
         __syncthreads();
         if (w == 0) {
@@ -1601,7 +1516,6 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
     __syncthreads();
     trace_phase(a.phase, 4);
     xattn_pv<COH>(a, c, h, b, M, vf);
-    link_signal(a.link);
     trace_phase(a.phase, 7);
     trace_end(a.trace);
 }
@@ -1613,7 +1527,6 @@ __global__ __launch_bounds__(256) void k_dec_attn_pv(DecAttnArgs a) {
     half8 vf[4];
     xattn_load_v(a, c, h, b, M, vf);
     xattn_pv<false>(a, c, h, b, M, vf);
-    link_signal(a.link);
     trace_end(a.trace);
 }
 
@@ -1634,30 +1547,7 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     __shared__ __attribute__((aligned(16))) uint16_t P[MK];
     if (M > MK && tid == 0 && a.err) atomicOr(a.err, 2u);  // host bucketing error: flagged, never silent
     __shared__ float ored[32][64];
-    // fused output projection: this head's 64 Wo columns for output rows
-    // tid + 256 r (the first two prefetched now, independent of the attention)
-    // Split form (gridDim.z = n / 128 > 1): workgroup z owns output rows
-    // [128 z, 128 z + 128), two threads per row (32 columns each); the
-    // attention itself is recomputed by each of the head's workgroups.
-    // Constants, so requested before the wait for the chained QKV launch.
-    constexpr int WOR = 2;
-    const bool wsplit = gridDim.z > 1;
-    half8 wov[WOR][8];
-    if (a.Wo && wsplit) {
-        const int orow = blockIdx.z * 128 + (tid >> 1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            wov[0][i] = wload((const half8 *)(a.Wo + (int64_t)orow * n + h * 64 + 32 * (tid & 1) + 8 * i));
-    } else if (a.Wo) {
-#pragma unroll
-        for (int r = 0; r < WOR; ++r) {
-            const int orow = min(tid + 256 * r, n - 1);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) wov[r][i] = wload((const half8 *)(a.Wo + (int64_t)orow * n + h * 64 + 8 * i));
-        }
-    }
-    link_wait(a.link, M - 1);
-    // the step's first launch has read the previous argmax words by now
+    const f16 *qr = (const f16 *)a.q + (int64_t)b * n + h * 64;
     if (a.reset_amax && h == 0 && b == 0 && blockIdx.z == 0)
         for (int i = tid; i < a.B * AMAX_SHARDS; i += 256) a.reset_amax[i] = 0ull;
     // cache row of key j: slot b, or (beam search) the slot holding the
@@ -1690,18 +1580,38 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     half8 kv[RK][8];
 #pragma unroll
     for (int r = 0; r < RK; ++r) {
-        // sc1: row pos was written by the chained QKV launch
-        const uint32_t ko = (uint32_t)((sk[r] * a.clip_stride + (int64_t)jk[r] * n + h * 64) * 2);
+        const f16 *kr = (const f16 *)a.K + sk[r] * a.clip_stride + (int64_t)jk[r] * n + h * 64;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) kv[r][i] = ld1_h8(a.K, ko + 16u * i);
+        for (int i = 0; i < 8; ++i) kv[r][i] = *(const half8 *)(kr + 8 * i);
     }
     half8 vv[NVI];
 #pragma unroll
     for (int i = 0; i < NVI; ++i)
-        vv[i] = ld1_h8(a.V, (uint32_t)((sv[i] * a.clip_stride + (int64_t)jv[i] * n + h * 64 + doct * 8) * 2));
+        vv[i] = *(const half8 *)((const f16 *)a.V + sv[i] * a.clip_stride + (int64_t)jv[i] * n + h * 64 + doct * 8);
     half8 qv[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) qv[i] = ld1_h8(a.q, (uint32_t)(((int64_t)b * n + h * 64 + 8 * i) * 2));
+    for (int i = 0; i < 8; ++i) qv[i] = *(const half8 *)(qr + 8 * i);
+    // fused output projection: this head's 64 Wo columns for output rows
+    // tid + 256 r (the first two prefetched now, independent of the attention)
+    // Split form (gridDim.z = n / 128 > 1): workgroup z owns output rows
+    // [128 z, 128 z + 128), two threads per row (32 columns each); the
+    // attention itself is recomputed by each of the head's workgroups
+    constexpr int WOR = 2;
+    const bool wsplit = gridDim.z > 1;
+    half8 wov[WOR][8];
+    if (a.Wo && wsplit) {
+        const int orow = blockIdx.z * 128 + (tid >> 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            wov[0][i] = wload((const half8 *)(a.Wo + (int64_t)orow * n + h * 64 + 32 * (tid & 1) + 8 * i));
+    } else if (a.Wo) {
+#pragma unroll
+        for (int r = 0; r < WOR; ++r) {
+            const int orow = min(tid + 256 * r, n - 1);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wov[r][i] = wload((const half8 *)(a.Wo + (int64_t)orow * n + h * 64 + 8 * i));
+        }
+    }
     trace_phase(a.phase, 1);
     float sc[RK];
     float mx = -INFINITY;
@@ -1751,9 +1661,8 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
         if (tid < 64) {
             float v = ored[0][tid];
             for (int g = 1; g < 32; ++g) v = v + ored[g][tid];
-            st1_f32(a.opart + (int64_t)b * n + h * 64 + tid, v);
+            a.opart[(int64_t)b * n + h * 64 + tid] = v;
         }
-        link_signal(a.link);
         trace_end(a.trace);
         return;
     }
@@ -1774,8 +1683,7 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc = dot8(wov[0][i], part ? ov[4 + i] : ov[i], acc);
         const float other = __shfl_xor(acc, 1);
-        if (part == 0) st1_f32(dst + blockIdx.z * 128 + (tid >> 1), acc + other);  // summed by the next launch
-        link_signal(a.link);
+        if (part == 0) dst[blockIdx.z * 128 + (tid >> 1)] = acc + other;  // summed by the next kernel's prologue
         trace_phase(a.phase, 7);
         trace_end(a.trace);
         return;
@@ -1794,9 +1702,8 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
         float acc = 0.0f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc = dot8(wr[i], ov[i], acc);
-        if (orow < n) st1_f32(dst + orow, acc);  // summed by the next launch's prologue
+        if (orow < n) dst[orow] = acc;  // summed by the next kernel's prologue
     }
-    link_signal(a.link);
     trace_end(a.trace);
 }
 
@@ -1824,15 +1731,10 @@ hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
     // (<= 2 workgroups per CU) and the Wq rows fit the register budget;
     // otherwise the two-kernel form
     const bool coop = a.sync && a.n_chunks * a.H * a.B <= 512 && a.n <= 768;
-    // two-kernel form: the first launch waits for the chained predecessor,
-    // the second (P.V, stream-ordered behind it) signals the successor
-    DecAttnArgs a1 = a, a2 = a;
-    a1.link.signal = nullptr;
-    a2.link.wait = nullptr;
 #define XA(KC)                                                                                  \
     case KC:                                                                                    \
         if (coop) hipLaunchKernelGGL((k_dec_xattn<KC, 1>), grid, dim3(256), 0, s, a);          \
-        else hipLaunchKernelGGL((k_dec_xattn<KC, 0>), grid, dim3(256), 0, s, a1);              \
+        else hipLaunchKernelGGL((k_dec_xattn<KC, 0>), grid, dim3(256), 0, s, a);               \
         break;
     switch (a.n / 128) {
         XA(1) XA(2) XA(3) XA(4) XA(5) XA(6) XA(8) XA(10)
@@ -1841,19 +1743,8 @@ hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
 #undef XA
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || coop) return e;
-    hipLaunchKernelGGL(k_dec_attn_pv, grid, dim3(256), 0, s, a2);
+    hipLaunchKernelGGL(k_dec_attn_pv, grid, dim3(256), 0, s, a);
     return hipGetLastError();
-}
-
-// workgroups of each decoder launch (the chained successor's wait count)
-int dec_gemv_grid(int epi, const DecGemvArgs &a) {
-    const int nw = (epi != DEC_LOGITS && (g_gemv_nw == 1 || (g_gemv_nw == 0 && a.B <= 2))) ? 1 : 4;
-    const int nrg = cdiv(a.N, 4 * nw), cap = epi == DEC_LOGITS ? g_logits_cap : 1 << 30;
-    return nrg < cap ? nrg : cap;
-}
-int dec_attn_grid(const DecAttnArgs &a) {
-    if (a.M_fixed == 0) return a.H * a.B * ((g_self_split && a.Wo && a.n % 128 == 0) ? a.n / 128 : 1);
-    return a.n_chunks * a.H * a.B;
 }
 
 // records the token produced by the last step (the in-step record happens in
