@@ -662,6 +662,7 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
     const size_t o_filt = add(filt_t.data(), filt_t.size() * 4);
     const size_t o_gelu = add(gelu.data(), gelu.size() * 2);
     std::vector<uint16_t> expneg(expt.begin() + 0x8000, expt.begin() + 0x8000 + n_exp);
+    expneg.resize((expneg.size() + 7) / 8 * 8, 0);  // whole 16-byte chunks for the LDS copy
     const size_t o_exp = add(expneg.data(), expneg.size() * 2);
     // conv weights -> [o][tap][Cp] (implicit-GEMM B operand)
     auto pack_conv = [&](const HostTensor &w, int Cin, int Cp) {
@@ -1558,6 +1559,7 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (getenv("WMI_NO_COOP")) ctx->use_coop = false;
     if (getenv("WMI_NO_Q5")) ctx->use_q5 = false;
     if (getenv("WMI_NO_FUSE")) ctx->fuse_wo = false;
+    if (const char *c = getenv("WMI_ATTN_V1")) g_attn_v1 = atoi(c) == 2 ? 2 : 1;
     if (const char *c = getenv("WMI_LOGITS_CAP")) g_logits_cap = atoi(c) > 0 ? atoi(c) : g_logits_cap;
     if (const char *c = getenv("WMI_GEMV_NW")) g_gemv_nw = atoi(c) == 1 ? 1 : atoi(c) == 0 ? 0 : 4;
     if (const char *c = getenv("WMI_SELF_SPLIT")) g_self_split = atoi(c) >= 0 ? atoi(c) : g_self_split;

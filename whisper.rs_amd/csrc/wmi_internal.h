@@ -86,6 +86,7 @@ struct AttnArgs {
     float scale;
 };
 hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a);
+extern int g_attn_v1;
 
 // ---- decoder step -----------------------------------------
 struct DecState {          // device-resident, advanced by the kernels
