@@ -103,6 +103,22 @@ int wmi_set_audio_ctx(wmi_context *ctx, int n_audio_ctx);
  * terminated) into buf, *len = byte count; WMI_E_NO_SPACE if cap too small. */
 int wmi_token_to_bytes(const wmi_context *ctx, int32_t id, char *buf, size_t cap, size_t *len);
 
+/* ---- audio input and text output --------------- */
+
+/* hound::WavReader::open(path) + samples::<i16>() (main.rs:2067-2068):
+ * 16-bit integer PCM RIFF/WAVE, samples interleaved as stored.  With
+ * samples == NULL only *n_samples (and rate / channels) are filled.
+ * WMI_E_IO: missing / malformed file; WMI_E_UNSUPPORTED: not 16-bit PCM;
+ * WMI_E_NO_SPACE: cap < *n_samples.  Needs no context or device. */
+int wmi_read_wav(const char *path, int16_t *samples, size_t cap, size_t *n_samples, int32_t *sample_rate,
+                 int32_t *channels);
+/* convert_integer_to_float_audio (main.rs:1673-1679): out[i] = s16[i] / 32768. */
+int wmi_pcm16_to_f32(const int16_t *s16, size_t n, float *out);
+/* Detokenise: the id_to_token bytes (main.rs:578-592) of the text tokens
+ * (id < eot) of ids[0..n), concatenated; special and timestamp tokens are
+ * skipped.  *len = byte count; WMI_E_NO_SPACE if cap < *len. */
+int wmi_tokens_to_text(const wmi_context *ctx, const int32_t *ids, int n, char *buf, size_t cap, size_t *len);
+
 /* ---- pipeline (reference entry points) ------------------------------ */
 
 /* whisper_pcm_to_mel (main.rs:1681-1707): f32 PCM (s16/32768) -> log-mel. */

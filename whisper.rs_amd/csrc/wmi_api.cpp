@@ -1611,6 +1611,84 @@ int wmi_set_audio_ctx(wmi_context *ctx, int n_audio_ctx) {
     return WMI_OK;
 }
 
+// hound::WavReader::open(path) + samples::<i16>() (main.rs:2067-2068): a
+// RIFF/WAVE file with 16-bit integer PCM; samples interleaved as stored.
+// Chunks other than "fmt " and "data" are skipped (word-aligned, as RIFF
+// requires); a data chunk longer than the file is an IO error, as is a
+// missing "fmt " before "data".
+int wmi_read_wav(const char *path, int16_t *samples, size_t cap, size_t *n_samples, int32_t *sample_rate,
+                 int32_t *channels) {
+    if (!path || !n_samples) return set_err(nullptr, WMI_E_INVALID_ARG, "null argument");
+    FILE *f = fopen(path, "rb");
+    if (!f) return set_err(nullptr, WMI_E_IO, "cannot open %s", path);
+    struct Closer { FILE *f; ~Closer() { fclose(f); } } closer{f};
+    unsigned char hdr[12];
+    if (fread(hdr, 1, 12, f) != 12 || memcmp(hdr, "RIFF", 4) || memcmp(hdr + 8, "WAVE", 4))
+        return set_err(nullptr, WMI_E_IO, "%s: not a RIFF/WAVE file", path);
+    auto u16 = [](const unsigned char *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); };
+    auto u32 = [](const unsigned char *p) {
+        return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+    };
+    bool have_fmt = false;
+    uint32_t fmt_tag = 0, nch = 0, sr = 0, bits = 0;
+    for (;;) {
+        unsigned char ch[8];
+        if (fread(ch, 1, 8, f) != 8) return set_err(nullptr, WMI_E_IO, "%s: no data chunk", path);
+        const uint32_t size = u32(ch + 4);
+        if (!memcmp(ch, "fmt ", 4)) {
+            if (size < 16) return set_err(nullptr, WMI_E_IO, "%s: short fmt chunk", path);
+            std::vector<unsigned char> fmt(size + (size & 1));
+            if (fread(fmt.data(), 1, fmt.size(), f) != fmt.size()) return set_err(nullptr, WMI_E_IO, "%s: truncated fmt", path);
+            fmt_tag = u16(fmt.data());
+            nch = u16(fmt.data() + 2);
+            sr = u32(fmt.data() + 4);
+            bits = u16(fmt.data() + 14);
+            if (fmt_tag == 0xFFFE && size >= 26) fmt_tag = u16(fmt.data() + 24);  // WAVE_FORMAT_EXTENSIBLE subformat
+            have_fmt = true;
+        } else if (!memcmp(ch, "data", 4)) {
+            if (!have_fmt) return set_err(nullptr, WMI_E_IO, "%s: data before fmt", path);
+            if (fmt_tag != 1 || bits != 16 || nch < 1)
+                return set_err(nullptr, WMI_E_UNSUPPORTED, "%s: format %u, %u bits, %u channels (need 16-bit PCM)", path,
+                               fmt_tag, bits, nch);
+            const size_t n = size / 2;
+            *n_samples = n;
+            if (sample_rate) *sample_rate = (int32_t)sr;
+            if (channels) *channels = (int32_t)nch;
+            if (!samples) return WMI_OK;
+            if (cap < n) return WMI_E_NO_SPACE;
+            std::vector<unsigned char> raw(size);
+            if (fread(raw.data(), 1, size, f) != size) return set_err(nullptr, WMI_E_IO, "%s: truncated data", path);
+            for (size_t i = 0; i < n; ++i) samples[i] = (int16_t)u16(raw.data() + 2 * i);
+            return WMI_OK;
+        } else if (fseek(f, (long)(size + (size & 1)), SEEK_CUR) != 0) {
+            return set_err(nullptr, WMI_E_IO, "%s: truncated chunk", path);
+        }
+    }
+}
+
+// convert_integer_to_float_audio (main.rs:1673-1679): f = s / 32768.0
+int wmi_pcm16_to_f32(const int16_t *s16, size_t n, float *out) {
+    if ((!s16 || !out) && n) return WMI_E_INVALID_ARG;
+    for (size_t i = 0; i < n; ++i) out[i] = (float)s16[i] / 32768.0f;
+    return WMI_OK;
+}
+
+// Text of a token sequence: the id_to_token bytes (main.rs:578-592) of every
+// text token (id < eot) concatenated, special and timestamp tokens skipped,
+// as whisper.cpp-1.0.3's whisper_full builds a segment's text.
+int wmi_tokens_to_text(const wmi_context *ctx, const int32_t *ids, int n, char *buf, size_t cap, size_t *len) {
+    if (!ctx || (!ids && n) || n < 0 || !len) return WMI_E_INVALID_ARG;
+    std::string s;
+    for (int i = 0; i < n; ++i) {
+        if (ids[i] < 0 || ids[i] >= (int32_t)ctx->vocab.size()) return WMI_E_INVALID_ARG;
+        if (ids[i] < ctx->sp.eot) s += ctx->vocab[ids[i]];
+    }
+    *len = s.size();
+    if (!buf || cap < s.size()) return WMI_E_NO_SPACE;
+    memcpy(buf, s.data(), s.size());
+    return WMI_OK;
+}
+
 int wmi_token_to_bytes(const wmi_context *ctx, int32_t id, char *buf, size_t cap, size_t *len) {
     if (!ctx || !len) return WMI_E_INVALID_ARG;
     if (id < 0 || id >= (int32_t)ctx->vocab.size()) return WMI_E_INVALID_ARG;

@@ -60,6 +60,7 @@ _ERRORS = {c.code: c for c in (UnexpectIO, BadMagic, NotEnoughSpace, UnknownTens
 EXPORTS = (
     "wmi_init_from_file", "wmi_free", "wmi_strerror", "wmi_last_error", "wmi_last_error_global",
     "wmi_get_hparams", "wmi_get_special_tokens", "wmi_set_audio_ctx", "wmi_token_to_bytes",
+    "wmi_read_wav", "wmi_pcm16_to_f32", "wmi_tokens_to_text",
     "wmi_pcm_to_mel", "wmi_pcm_to_mel_batch", "wmi_encode", "wmi_decode_greedy", "wmi_decode_logits",
     "wmi_decode_beam", "wmi_full", "wmi_stage_pcm", "wmi_run_staged", "wmi_run_staged_beam", "wmi_get_tokens", "wmi_get_timings", "wmi_sync",
     "wmi_get_mel", "wmi_get_encoder_out", "wmi_get_cross_kv", "wmi_bench_kernel", "wmi_selftest",
@@ -112,6 +113,9 @@ def lib():
         L.wmi_get_special_tokens.argtypes = [vp, C.POINTER(SpecialTokens)]
         L.wmi_set_audio_ctx.argtypes = [vp, C.c_int]
         L.wmi_token_to_bytes.argtypes = [vp, i32, C.c_char_p, sz, C.POINTER(sz)]
+        L.wmi_read_wav.argtypes = [C.c_char_p, vp, sz, C.POINTER(sz), C.POINTER(i32), C.POINTER(i32)]
+        L.wmi_pcm16_to_f32.argtypes = [vp, sz, vp]
+        L.wmi_tokens_to_text.argtypes = [vp, vp, C.c_int, C.c_char_p, sz, C.POINTER(sz)]
         L.wmi_pcm_to_mel.argtypes = [vp, vp, sz]
         L.wmi_pcm_to_mel_batch.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(sz)]
         L.wmi_stage_pcm.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(sz)]
@@ -155,6 +159,25 @@ def convert_integer_to_float_audio(samples) -> np.ndarray:
 
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
+
+
+def read_wav(path: str):
+    """hound::WavReader::open + samples::<i16>() (main.rs:2067-2068) through
+    the C ABI: (int16 samples interleaved, sample_rate, channels)."""
+    L = lib()
+    n, sr, ch = C.c_size_t(), C.c_int32(), C.c_int32()
+    _raise(L.wmi_read_wav(os.fsencode(path), None, 0, C.byref(n), C.byref(sr), C.byref(ch)))
+    out = np.zeros(n.value, np.int16)
+    _raise(L.wmi_read_wav(os.fsencode(path), _ptr(out), out.size, C.byref(n), C.byref(sr), C.byref(ch)))
+    return out, sr.value, ch.value
+
+
+def pcm16_to_f32(s16) -> np.ndarray:
+    """convert_integer_to_float_audio (main.rs:1673-1679) through the C ABI."""
+    s16 = np.ascontiguousarray(s16, dtype=np.int16)
+    out = np.zeros(s16.size, np.float32)
+    _raise(lib().wmi_pcm16_to_f32(_ptr(s16), s16.size, _ptr(out)))
+    return out
 
 
 class WhisperContext:
@@ -211,6 +234,17 @@ class WhisperContext:
         n = C.c_size_t()
         buf = C.create_string_buffer(512)
         _raise(lib().wmi_token_to_bytes(self._h, tid, buf, 512, C.byref(n)), self._h)
+        return buf.raw[:n.value]
+
+    def tokens_to_text(self, ids) -> bytes:
+        """Text bytes of the text tokens of ids (specials / timestamps skipped)."""
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        n = C.c_size_t()
+        rc = lib().wmi_tokens_to_text(self._h, _ptr(ids), ids.size, None, 0, C.byref(n))
+        if rc not in (WMI_OK, NotEnoughSpace.code):
+            _raise(rc, self._h)
+        buf = C.create_string_buffer(max(1, n.value))
+        _raise(lib().wmi_tokens_to_text(self._h, _ptr(ids), ids.size, buf, n.value, C.byref(n)), self._h)
         return buf.raw[:n.value]
 
     # --- pipeline ---------------------------------------------------------
