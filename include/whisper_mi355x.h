@@ -157,6 +157,37 @@ int wmi_decode_beam(wmi_context *ctx, int beam_size, int max_tokens, int suppres
 int wmi_full(wmi_context *ctx, const float *pcm, size_t n_samples, int max_tokens,
              int32_t *tokens, int32_t *n_tokens);
 
+/* ---- timestamps, segments, long audio ---------- */
+
+/* WhisperTokenData (main.rs:317-331) as sampled: id, tid = most probable
+ * timestamp token, p = P(id), pt = P(tid) / (sum of timestamp
+ * probabilities + 1e-10), ptsum = that sum.  Token-level t0 / t1 are not
+ * computed (-1) and vlen is 0, as in whisper.cpp-1.0.3 by default. */
+typedef struct wmi_token_data {
+    int32_t id, tid;
+    float p, pt, ptsum;
+    int64_t t0, t1;
+    float vlen;
+} wmi_token_data;
+
+/* One timestamp-decoding window of the encoded clip 0 after `prompt`
+ * (whisper.cpp-1.0.3 sampling: the first token is the most probable
+ * timestamp > beg; then a timestamp whenever the timestamp probabilities sum
+ * above the most probable text token, else the most probable token other
+ * than sot / solm / not).  Stops after EOT or max_tokens; out[max_tokens]. */
+int wmi_decode_timestamps(wmi_context *ctx, const int32_t *prompt, int n_prompt, int max_tokens,
+                          wmi_token_data *out, int32_t *n_out);
+/* whisper_full with timestamps over audio of any length: 30 s windows
+ * (2 * n_audio_ctx mel frames) advanced by the last timestamp (mel_offset,
+ * main.rs:1822-1823), earlier text as prompt context; fills the context's
+ * segment list (WhisperSegment, main.rs:599-604; result_all, main.rs:353).
+ * max_tokens caps the tokens per window (<= n_text_ctx / 2 - 4). */
+int wmi_transcribe(wmi_context *ctx, const float *pcm, size_t n_samples, int max_tokens, int32_t *n_segments);
+/* Segment i of the last transcribe: [t0, t1) in 10 ms units, text bytes. */
+int wmi_get_segment(const wmi_context *ctx, int i, int64_t *t0, int64_t *t1, char *text, size_t cap, size_t *len);
+/* Its tokens (text and timestamp tokens of the segment). */
+int wmi_get_segment_tokens(const wmi_context *ctx, int i, wmi_token_data *out, size_t cap, int32_t *n);
+
 /* ---- device-resident benchmark path --------------------------------- */
 
 /* Upload n_clips PCM clips to HBM once (untimed). */

@@ -166,3 +166,116 @@ class OracleModel:
         if rc:
             raise OracleError(rc, "decode_beam")
         return toks[:n.value], score.value, gap.value
+
+
+# ---------------------------------------------------------------------------
+# Timestamp decoding and whisper_full windows.  Neither
+# exists in the reference (it declares WhisperTokenData / WhisperSegment,
+# main.rs:317-331, 599-604, and exp_n_audio_ctx / mel_offset windowing,
+# main.rs:362, 1822-1823, but no loop); the semantics restated here are
+# whisper.cpp-1.0.3's whisper_sample_timestamp / whisper_sample_best /
+# whisper_full, which the reference's structs follow.  Parity unpinned beyond
+# this restatement.  float64 softmax over the f32 logits.
+# ---------------------------------------------------------------------------
+def ts_sample(logits, special, first: bool):
+    """One sampled token: (record dict, decision margin).  margin = the
+    smaller of the top-2 logit gap in the chosen candidate set and the
+    relative gap of the timestamp-vs-text test (0 for the forced first one)."""
+    l32 = np.asarray(logits, np.float32)
+    l = l32.astype(np.float64)
+    mx = float(l32.max())
+    e = np.exp(l - mx)
+    Z = e.sum()
+    beg = special["beg"]
+    ts = e[beg:].sum() / Z
+    id_ts = beg + int(np.argmax(l32[beg:]))
+    id_tx = int(np.argmax(l32[:beg]))
+    p_tx = e[id_tx] / Z
+    if first:
+        cand = np.arange(beg + 1, l.size)
+        dec_margin = np.inf
+    elif ts > p_tx:
+        cand = np.arange(beg, l.size)
+        dec_margin = abs(ts - p_tx) / max(ts, p_tx)
+    else:
+        mask = np.ones(l.size, bool)
+        mask[[special["sot"], special["solm"], special["not"]]] = False
+        cand = np.nonzero(mask)[0]
+        dec_margin = abs(ts - p_tx) / max(ts, p_tx)
+    vals = l32[cand]
+    k = int(np.argmax(vals))
+    tid = int(cand[k])
+    srt = np.sort(vals)
+    gap = float(srt[-1] - srt[-2]) if srt.size > 1 else np.inf
+    rec = {"id": tid, "tid": id_ts, "p": e[tid] / Z, "pt": (e[id_ts] / Z) / (ts + 1e-10), "ptsum": ts}
+    return rec, min(gap, dec_margin)
+
+
+def ts_window_ref(om, ck, cv, prompt, max_tokens, n_threads=8):
+    """One window (wmi_decode_timestamps): records and the smallest margin.
+    Teacher-forced logits of prompt + tokens so far at every step."""
+    toks, recs, margin = list(prompt), [], np.inf
+    for t in range(max_tokens):
+        lg = om.decode_logits(ck, cv, np.array(toks, np.int32), n_threads=n_threads)[-1]
+        r, m = ts_sample(lg, om.special, t == 0)
+        recs.append(r)
+        margin = min(margin, m)
+        toks.append(r["id"])
+        if r["id"] == om.special["eot"]:
+            break
+    return recs, margin
+
+
+def transcribe_ref(om, pcm, n_ctx, max_tokens, token_text, n_threads=8):
+    """whisper_full restated (wmi_api.cpp run_transcribe): segments
+    [{t0, t1, text, ids}] and the smallest sampling margin met."""
+    sp, hp = om.special, om.hp
+    mel = om.mel(pcm, n_threads=4)
+    n_len = mel.shape[1]
+    window, beg, eot = 2 * n_ctx, sp["beg"], sp["eot"]
+    n_max = min(max_tokens, hp["n_text_ctx"] // 2 - 4)
+    init = [sp["sot"]] + ([sp["sot"] + 1, sp["transcribe"]] if sp["multilingual"] else [])
+    past, segs, margin, seek = [], [], np.inf, 0
+    while seek < n_len:
+        _, ck, cv = om.encode(mel, n_ctx=n_ctx, mel_offset=seek, n_threads=n_threads)
+        prompt = ([sp["prev"]] + past[-(hp["n_text_ctx"] // 2 - 1):] if past else []) + init
+        toks, m = ts_window_ref(om, ck, cv, prompt, n_max, n_threads)
+        margin = min(margin, m)
+        seek_delta, result_len, failed, ended = window, 0, False, False
+        for i, t in enumerate(toks):
+            if t["id"] > beg:
+                seek_delta, result_len = 2 * (t["id"] - beg), i + 1
+            if t["id"] == eot:
+                ended = True
+                if result_len == 0:
+                    if seek + seek_delta + 100 >= n_len:
+                        result_len = i + 1
+                    else:
+                        failed = True
+                break
+        if not ended and (result_len == 0 or seek_delta < window // 2):
+            failed = True
+        if failed:
+            seek += 100
+            continue
+        toks = toks[:result_len]
+        past += [t["id"] for t in toks]
+        if toks:
+            i0, t0, text, i = 0, seek + 2 * (toks[0]["tid"] - beg), b"", 0
+            while i < len(toks):
+                if toks[i]["id"] < eot:
+                    text += token_text(toks[i]["id"])
+                if toks[i]["id"] > beg:
+                    t1 = seek + 2 * (toks[i]["tid"] - beg)
+                    if text:
+                        segs.append({"t0": t0, "t1": t1, "text": text, "ids": [t["id"] for t in toks[i0:i + 1]]})
+                    text = b""
+                    while i < len(toks) and toks[i]["id"] > beg:
+                        i += 1
+                    i -= 1
+                    t0, i0 = t1, i + 1
+                i += 1
+            if text:
+                segs.append({"t0": t0, "t1": seek + seek_delta, "text": text, "ids": [t["id"] for t in toks[i0:]]})
+        seek += seek_delta
+    return segs, margin

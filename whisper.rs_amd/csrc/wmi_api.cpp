@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <string>
@@ -216,6 +217,13 @@ struct wmi_context {
     std::vector<int32_t> kvsrc_init;
     int beam_k = 0;             // > 0 while enqueueing a beam-search step
     int beam_max_tokens = 0;
+    // timestamp decoding (wmi_transcribe / wmi_decode_timestamps)
+    bool ts_mode = false;       // enqueueing steps with the timestamp sampler
+    int32_t *dts_tok = nullptr; // [8] token the sampler chose for the next step
+    TsRec *dts_rec = nullptr;   // [n_text_ctx] per generated token
+    struct Segment { int64_t t0, t1; int first, count; std::string text; };
+    std::vector<Segment> segments;      // result_all (main.rs:353) of the last transcribe
+    std::vector<TsRec> seg_tokens;      // their tokens, in order
     uint32_t *derr = nullptr;
     size_t sync_bytes = 0;
     int s_stride = 0, n_chunks_max = 0;
@@ -1143,6 +1151,9 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
             if (beam) {
                 g.tokens_out = nullptr;
                 g.beam_tok = ctx->dbstate->tok;
+            } else if (ctx->ts_mode) {
+                g.tokens_out = nullptr;
+                g.beam_tok = ctx->dts_tok;
             }
         }
         g.trace = tslot(ctx, "qkv", l);
@@ -1221,8 +1232,15 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     g.st_advance = ctx->dstate;
     g.trace = tslot(ctx, "logits", 0);
     g.phase = pslot(ctx, 5, "logits");
-    if (beam) g.amax = nullptr;
+    if (beam || ctx->ts_mode) g.amax = nullptr;
     HIPCHK(ctx, launch_dec_gemv(s, DEC_LOGITS, g));
+    if (ctx->ts_mode) {
+        TsArgs ta{};
+        ta.logits = ctx->dlogits; ta.V = hp.n_vocab; ta.beg = ctx->sp.beg; ta.eot = ctx->sp.eot; ta.sot = ctx->sp.sot;
+        ta.solm = ctx->sp.solm; ta.not_ = ctx->sp.not_; ta.feed_len = feed_len; ta.max_rec = hp.n_text_ctx;
+        ta.st = ctx->dstate; ta.tok_out = ctx->dts_tok; ta.rec = ctx->dts_rec;
+        HIPCHK(ctx, launch_ts_sample(s, ta));
+    }
     if (beam) {
         BeamArgs ba{};
         ba.logits = ctx->dlogits; ba.V = hp.n_vocab; ba.K = ctx->beam_k; ba.suppress_id = suppress_eot ? ctx->sp.eot : -1;
@@ -1282,9 +1300,9 @@ int run_dec_steps(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride
             continue;
         }
         char key[192];
-        snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%p/%p/%d/%d/%d", b0, B, feed_len, feed_stride, suppress_eot,
+        snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%p/%p/%d/%d/%d/%d", b0, B, feed_len, feed_stride, suppress_eot,
                  out_stride, ctx->enc_T, ctx->enc_clips, (void *)ctx->dfeed, (void *)ctx->dtokens, ctx->beam_k,
-                 ctx->beam_max_tokens, mk);
+                 ctx->beam_max_tokens, mk, (int)ctx->ts_mode);
         auto it = ctx->graphs.find(key);
         if (it == ctx->graphs.end()) {
             if (ctx->graphs.size() >= 32) ctx->clear_graphs();
@@ -1395,6 +1413,135 @@ bool valid(const wmi_context *ctx) { return ctx != nullptr && ctx->d_model != nu
 
 // beam search (config C5) of every encoded clip, one clip (K decoder rows) at
 // a time; per-clip best hypothesis (tokens, score) on the host
+// Timestamp decoding of encoded clip `clip` after `prompt` (whisper.cpp-1.0.3
+// whisper_full inner loop): up to max_tokens sampled
+// with the device timestamp sampler (k_ts_sample), stopping after EOT.
+int run_ts_window(wmi_context *ctx, int clip, const std::vector<int32_t> &prompt, int max_tokens,
+                  std::vector<TsRec> *out) {
+    const wmi_hparams &hp = ctx->hp;
+    const int np = (int)prompt.size();
+    if (ctx->enc_T <= 0) return set_err(ctx, WMI_E_INVALID_ARG, "decode before encode");
+    if (np < 1 || max_tokens < 1 || np + max_tokens > hp.n_text_ctx)
+        return set_err(ctx, WMI_E_INVALID_ARG, "prompt %d + max_tokens %d exceed n_text_ctx %d", np, max_tokens,
+                       hp.n_text_ctx);
+    if (!ctx->dts_tok) {
+        HIPCHK(ctx, hipMalloc(&ctx->dts_tok, 64));
+        HIPCHK(ctx, hipMalloc(&ctx->dts_rec, (size_t)hp.n_text_ctx * sizeof(TsRec)));
+        ctx->clear_graphs();
+    }
+    int rc = ensure_decode_buffers(ctx, np, 1);
+    if (rc) return rc;
+    HIPCHK(ctx, hipMemcpyAsync(ctx->dfeed, prompt.data(), (size_t)np * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * AMAX_SHARDS * 8, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->dsync, 0, ctx->sync_bytes, ctx->stream));
+    ctx->ts_mode = true;
+    struct Reset { wmi_context *c; ~Reset() { c->ts_mode = false; } } reset{ctx};
+    const int total = np + max_tokens - 1;
+    std::vector<TsRec> rec((size_t)max_tokens);
+    int n_out = max_tokens;
+    for (int done = 0; done < total;) {
+        const int chunk = std::min(16, total - done);
+        rc = run_dec_steps(ctx, clip, 1, np, np, 0, 1, done, chunk);
+        if (rc) return rc;
+        done += chunk;
+        const int have = done - np + 1;  // records written so far
+        if (have <= 0) continue;
+        HIPCHK(ctx, hipMemcpyAsync(rec.data(), ctx->dts_rec, (size_t)have * sizeof(TsRec), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        bool eot = false;
+        for (int i = 0; i < have && !eot; ++i)
+            if (rec[i].id == ctx->sp.eot) { n_out = i + 1; eot = true; }
+        if (eot) break;
+    }
+    uint32_t err = 0;
+    HIPCHK(ctx, hipMemcpy(&err, ctx->derr, 4, hipMemcpyDeviceToHost));
+    if (err) return dec_err(ctx, err);
+    out->assign(rec.begin(), rec.begin() + n_out);
+    return WMI_OK;
+}
+
+// whisper_full (whisper.cpp-1.0.3, the loop the reference's WhisperSegment /
+// WhisperTokenData / prompt_past fields belong to, main.rs:317-331, 353-362,
+// 599-604): windows of 2 * n_ctx mel frames from `seek`, prompt = [prev] +
+// the last n_text_ctx/2 - 1 tokens of earlier windows + [sot (, lang,
+// transcribe)], timestamp sampling; a window's tokens up to its last
+// timestamp form segments [t0, t1) in 10 ms units; seek advances to the
+// last timestamp, or past the window; a window without a usable timestamp is
+// skipped by 100 frames.  Restated op for op in oracle/pyoracle.py transcribe_ref.
+int run_transcribe(wmi_context *ctx, int max_tokens) {
+    const wmi_hparams &hp = ctx->hp;
+    const int64_t n_len = ctx->n_len_host[0];
+    const int n_ctx = ctx->cur_ctx > 0 ? ctx->cur_ctx : hp.n_audio_ctx;
+    const int window = 2 * n_ctx, beg = ctx->sp.beg, eot = ctx->sp.eot;
+    const int n_max = std::min(max_tokens, hp.n_text_ctx / 2 - 4);
+    std::vector<int32_t> init{ctx->sp.sot};
+    if (ctx->sp.is_multilingual) { init.push_back(ctx->sp.sot + 1); init.push_back(ctx->sp.transcribe); }
+    std::vector<int32_t> past;
+    ctx->segments.clear();
+    ctx->seg_tokens.clear();
+    for (int64_t seek = 0; seek < n_len;) {
+        int rc = run_encode(ctx, (int)seek);
+        if (rc) return rc;
+        std::vector<int32_t> prompt;
+        if (!past.empty()) {
+            prompt.push_back(ctx->sp.prev);
+            const size_t keep = std::min(past.size(), (size_t)(hp.n_text_ctx / 2 - 1));
+            prompt.insert(prompt.end(), past.end() - keep, past.end());
+        }
+        prompt.insert(prompt.end(), init.begin(), init.end());
+        std::vector<TsRec> toks;
+        rc = run_ts_window(ctx, 0, prompt, n_max, &toks);
+        if (rc) return rc;
+        int64_t seek_delta = window;
+        int result_len = 0;
+        bool failed = false, ended = false;
+        for (int i = 0; i < (int)toks.size(); ++i) {
+            if (toks[i].id > beg) { seek_delta = 2 * (int64_t)(toks[i].id - beg); result_len = i + 1; }
+            if (toks[i].id == eot) {
+                ended = true;
+                if (result_len == 0) {
+                    if (seek + seek_delta + 100 >= n_len) result_len = i + 1;
+                    else failed = true;
+                }
+                break;
+            }
+        }
+        if (!ended && (result_len == 0 || seek_delta < window / 2)) failed = true;  // stuck: no end in n_max tokens
+        if (failed) { seek += 100; continue; }
+        toks.resize(result_len);
+        for (const TsRec &t : toks) past.push_back(t.id);
+        if (!toks.empty()) {
+            int i0 = 0;
+            int64_t t0 = seek + 2 * (int64_t)(toks.front().tid - beg);
+            std::string text;
+            for (int i = 0; i < (int)toks.size(); ++i) {
+                if (toks[i].id < eot) text += ctx->vocab[toks[i].id];
+                if (toks[i].id > beg) {
+                    const int64_t t1 = seek + 2 * (int64_t)(toks[i].tid - beg);
+                    if (!text.empty()) {
+                        ctx->segments.push_back({t0, t1, (int)ctx->seg_tokens.size(), i - i0 + 1, text});
+                        ctx->seg_tokens.insert(ctx->seg_tokens.end(), toks.begin() + i0, toks.begin() + i + 1);
+                    }
+                    text.clear();
+                    while (i < (int)toks.size() && toks[i].id > beg) ++i;
+                    --i;
+                    t0 = t1;
+                    i0 = i + 1;
+                }
+            }
+            if (!text.empty()) {
+                ctx->segments.push_back({t0, seek + seek_delta, (int)ctx->seg_tokens.size(),
+                                         (int)toks.size() - i0, text});
+                ctx->seg_tokens.insert(ctx->seg_tokens.end(), toks.begin() + i0, toks.end());
+            }
+        }
+        seek += seek_delta;
+    }
+    return WMI_OK;
+}
+
 int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_stop,
              std::vector<std::vector<int32_t>> *out_tokens, std::vector<double> *out_scores) {
     const int Bt = ctx->enc_clips;
@@ -1686,6 +1833,58 @@ int wmi_tokens_to_text(const wmi_context *ctx, const int32_t *ids, int n, char *
     *len = s.size();
     if (!buf || cap < s.size()) return WMI_E_NO_SPACE;
     memcpy(buf, s.data(), s.size());
+    return WMI_OK;
+}
+
+static void to_token_data(const TsRec &r, wmi_token_data *d) {
+    d->id = r.id; d->tid = r.tid; d->p = r.p; d->pt = r.pt; d->ptsum = r.ptsum;
+    d->t0 = -1; d->t1 = -1; d->vlen = 0.0f;  // token-level timestamps are not computed (as whisper.cpp-1.0.3 by default)
+}
+
+int wmi_decode_timestamps(wmi_context *ctx, const int32_t *prompt, int n_prompt, int max_tokens, wmi_token_data *out,
+                          int32_t *n_out) {
+    if (!valid(ctx) || !prompt || n_prompt < 1 || !out || !n_out) return WMI_E_INVALID_ARG;
+    for (int i = 0; i < n_prompt; ++i)
+        if (prompt[i] < 0 || prompt[i] >= ctx->hp.n_vocab) return set_err(ctx, WMI_E_INVALID_ARG, "token id %d", prompt[i]);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    std::vector<TsRec> rec;
+    int rc = run_ts_window(ctx, 0, std::vector<int32_t>(prompt, prompt + n_prompt), max_tokens, &rec);
+    if (rc) return rc;
+    for (size_t i = 0; i < rec.size(); ++i) to_token_data(rec[i], out + i);
+    *n_out = (int32_t)rec.size();
+    return WMI_OK;
+}
+
+int wmi_transcribe(wmi_context *ctx, const float *pcm, size_t n_samples, int max_tokens, int32_t *n_segments) {
+    if (!valid(ctx) || (!pcm && n_samples) || max_tokens < 1 || !n_segments) return WMI_E_INVALID_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const float *pp[1] = {pcm};
+    const size_t nn[1] = {n_samples};
+    int rc = wmi_pcm_to_mel_batch(ctx, 1, pp, nn);
+    if (rc) return rc;
+    rc = run_transcribe(ctx, max_tokens);
+    if (rc) return rc;
+    *n_segments = (int32_t)ctx->segments.size();
+    return WMI_OK;
+}
+
+int wmi_get_segment(const wmi_context *ctx, int i, int64_t *t0, int64_t *t1, char *text, size_t cap, size_t *len) {
+    if (!ctx || i < 0 || i >= (int)ctx->segments.size() || !len) return WMI_E_INVALID_ARG;
+    const auto &sg = ctx->segments[i];
+    if (t0) *t0 = sg.t0;
+    if (t1) *t1 = sg.t1;
+    *len = sg.text.size();
+    if (!text || cap < sg.text.size()) return WMI_E_NO_SPACE;
+    memcpy(text, sg.text.data(), sg.text.size());
+    return WMI_OK;
+}
+
+int wmi_get_segment_tokens(const wmi_context *ctx, int i, wmi_token_data *out, size_t cap, int32_t *n) {
+    if (!ctx || i < 0 || i >= (int)ctx->segments.size() || !n) return WMI_E_INVALID_ARG;
+    const auto &sg = ctx->segments[i];
+    *n = sg.count;
+    if (!out || cap < (size_t)sg.count) return WMI_E_NO_SPACE;
+    for (int k = 0; k < sg.count; ++k) to_token_data(ctx->seg_tokens[sg.first + k], out + k);
     return WMI_OK;
 }
 

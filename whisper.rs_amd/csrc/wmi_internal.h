@@ -215,6 +215,22 @@ struct BeamArgs {
 };
 hipError_t launch_beam_step(hipStream_t s, const BeamArgs &a);
 
+// ---- timestamp sampling (whisper.cpp-1.0.3 whisper_sample_best /
+// whisper_sample_timestamp semantics, restated in oracle/pyoracle.py) --------
+struct TsRec {               // WhisperTokenData (main.rs:317-331) as sampled
+    int32_t id, tid;
+    float p, pt, ptsum;
+    int32_t pad;
+};
+struct TsArgs {
+    const float *logits;     // [V] (row 0)
+    int V, beg, eot, sot, solm, not_, feed_len, max_rec;
+    const DecState *st;      // pos already advanced by the logits launch
+    int32_t *tok_out;        // token fed at the next step
+    TsRec *rec;              // [max_rec], record t = pos - feed_len
+};
+hipError_t launch_ts_sample(hipStream_t s, const TsArgs &a);
+
 struct DecEmbedArgs {
     const uint16_t *te;      // [V][n]
     const float *pe;         // [n_text_ctx][n]

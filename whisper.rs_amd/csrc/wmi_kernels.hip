@@ -2154,6 +2154,98 @@ hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
     return hipGetLastError();
 }
 
+// ---- timestamp sampling: one workgroup over the vocabulary -----------------
+// p_i = exp(l_i - lse) in double.  First generated token: argmax over the
+// timestamp ids > beg (whisper_sample_timestamp).  Later: if the summed
+// timestamp probability (ids >= beg) exceeds the largest text probability
+// (ids < beg) the argmax over ids >= beg, else the argmax over every id but
+// sot / solm / not (whisper_sample_best); ties to the lowest id.  Records
+// {id, tid = argmax over ids >= beg, p, pt = max_ts / (sum_ts + 1e-10), ptsum}.
+__device__ __forceinline__ unsigned long long ts_key(float v, int id) {
+    return ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)id);
+}
+__device__ __forceinline__ int ts_key_id(unsigned long long k) { return (int)(0xffffffffu - (uint32_t)(k & 0xffffffffu)); }
+
+__global__ __launch_bounds__(1024) void k_ts_sample(TsArgs a) {
+    const int pos = a.st->pos;
+    if (pos < a.feed_len) return;  // still feeding the prompt
+    const int t = pos - a.feed_len;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    __shared__ float smax[16];
+    __shared__ double ssum[16], sts[16];
+    __shared__ unsigned long long sk[3][16];
+    float mx = -INFINITY;
+    unsigned long long k_all = 0, k_ts = 0, k_ts1 = 0, k_tx = 0;
+    for (int i = tid; i < a.V; i += 1024) {
+        const float l = a.logits[i];
+        mx = fmaxf(mx, l);
+        const unsigned long long k = ts_key(l, i);
+        if (i >= a.beg) k_ts = k > k_ts ? k : k_ts;
+        else k_tx = k > k_tx ? k : k_tx;
+        if (i > a.beg) k_ts1 = k > k_ts1 ? k : k_ts1;
+        if (i != a.sot && i != a.solm && i != a.not_) k_all = k > k_all ? k : k_all;
+    }
+    mx = wave_max(mx);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        unsigned long long x;
+        x = __shfl_xor(k_all, o); k_all = x > k_all ? x : k_all;
+        x = __shfl_xor(k_ts, o); k_ts = x > k_ts ? x : k_ts;
+        x = __shfl_xor(k_ts1, o); k_ts1 = x > k_ts1 ? x : k_ts1;
+        x = __shfl_xor(k_tx, o); k_tx = x > k_tx ? x : k_tx;
+    }
+    __shared__ unsigned long long stx[16];
+    if (lane == 0) { smax[w] = mx; sk[0][w] = k_all; sk[1][w] = k_ts; sk[2][w] = k_ts1; stx[w] = k_tx; }
+    __syncthreads();
+    mx = smax[0];
+    k_all = sk[0][0]; k_ts = sk[1][0]; k_ts1 = sk[2][0]; k_tx = stx[0];
+    for (int i = 1; i < 16; ++i) {
+        mx = fmaxf(mx, smax[i]);
+        k_all = sk[0][i] > k_all ? sk[0][i] : k_all;
+        k_ts = sk[1][i] > k_ts ? sk[1][i] : k_ts;
+        k_ts1 = sk[2][i] > k_ts1 ? sk[2][i] : k_ts1;
+        k_tx = stx[i] > k_tx ? stx[i] : k_tx;
+    }
+    double s = 0.0, st = 0.0;
+    for (int i = tid; i < a.V; i += 1024) {
+        const double e = exp((double)a.logits[i] - (double)mx);
+        s += e;
+        if (i >= a.beg) st += e;
+    }
+    s = wave_sum(s);
+    st = wave_sum(st);
+    if (lane == 0) { ssum[w] = s; sts[w] = st; }
+    __syncthreads();
+    if (tid != 0) return;
+    double Z = 0.0, TS = 0.0;
+    for (int i = 0; i < 16; ++i) { Z += ssum[i]; TS += sts[i]; }
+    const int id_ts = ts_key_id(k_ts), id_tx = ts_key_id(k_tx);
+    const double p_maxts = exp((double)a.logits[id_ts] - (double)mx) / Z;
+    const double p_maxtx = exp((double)a.logits[id_tx] - (double)mx) / Z;
+    const double sum_ts = TS / Z;
+    int id;
+    if (t == 0) id = ts_key_id(k_ts1);
+    else if (sum_ts > p_maxtx) id = id_ts;
+    else id = ts_key_id(k_all);
+    a.tok_out[0] = id;
+    if (t < a.max_rec) {
+        TsRec r;
+        r.id = id;
+        r.tid = id_ts;
+        r.p = (float)(exp((double)a.logits[id] - (double)mx) / Z);
+        r.pt = (float)(p_maxts / (sum_ts + 1e-10));
+        r.ptsum = (float)sum_ts;
+        r.pad = 0;
+        a.rec[t] = r;
+    }
+}
+
+hipError_t launch_ts_sample(hipStream_t s, const TsArgs &a) {
+    if (a.V < a.beg + 2) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ts_sample, dim3(1), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
 // records the token produced by the last step (the in-step record happens in
 // the first layer's QKV prologue): one wave per clip
 __global__ __launch_bounds__(64) void k_dec_record(DecEmbedArgs a) {

@@ -61,6 +61,7 @@ EXPORTS = (
     "wmi_init_from_file", "wmi_free", "wmi_strerror", "wmi_last_error", "wmi_last_error_global",
     "wmi_get_hparams", "wmi_get_special_tokens", "wmi_set_audio_ctx", "wmi_token_to_bytes",
     "wmi_read_wav", "wmi_pcm16_to_f32", "wmi_tokens_to_text",
+    "wmi_decode_timestamps", "wmi_transcribe", "wmi_get_segment", "wmi_get_segment_tokens",
     "wmi_pcm_to_mel", "wmi_pcm_to_mel_batch", "wmi_encode", "wmi_decode_greedy", "wmi_decode_logits",
     "wmi_decode_beam", "wmi_full", "wmi_stage_pcm", "wmi_run_staged", "wmi_run_staged_beam", "wmi_get_tokens", "wmi_get_timings", "wmi_sync",
     "wmi_get_mel", "wmi_get_encoder_out", "wmi_get_cross_kv", "wmi_bench_kernel", "wmi_selftest",
@@ -84,6 +85,15 @@ class SpecialTokens(C.Structure):
 class KernelBench(C.Structure):
     _fields_ = [("avg_us", C.c_float), ("alg_bytes", C.c_double), ("alg_flops", C.c_double),
                 ("name", C.c_char * 48)]
+
+
+class TokenData(C.Structure):
+    """WhisperTokenData (main.rs:317-331)."""
+    _fields_ = [("id", C.c_int32), ("tid", C.c_int32), ("p", C.c_float), ("pt", C.c_float), ("ptsum", C.c_float),
+                ("t0", C.c_int64), ("t1", C.c_int64), ("vlen", C.c_float)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
 
 
 class Timings(C.Structure):
@@ -116,6 +126,11 @@ def lib():
         L.wmi_read_wav.argtypes = [C.c_char_p, vp, sz, C.POINTER(sz), C.POINTER(i32), C.POINTER(i32)]
         L.wmi_pcm16_to_f32.argtypes = [vp, sz, vp]
         L.wmi_tokens_to_text.argtypes = [vp, vp, C.c_int, C.c_char_p, sz, C.POINTER(sz)]
+        L.wmi_decode_timestamps.argtypes = [vp, vp, C.c_int, C.c_int, vp, C.POINTER(i32)]
+        L.wmi_transcribe.argtypes = [vp, vp, sz, C.c_int, C.POINTER(i32)]
+        L.wmi_get_segment.argtypes = [vp, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_char_p, sz,
+                                      C.POINTER(sz)]
+        L.wmi_get_segment_tokens.argtypes = [vp, C.c_int, vp, sz, C.POINTER(i32)]
         L.wmi_pcm_to_mel.argtypes = [vp, vp, sz]
         L.wmi_pcm_to_mel_batch.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(sz)]
         L.wmi_stage_pcm.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(sz)]
@@ -246,6 +261,35 @@ class WhisperContext:
         buf = C.create_string_buffer(max(1, n.value))
         _raise(lib().wmi_tokens_to_text(self._h, _ptr(ids), ids.size, buf, n.value, C.byref(n)), self._h)
         return buf.raw[:n.value]
+
+    # --- timestamps / segments (whisper.cpp-1.0.3 whisper_full) ----------
+    def decode_timestamps(self, prompt, max_tokens: int):
+        """One timestamp-decoding window of encoded clip 0: [WhisperTokenData dict]."""
+        prompt = np.ascontiguousarray(prompt, dtype=np.int32)
+        out = (TokenData * max_tokens)()
+        n = C.c_int32()
+        _raise(lib().wmi_decode_timestamps(self._h, _ptr(prompt), prompt.size, max_tokens, out, C.byref(n)), self._h)
+        return [out[i].as_dict() for i in range(n.value)]
+
+    def transcribe(self, pcm, max_tokens: int = 220):
+        """whisper_full with timestamps: [{"t0", "t1", "text", "tokens"}] (t in 10 ms)."""
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        ns = C.c_int32()
+        _raise(lib().wmi_transcribe(self._h, _ptr(pcm), pcm.size, max_tokens, C.byref(ns)), self._h)
+        self.n_clips = 1
+        segs = []
+        for i in range(ns.value):
+            t0, t1, ln = C.c_int64(), C.c_int64(), C.c_size_t()
+            lib().wmi_get_segment(self._h, i, C.byref(t0), C.byref(t1), None, 0, C.byref(ln))
+            buf = C.create_string_buffer(max(1, ln.value))
+            _raise(lib().wmi_get_segment(self._h, i, C.byref(t0), C.byref(t1), buf, ln.value, C.byref(ln)), self._h)
+            nt = C.c_int32()
+            lib().wmi_get_segment_tokens(self._h, i, None, 0, C.byref(nt))
+            toks = (TokenData * max(1, nt.value))()
+            _raise(lib().wmi_get_segment_tokens(self._h, i, toks, nt.value, C.byref(nt)), self._h)
+            segs.append({"t0": t0.value, "t1": t1.value, "text": buf.raw[:ln.value],
+                         "tokens": [toks[k].as_dict() for k in range(nt.value)]})
+        return segs
 
     # --- pipeline ---------------------------------------------------------
     def pcm_to_mel_batch(self, clips) -> None:
