@@ -4,7 +4,17 @@ through the C ABI, against the restatement in oracle/pyoracle.py
 whisper_full: parity unpinned beyond that restatement — the reference declares
 WhisperTokenData / WhisperSegment, main.rs:317-331, 599-604, but no loop).
 Ids must match exactly up to the first near-tie the oracle meets (a sampling
-decision whose margin is below TIE, which f32 reordering may flip)."""
+decision whose margin is below TIE, which f32 reordering may flip).
+
+Random weights make the decoder settle on one token forever (all timestamps, so
+no segment has text).  `segmenting_model` therefore shapes the micro model's
+decoder embeddings so that windows alternate <|ts|> text <|ts|> text ...: a
+unit direction u is added to the token embeddings of timestamps 32..63 and,
+with alternating sign, to the decoder positional embedding, so even steps pick
+a timestamp (seek_delta 64..126 frames, several windows over 4 s) and odd steps
+a text token.  test_segmenting_model_has_segments pins that on the CPU."""
+import os
+
 import numpy as np
 import pytest
 
@@ -12,8 +22,37 @@ import pyoracle
 import synth
 from conftest import threads
 
-pytestmark = pytest.mark.gpu
 TIE = 1e-3
+
+
+def write_segmenting_model(path):
+    hp = synth.MODEL_DIMS["micro"]
+    beg = hp["n_vocab"] - 1501           # <|0.00|> of an English-only vocab
+    u = np.random.default_rng(5).standard_normal(hp["n_text_state"]).astype(np.float32)
+    u /= np.linalg.norm(u)
+
+    def hook(name, arr):
+        dt = arr.dtype
+        if name == "decoder.token_embedding.weight":
+            e = arr.astype(np.float32) * 10.0
+            j = np.arange(e.shape[0] - beg)
+            good = ((j >= 32) & (j < 64)).astype(np.float32)
+            e[beg:] = e[(j * 37) % 50000] * 0.5 + 10.0 * good[:, None] * u[None, :]
+            return e.astype(dt)
+        if name == "decoder.positional_embedding":
+            sgn = np.where(np.arange(arr.shape[0]) % 2 == 0, 60.0, -60.0).astype(np.float32)
+            return (arr.astype(np.float32) + sgn[:, None] * u[None, :]).astype(dt)
+        return arr
+    synth.write_ggml(path, "micro", tensor_hook=hook)
+
+
+@pytest.fixture(scope="module")
+def segmenting_model(model_cache):
+    path = os.path.join(model_cache, "ggml-micro-segmenting.bin")
+    if not os.path.exists(path):
+        os.makedirs(model_cache, exist_ok=True)
+        write_segmenting_model(path)          # synth writes a temp file, then renames
+    return path
 
 
 @pytest.fixture(scope="module")
@@ -24,6 +63,29 @@ def ctx(micro_model):
     c.close()
 
 
+@pytest.fixture(scope="module")
+def seg_pair(segmenting_model):
+    om = pyoracle.OracleModel(segmenting_model)
+    yield om
+    om.close()
+
+
+def token_text(i):
+    return b"<%d>" % i
+
+
+def test_segmenting_model_has_segments(seg_pair):
+    """CPU: the shaped model really exercises text segments over several
+    windows, so the GPU test below compares more than empty lists."""
+    segs, margin = pyoracle.transcribe_ref(seg_pair, synth.synth_pcm_f32(4.0, 21), 64, 10,
+                                           token_text, n_threads=threads())
+    assert margin >= TIE
+    assert len(segs) >= 8
+    assert len({s["t0"] for s in segs}) >= 3            # more than one window
+    assert all(s["text"] for s in segs)
+
+
+@pytest.mark.gpu
 def test_timestamp_window_matches_oracle(ctx, oracle_micro):
     om = oracle_micro
     checked = 0
@@ -52,6 +114,7 @@ def test_timestamp_window_matches_oracle(ctx, oracle_micro):
         pytest.skip("every seed met a near-tie")
 
 
+@pytest.mark.gpu
 def test_transcribe_windows_match_oracle(ctx, oracle_micro):
     """Several 128-frame windows (n_audio_ctx 64) over 4 s of audio: seek,
     prompt context from earlier windows, segment boundaries and texts."""
@@ -67,3 +130,27 @@ def test_transcribe_windows_match_oracle(ctx, oracle_micro):
     assert [[t["id"] for t in s["tokens"]] for s in got] == [s["ids"] for s in ref]
     for s in got:
         assert s["t0"] <= s["t1"]
+
+
+@pytest.mark.gpu
+def test_transcribe_segments_match_oracle(segmenting_model, seg_pair):
+    """Text segments over several windows: t0/t1, texts, token ids and the
+    per-token probabilities of every segment."""
+    import wmi
+    om = seg_pair
+    pcm = synth.synth_pcm_f32(4.0, 21)
+    c = wmi.WhisperContext.new(segmenting_model, 0, max_clips=1)
+    try:
+        c.set_audio_ctx(64)
+        ref, margin = pyoracle.transcribe_ref(om, pcm, 64, 10, c.token_to_str, n_threads=threads())
+        assert margin >= TIE and len(ref) >= 8
+        got = c.transcribe(pcm, max_tokens=10)
+    finally:
+        c.close()
+    assert [(s["t0"], s["t1"]) for s in got] == [(s["t0"], s["t1"]) for s in ref]
+    assert [s["text"] for s in got] == [s["text"] for s in ref]
+    assert [[t["id"] for t in s["tokens"]] for s in got] == [s["ids"] for s in ref]
+    beg = om.special["beg"]
+    for s in got:
+        ts = [t for t in s["tokens"] if t["id"] > beg]
+        assert ts and all(0.0 < t["p"] <= 1.0 for t in s["tokens"])
