@@ -1708,6 +1708,8 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (getenv("WMI_NO_FUSE")) ctx->fuse_wo = false;
     if (const char *c = getenv("WMI_ATTN_V1")) g_attn_v1 = atoi(c) == 2 ? 2 : 1;
     if (const char *c = getenv("WMI_LOGITS_CAP")) g_logits_cap = atoi(c) > 0 ? atoi(c) : g_logits_cap;
+    if (const char *c = getenv("WMI_LOGITS_G")) g_logits_g = atoi(c);
+    if (const char *c = getenv("WMI_LOGITS_CAP2")) g_logits_cap2 = atoi(c) > 0 ? atoi(c) : g_logits_cap2;
     if (const char *c = getenv("WMI_GEMV_NW")) g_gemv_nw = atoi(c) == 1 ? 1 : atoi(c) == 0 ? 0 : 4;
     if (const char *c = getenv("WMI_SELF_SPLIT")) g_self_split = atoi(c) >= 0 ? atoi(c) : g_self_split;
     if (getenv("WMI_TRACE")) {
@@ -2119,6 +2121,13 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
     uint32_t *bar_cnt = ctx->derr + 32;  // inside the 256-byte tail of the sync region
     uint32_t bar_base = 0;
     if (which >= 6 && which <= 8) HIPCHK(ctx, hipMemsetAsync(bar_cnt, 0, 4, s));
+    // 9-12: hierarchical barrier at 256 WGs, modes 0-3; 13: mode 2 at 512 WGs
+    const int hb_mode = which == 13 ? 2 : which - 9, hb_wg = which == 13 ? 512 : 256;
+    uint32_t *hb_cnt = nullptr, hb_base = 0;
+    if (which >= 9 && which <= 13) {
+        HIPCHK(ctx, hipMalloc(&hb_cnt, 4096));
+        HIPCHK(ctx, hipMemsetAsync(hb_cnt, 0, 4096, s));
+    }
     auto launch = [&]() -> int {
         if (which == 0) {
             DecGemvArgs g{};
@@ -2151,6 +2160,9 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
         } else if (which >= 6 && which <= 8) {
             HIPCHK(ctx, launch_probe_barrier(s, bar_wg, bar_rounds, bar_cnt, bar_base, ctx->derr));
             bar_base += (uint32_t)(bar_wg * bar_rounds);
+        } else if (which >= 9 && which <= 13) {
+            HIPCHK(ctx, launch_probe_barrier_h(s, hb_mode, hb_wg, bar_rounds, hb_cnt, hb_base, ctx->derr));
+            hb_base += (uint32_t)bar_rounds;
         } else {
             return set_err(ctx, WMI_E_INVALID_ARG, "unknown kernel %d", which);
         }
@@ -2168,6 +2180,7 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
     float ms = 0;
     HIPCHK(ctx, hipEventElapsedTime(&ms, ctx->ev[6], ctx->ev[7]));
     out->avg_us = ms * 1000.0f / iters;
+    if (hb_cnt) HIPCHK(ctx, hipFree(hb_cnt));
     const double nt = hp.n_text_state, V = hp.n_vocab;
     if (which == 0) {
         const double b = B < 8 ? B : 8;
@@ -2190,6 +2203,8 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
         snprintf(out->name, sizeof out->name, "k_probe_copy (1 MiB)");
     } else if (which >= 6 && which <= 8) {
         snprintf(out->name, sizeof out->name, "k_probe_barrier (%d WG x %d barriers)", bar_wg, bar_rounds);
+    } else if (which >= 9 && which <= 13) {
+        snprintf(out->name, sizeof out->name, "k_probe_barrier_h mode %d (%d WG x %d barriers)", hb_mode, hb_wg, bar_rounds);
     } else {
         const double N = hp.n_text_layer * 2.0 * nt;
         out->alg_flops = 2.0 * M * N * n;

@@ -13,6 +13,8 @@ namespace wmi {
 // ---- launch-overhead probes: 0 = empty kernel, 1 = 256 x 4 KiB copy ---------
 hipError_t launch_probe(hipStream_t s, int which, const void *src, void *dst);
 hipError_t launch_probe_barrier(hipStream_t s, int n_wg, int rounds, uint32_t *cnt, uint32_t base, uint32_t *err);
+hipError_t launch_probe_barrier_h(hipStream_t s, int mode, int n_wg, int rounds, uint32_t *cnt, uint32_t base,
+                                  uint32_t *err);
 // device exp (decoder attention) vs the host-built ggml exp table, all inputs
 hipError_t launch_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *mismatch);
 
@@ -135,6 +137,8 @@ constexpr int AMAX_SHARDS = 64;
 constexpr int DEC_ROWS = 8;  // decoder rows per step: clips (greedy) or beam hypotheses
 hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a);
 extern int g_logits_cap;
+extern int g_logits_g;
+extern int g_logits_cap2;
 extern int g_gemv_nw;
 extern int g_self_split;
 

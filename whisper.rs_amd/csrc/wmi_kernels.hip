@@ -1180,10 +1180,11 @@ __device__ __forceinline__ float keep1(float v, bool ok) { return v * (ok ? 1.0f
 
 // LayerNorm input row as float4 registers: unconditional (clamped) loads so
 // every request is in flight before the first wait
-__device__ __forceinline__ void ln_load_row(const float *x, int K, int lane, float4 (&xv)[DG_LNV]) {
+template <int L>
+__device__ __forceinline__ void ln_load_row(const float *x, int K, int lane, float4 (&xv)[L]) {
     const float4 *xr = (const float4 *)x;
 #pragma unroll
-    for (int i = 0; i < DG_LNV; ++i) {
+    for (int i = 0; i < L; ++i) {
         const int idx = lane + 64 * i;
         const bool ok = idx * 4 < K;
         xv[i] = keep4(xr[ok ? idx : 0], ok);
@@ -1191,10 +1192,11 @@ __device__ __forceinline__ void ln_load_row(const float *x, int K, int lane, flo
 }
 
 // LayerNorm gain / bias as float4 registers
-__device__ __forceinline__ void ln_load_params(const float *lw, const float *lb, int K, int lane, float4 (&gw)[DG_LNV],
-                                               float4 (&gb)[DG_LNV]) {
+template <int L>
+__device__ __forceinline__ void ln_load_params(const float *lw, const float *lb, int K, int lane, float4 (&gw)[L],
+                                               float4 (&gb)[L]) {
 #pragma unroll
-    for (int i = 0; i < DG_LNV; ++i) {
+    for (int i = 0; i < L; ++i) {
         const int e = (lane + 64 * i) * 4, ec = e < K ? e : 0;
         gw[i] = keep4(*(const float4 *)(lw + ec), e < K);
         gb[i] = keep4(*(const float4 *)(lb + ec), e < K);
@@ -1202,17 +1204,18 @@ __device__ __forceinline__ void ln_load_params(const float *lw, const float *lb,
 }
 
 // LayerNorm of one K-row held as float4 registers (ggml norm semantics)
-__device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K, const float4 (&gw)[DG_LNV],
-                                               const float4 (&gb)[DG_LNV], f16 *dst, int lane) {
+template <int L>
+__device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[L], int K, const float4 (&gw)[L],
+                                               const float4 (&gb)[L], f16 *dst, int lane) {
     double s1 = 0.0;
 #pragma unroll
-    for (int i = 0; i < DG_LNV; ++i)
+    for (int i = 0; i < L; ++i)
         if ((lane + 64 * i) * 4 < K) s1 += ((double)xv[i].x + (double)xv[i].y) + ((double)xv[i].z + (double)xv[i].w);
     s1 = wave_sum(s1);
     const double mean = s1 / K;
     double s2 = 0.0;
 #pragma unroll
-    for (int i = 0; i < DG_LNV; ++i)
+    for (int i = 0; i < L; ++i)
         if ((lane + 64 * i) * 4 < K) {
             const double d0 = (double)xv[i].x - mean, d1 = (double)xv[i].y - mean;
             const double d2 = (double)xv[i].z - mean, d3 = (double)xv[i].w - mean;
@@ -1221,7 +1224,7 @@ __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K
     s2 = wave_sum(s2);
     const float scale = (float)(1.0 / sqrt(s2 / K + (double)1e-5f));
 #pragma unroll
-    for (int i = 0; i < DG_LNV; ++i) {
+    for (int i = 0; i < L; ++i) {
         const int e = (lane + 64 * i) * 4;
         if (e < K) {
             const float xx[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
@@ -1236,9 +1239,10 @@ __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K
 }
 
 // the same with the gain / bias requested here (before the two reductions)
-__device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[DG_LNV], int K, const float *lw, const float *lb,
+template <int L>
+__device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[L], int K, const float *lw, const float *lb,
                                                f16 *dst, int lane) {
-    float4 gw[DG_LNV], gb[DG_LNV];
+    float4 gw[L], gb[L];
     ln_load_params(lw, lb, K, lane, gw, gb);
     ln_regs_to_lds(xv, K, gw, gb, dst, lane);
 }
@@ -1309,6 +1313,8 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
     // register sets: row group i + 1's weights are in flight while group i is
     // reduced and written (PIPE); the others run one row group per workgroup
     constexpr bool PIPE = EPI == DEC_LOGITS;
+    // LayerNorm row registers: the K <= 512 (NC = 4, f16) instances need 2 float4 per lane
+    constexpr int LNV = (NC == 4 && !WQ) ? 2 : DG_LNV;
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
     f16 *xs = (f16 *)smraw;  // [B][K]
     __shared__ unsigned long long amax_s[DG_MAXB];
@@ -1450,7 +1456,7 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
     };
     // LayerNorm operands of row w first: the LN below then waits for them
     // while the weight stream issued after them is still in flight
-    float4 xv0[DG_LNV], gw0[DG_LNV], gb0[DG_LNV];
+    float4 xv0[LNV], gw0[LNV], gb0[LNV];
     if (IN == 0 && w < B) {
         ln_load_row(a.x + (int64_t)w * K, K, lane, xv0);
         ln_load_params(a.ln_w, a.ln_b, K, lane, gw0, gb0);
@@ -1472,7 +1478,7 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
         for (int rr = 0; rr < DG_MAXB / NW; ++rr) {
             const int rb = w + NW * rr;
             if (rb < B) {
-                float4 xv[DG_LNV];
+                float4 xv[LNV];
                 if (IN == 0 && rr == 0) {
                     ln_regs_to_lds(xv0, K, gw0, gb0, xs + rb * K, lane);
                     continue;
@@ -1486,16 +1492,16 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
                                             : (a.beam_tok ? a.beam_tok[rb] : shard_token(a.amax + rb * AMAX_SHARDS, lane));
                     const f16 *ter = (const f16 *)a.te + (int64_t)tok * K;
                     const float *per = a.pe + (int64_t)pos * K;
-                    half4 tv[DG_LNV];
-                    float4 pv[DG_LNV];
+                    half4 tv[LNV];
+                    float4 pv[LNV];
 #pragma unroll
-                    for (int i = 0; i < DG_LNV; ++i) {
+                    for (int i = 0; i < LNV; ++i) {
                         const int e = (lane + 64 * i) * 4, ec = e < K ? e : 0;
                         tv[i] = *(const half4 *)(ter + ec);
                         pv[i] = *(const float4 *)(per + ec);
                     }
 #pragma unroll
-                    for (int i = 0; i < DG_LNV; ++i) {
+                    for (int i = 0; i < LNV; ++i) {
                         const int e = (lane + 64 * i) * 4;
                         xv[i] = keep4(make_float4((float)tv[i][0] + pv[i].x, (float)tv[i][1] + pv[i].y,
                                                   (float)tv[i][2] + pv[i].z, (float)tv[i][3] + pv[i].w),
@@ -1581,6 +1587,11 @@ int g_logits_cap = 512;  // persistent logits grid (WMI_LOGITS_CAP overrides; 2 
 // one wave at B <= 2): 4 measured fastest at base, B = 1 (one wave per
 // workgroup: mlp0 4.6 -> 10 us, every workgroup repeating the LayerNorm)
 int g_gemv_nw = 4;
+// row groups per register set of the vocabulary GEMV at K <= 512 (WMI_LOGITS_G
+// = 1 / 2 / 4) and its persistent grid cap (WMI_LOGITS_CAP2): base 13.9 us at
+// G = 1 -> 12.1 us at G = 2 over 1024 workgroups
+int g_logits_g = 2;
+int g_logits_cap2 = 1024;
 int g_self_split = 1;    // self-attention output projection over n / 128 workgroups per head (WMI_SELF_SPLIT=0: one)
 
 template <int EPI, int IN, int WQ, int NW>
@@ -1602,6 +1613,22 @@ static hipError_t dec_gemv_nw(hipStream_t s, const DecGemvArgs &a) {
         hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 16, 0, NW>, lds);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 16, 0, NW>), grid, block, lds, s, a);
+    } else if (EPI == DEC_LOGITS && a.K <= 512 && g_logits_g > 1) {
+        // K <= 512: 4 chunks cover a row, so each register set can hold G = 2
+        // or 4 row groups (more bytes in flight per wave at the same VGPRs)
+        // (128 VGPRs at G = 2: four workgroups per CU, hence the larger cap;
+        // a balanced grid of equal row-group counts measured slower)
+        const int G = g_logits_g == 2 ? 2 : 4, ng = cdiv(a.N, 4 * NW * G);
+        const dim3 grid2(ng < g_logits_cap2 ? ng : g_logits_cap2);
+        if (G == 2) {
+            hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 2, 4, 0, NW>, lds);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 2, 4, 0, NW>), grid2, block, lds, s, a);
+        } else {
+            hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 4, 4, 0, NW>, lds);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 4, 4, 0, NW>), grid2, block, lds, s, a);
+        }
     } else {
         hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 8, 0, NW>, lds);
         if (e != hipSuccess) return e;
@@ -1678,6 +1705,45 @@ __global__ __launch_bounds__(256) void k_probe_barrier(uint32_t *cnt, uint32_t b
         }
         __syncthreads();
     }
+}
+
+// hierarchical grid barrier probe: workgroup i arrives on group counter i % 8
+// (one group per XCD under round-robin dispatch, so arrivals contend only
+// within an XCD); the last arrival of a group bumps the top counter.  MODE 0:
+// every workgroup polls the top counter; MODE 1: group leaders poll it and
+// release their group through a per-group word.  FENCE adds the agent-scope
+// release / acquire fences a real hand-off of plain-stored data needs.
+// Layout (uint32 index): group counters g * 32, top 256, release words 288 + g * 32.
+template <int MODE, bool FENCE>
+__global__ __launch_bounds__(256) void k_probe_barrier_h(uint32_t *cnt, uint32_t base, int rounds, uint32_t *err) {
+    const int g = blockIdx.x & 7, ng = gridDim.x >> 3;
+    for (int r = 0; r < rounds; ++r) {
+        const uint32_t gen = base + (uint32_t)r + 1;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            const uint32_t old = __hip_atomic_fetch_add(cnt + g * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool last = old + 1 == gen * (uint32_t)ng;
+            if (last) __hip_atomic_fetch_add(cnt + 256, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (MODE == 0 || last) spin_until(cnt + 256, gen * 8u, err);
+            if (MODE == 1) {
+                if (last) __hip_atomic_store(cnt + 288 + g * 32, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else spin_until(cnt + 288 + g * 32, gen, err);
+            }
+            if (FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_probe_barrier_h(hipStream_t s, int mode, int n_wg, int rounds, uint32_t *cnt, uint32_t base,
+                                  uint32_t *err) {
+    if (n_wg % 8) return hipErrorInvalidValue;
+    if (mode == 0) hipLaunchKernelGGL((k_probe_barrier_h<0, false>), dim3(n_wg), dim3(256), 0, s, cnt, base, rounds, err);
+    else if (mode == 1) hipLaunchKernelGGL((k_probe_barrier_h<1, false>), dim3(n_wg), dim3(256), 0, s, cnt, base, rounds, err);
+    else if (mode == 2) hipLaunchKernelGGL((k_probe_barrier_h<0, true>), dim3(n_wg), dim3(256), 0, s, cnt, base, rounds, err);
+    else hipLaunchKernelGGL((k_probe_barrier_h<1, true>), dim3(n_wg), dim3(256), 0, s, cnt, base, rounds, err);
+    return hipGetLastError();
 }
 
 hipError_t launch_probe_barrier(hipStream_t s, int n_wg, int rounds, uint32_t *cnt, uint32_t base, uint32_t *err) {
@@ -1822,7 +1888,8 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
         rbo = *(const float4 *)(a.res_bias + 4 * tid);
         rx = *(const float4 *)(a.x + (int64_t)b * n + 4 * tid);
     }
-    float4 xv[DG_LNV], gw[DG_LNV], gb[DG_LNV];
+    constexpr int XLNV = (KC * 128 + 255) / 256;  // n = KC * 128
+    float4 xv[XLNV], gw[XLNV], gb[XLNV];
     if (w == 0) {
         ln_load_params(a.ln_w, a.ln_b, n, lane, gw, gb);
         if (!a.res_parts) ln_load_row(a.x + (int64_t)b * n, n, lane, xv);
