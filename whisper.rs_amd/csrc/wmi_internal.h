@@ -138,6 +138,7 @@ constexpr int DEC_ROWS = 8;  // decoder rows per step: clips (greedy) or beam hy
 hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a);
 extern int g_logits_cap;
 extern int g_logits_g;
+extern int g_down_nw1_b;
 extern int g_logits_cap2;
 extern int g_gemv_nw;
 extern int g_self_split;

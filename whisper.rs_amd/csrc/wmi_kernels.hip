@@ -1592,6 +1592,7 @@ int g_gemv_nw = 4;
 // G = 1 -> 12.1 us at G = 2 over 1024 workgroups
 int g_logits_g = 2;
 int g_logits_cap2 = 1024;
+int g_down_nw1_b = 0;    // MLP-down GEMV with one wave per workgroup up to this many rows (WMI_DOWN_NW1_B)
 int g_self_split = 1;    // self-attention output projection over n / 128 workgroups per head (WMI_SELF_SPLIT=0: one)
 
 template <int EPI, int IN, int WQ, int NW>
@@ -1644,7 +1645,10 @@ static hipError_t dec_gemv_g(hipStream_t s, const DecGemvArgs &a) {
     if constexpr (EPI == DEC_LOGITS) {
         return dec_gemv_nw<EPI, IN, WQ, 4>(s, a);
     } else {
-        const bool one = g_gemv_nw == 1 || (g_gemv_nw == 0 && a.B <= 2);
+        // the MLP down projection (K = 4n, no LayerNorm) streams 4x the bytes
+        // per row: one wave per workgroup spreads them over 4x the CUs
+        const bool down = EPI == DEC_RESID && IN == 1 && a.K > 1024 && a.B <= g_down_nw1_b;
+        const bool one = down || g_gemv_nw == 1 || (g_gemv_nw == 0 && a.B <= 2);
         return one ? dec_gemv_nw<EPI, IN, WQ, 1>(s, a) : dec_gemv_nw<EPI, IN, WQ, 4>(s, a);
     }
 }
@@ -2020,7 +2024,7 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     __shared__ double redd[4];
     __shared__ __attribute__((aligned(16))) uint16_t P[MK];
     if (M > MK && tid == 0 && a.err) atomicOr(a.err, 2u);  // host bucketing error: flagged, never silent
-    __shared__ float ored[32][64];
+    __shared__ float ored[4][64];
     const f16 *qr = (const f16 *)a.q + (int64_t)b * n + h * 64;
     if (a.reset_amax && h == 0 && b == 0 && blockIdx.z == 0)
         for (int i = tid; i < a.B * AMAX_SHARDS; i += 256) a.reset_amax[i] = 0ull;
@@ -2127,25 +2131,25 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vv[i][e];
     }
+    // the wave's 8 key groups by shuffles, then the 4 waves through LDS
 #pragma unroll
-    for (int e = 0; e < 8; ++e) ored[jg][doct * 8 + e] = o[e];
+    for (int e = 0; e < 8; ++e) {
+        o[e] += __shfl_xor(o[e], 8);
+        o[e] += __shfl_xor(o[e], 16);
+        o[e] += __shfl_xor(o[e], 32);
+    }
+    if (lane < 8)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ored[w][lane * 8 + e] = o[e];
     __syncthreads();
     trace_phase(a.phase, 3);
     if (!a.Wo) {
-        if (tid < 64) {
-            float v = ored[0][tid];
-            for (int g = 1; g < 32; ++g) v = v + ored[g][tid];
-            a.opart[(int64_t)b * n + h * 64 + tid] = v;
-        }
+        if (tid < 64) a.opart[(int64_t)b * n + h * 64 + tid] = ((ored[0][tid] + ored[1][tid]) + ored[2][tid]) + ored[3][tid];
         trace_end(a.trace);
         return;
     }
     __shared__ __attribute__((aligned(16))) f16 oh[64];
-    if (tid < 64) {
-        float v = ored[0][tid];
-        for (int g = 1; g < 32; ++g) v = v + ored[g][tid];
-        oh[tid] = (f16)v;  // the f16 input of the output projection
-    }
+    if (tid < 64) oh[tid] = (f16)(((ored[0][tid] + ored[1][tid]) + ored[2][tid]) + ored[3][tid]);  // f16 input of Wo
     __syncthreads();
     half8 ov[8];
 #pragma unroll
