@@ -373,3 +373,60 @@ def test_small_q5_1(wmi, model_cache):
         ctx16.close()
         ctx.close()
         om.close()
+
+
+def _ctx_with_env(wmi, path, env):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return wmi.WhisperContext.new(path, 0, max_clips=1)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("K", [2, 3])
+def test_beam_rows_cross_attention(wmi, micro_model, oracle_micro, K):
+    """Two-kernel cross-attention (WMI_NO_COOP=1) with beam rows sharing one
+    workgroup per (chunk, head) (k_dec_xattn_rows, forced with WMI_XATTN_ROWS=2): the oracle's beams, and
+    tokens and scores bit-identical to one workgroup per row
+    (WMI_XATTN_ROWS=0).  The fused output projection's residual update runs
+    inside the row loop at these sizes."""
+    rows = _ctx_with_env(wmi, micro_model, {"WMI_NO_COOP": "1", "WMI_XATTN_ROWS": "2"})
+    try:
+        ref, score, got, got_score = _beam_case(rows, oracle_micro, range(100, 130), K, 20, True)
+        np.testing.assert_array_equal(got, ref)
+        assert abs(got_score - score) < 1e-2
+    finally:
+        rows.close()
+    per = _ctx_with_env(wmi, micro_model, {"WMI_NO_COOP": "1", "WMI_XATTN_ROWS": "0"})
+    try:
+        ref2, score2, got2, got_score2 = _beam_case(per, oracle_micro, range(100, 130), K, 20, True)
+        np.testing.assert_array_equal(got2, got)
+        assert got_score2 == got_score
+    finally:
+        per.close()
+        _ctx_with_env(wmi, micro_model, {"WMI_XATTN_ROWS": "1"}).close()  # restore the process default
+
+
+def test_beam_rows_tiny_en_beam5_identical(wmi, model_cache):
+    """C5's width at full audio context: k_dec_xattn_rows (5 rows, 12 chunks)
+    gives the same beams and scores, bit for bit, as per-row workgroups."""
+    path = synth.model_path("tiny.en", model_cache)
+    pcm = synth.synth_pcm_f32(30.0, 1234)
+    out = []
+    for rows in ("2", "0", "1"):
+        ctx = _ctx_with_env(wmi, path, {"WMI_NO_COOP": "1", "WMI_XATTN_ROWS": rows})
+        try:
+            ctx.set_audio_ctx(1500)
+            ctx.pcm_to_mel_batch([pcm])
+            ctx.encode(1, 0)
+            out.append(ctx.decode_beam(5, 24, suppress_eot=True)[0])
+        finally:
+            ctx.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]

@@ -1134,6 +1134,12 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     // other buffer while its sibling workgroups still read this one)
     float *X[2] = {ctx->dx, ctx->dx2};
     int cur = 0;
+    // the fused output projection makes every cross-attention workgroup
+    // (chunks x H per row) re-sum its row's H partials (H n floats): worth a
+    // kernel while that re-read stays small (base/small greedy or 5 beams,
+    // base 8 clips), not at large-v3 x 5 beams (12 H^2 B n 4 B = 123 MB a
+    // layer; measured 554 -> 498 ms decode unfused)
+    const bool fuse_wo = ctx->fuse_wo && (int64_t)H * H * B * n <= ((int64_t)1 << 20);
     for (int l = 0; l < hp.n_text_layer; ++l) {
         const DecLayerDev &d = ctx->dec[l];
         uint16_t *kc = ctx->kcache + (size_t)l * DEC_ROWS * hp.n_text_ctx * n;
@@ -1171,14 +1177,14 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
             at.kv_src = ctx->dkvsrc;
             at.kv_src_stride = hp.n_text_ctx;
         }
-        if (ctx->fuse_wo) {  // per-head output-projection partials; residual in the next kernel
+        if (fuse_wo) {  // per-head output-projection partials; residual in the next kernel
             at.Wo = d.wo;
             at.wo_parts = ctx->dwoparts;
         }
         at.trace = tslot(ctx, "self_attn", l);
         if (l == 0) at.phase = pslot(ctx, 1, "self_attn[0]");
         HIPCHK(ctx, launch_dec_attn(s, at));
-        if (!ctx->fuse_wo) {
+        if (!fuse_wo) {
             g = DecGemvArgs{};
             g.parts = ctx->dopart; g.n_parts = 1; g.W = d.wo; g.bias = d.bo; g.N = n; g.K = n; g.B = B;
             g.Wq5 = q5 ? d.wo5 : nullptr;
@@ -1197,7 +1203,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         at.sync = ctx->use_coop ? ctx->dsync + (size_t)l * 8 * H : nullptr;
         at.err = ctx->derr;
         at.clip_div = beam ? B : 1;  // beam rows all read clip b0's cross K/V
-        if (ctx->fuse_wo) {
+        if (fuse_wo) {
             at.res_parts = ctx->dwoparts; at.res_bias = d.bo; at.x_out = X[cur ^ 1];
             cur ^= 1;
         }
@@ -1720,6 +1726,7 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (const char *c = getenv("WMI_DOWN_NW1_B")) g_down_nw1_b = atoi(c);
     if (const char *c = getenv("WMI_LOGITS_CAP2")) g_logits_cap2 = atoi(c) > 0 ? atoi(c) : g_logits_cap2;
     if (const char *c = getenv("WMI_GEMV_NW")) g_gemv_nw = atoi(c) == 1 ? 1 : atoi(c) == 0 ? 0 : 4;
+    if (const char *c = getenv("WMI_XATTN_ROWS")) g_xattn_rows = atoi(c);
     if (const char *c = getenv("WMI_SELF_SPLIT")) g_self_split = atoi(c) >= 0 ? atoi(c) : g_self_split;
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;

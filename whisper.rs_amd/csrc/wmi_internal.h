@@ -142,6 +142,7 @@ extern int g_down_nw1_b;
 extern int g_logits_cap2;
 extern int g_gemv_nw;
 extern int g_self_split;
+extern int g_xattn_rows;
 
 struct DecAttnArgs {
     const uint16_t *q;       // [B][n]

@@ -1593,6 +1593,7 @@ int g_gemv_nw = 4;
 int g_logits_g = 2;
 int g_logits_cap2 = 1024;
 int g_down_nw1_b = 0;    // MLP-down GEMV with one wave per workgroup up to this many rows (WMI_DOWN_NW1_B)
+int g_xattn_rows = 1;    // beam rows share cross-attention phase A: 1 auto (n > 768), 2 always, 0 never (WMI_XATTN_ROWS)
 int g_self_split = 1;    // self-attention output projection over n / 128 workgroups per head (WMI_SELF_SPLIT=0: one)
 
 template <int EPI, int IN, int WQ, int NW>
@@ -1998,6 +1999,106 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
     trace_end(a.trace);
 }
 
+// Phase A of cross-attention for beam rows, which all read one clip's cross
+// K / V (clip_div == B): one workgroup per (chunk, head) serves every row
+// (B <= 8), so the head's 64 Wq rows and the chunk's 128 keys are fetched
+// once instead of B times (large-v3 x 5 beams: 197 MB -> 39 MB of Wq reads a
+// layer).  Per row the arithmetic is k_dec_xattn<KC, 0>'s, op for op, so S
+// and cmax are bit-identical; k_dec_attn_pv follows as in the two-kernel form.
+template <int KC>
+__global__ __launch_bounds__(256) void k_dec_xattn_rows(DecAttnArgs a) {
+    trace_begin(a.trace);
+    const int c = blockIdx.x, h = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int q = lane >> 4, l16 = lane & 15;
+    const int M = a.M_fixed, n = a.n, B = a.B;
+    constexpr int H2 = 2 * KC, XLNV = (KC * 128 + 255) / 256;
+    __shared__ __attribute__((aligned(16))) f16 xs[8][KC * 128];
+    __shared__ __attribute__((aligned(16))) f16 qh[8][64];
+    __shared__ __attribute__((aligned(16))) float xnew[4][KC * 128];
+    __shared__ float red[8][4];
+    // row-shared operands first: the chunk's keys, the head's Wq rows, bq
+    const int key = c * DA_CK + (tid >> 1), half = tid & 1;
+    half8 kf[4];
+    {
+        const f16 *kr = (const f16 *)a.K + (int64_t)(key < M ? key : M - 1) * n + h * 64 + half * 32;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) kf[i] = *(const half8 *)(kr + 8 * i);
+    }
+    half8 wq[4][KC];
+    float bqr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = h * 64 + w * 16 + q * 4 + i;
+        const f16 *wr = (const f16 *)a.Wq + (int64_t)r * n + l16 * 8;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) wq[i][kc] = *(const half8 *)(wr + kc * 128);
+        bqr[i] = a.bq[r];
+    }
+    float4 gw[XLNV], gb[XLNV], xv[XLNV];
+    ln_load_params(a.ln_w, a.ln_b, n, lane, gw, gb);
+    // LayerNorm of every row into xs: wave w takes rows w, w + 4
+    for (int r = w; r < B; r += 4) {
+        const float *xr = a.x + (int64_t)r * n;
+        if (a.res_parts) {  // the fused self-attention's residual update, as in k_dec_xattn
+            const float *pp = a.res_parts + (int64_t)r * H2 * n;
+            for (int j = lane; j < n / 4; j += 64) {
+                float4 rp[H2];
+#pragma unroll
+                for (int hh = 0; hh < H2; ++hh) rp[hh] = *(const float4 *)(pp + (int64_t)hh * n + 4 * j);
+                const float4 rbo = *(const float4 *)(a.res_bias + 4 * j);
+                const float4 rx = *(const float4 *)(xr + 4 * j);
+                float4 sm = rp[0];
+#pragma unroll
+                for (int hh = 1; hh < H2; ++hh) {
+                    sm.x = sm.x + rp[hh].x; sm.y = sm.y + rp[hh].y; sm.z = sm.z + rp[hh].z; sm.w = sm.w + rp[hh].w;
+                }
+                float4 v;
+                v.x = (rbo.x + sm.x) + rx.x; v.y = (rbo.y + sm.y) + rx.y;
+                v.z = (rbo.z + sm.z) + rx.z; v.w = (rbo.w + sm.w) + rx.w;
+                *(float4 *)(xnew[w] + 4 * j) = v;
+                if (c == 0 && h == 0) *(float4 *)(a.x_out + (int64_t)r * n + 4 * j) = v;
+            }
+            wave_sync();
+            xr = xnew[w];
+        }
+        ln_load_row(xr, n, lane, xv);
+        ln_regs_to_lds(xv, n, gw, gb, xs[r], lane);
+        wave_sync();  // xnew[w] is rewritten by this wave's next row
+    }
+    __syncthreads();
+    for (int r = 0; r < B; ++r) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float acc = 0.0f;
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) acc = dot8(wq[i][kc], *(const half8 *)(xs[r] + kc * 128 + l16 * 8), acc);
+            acc += __shfl_xor(acc, 8);
+            acc += __shfl_xor(acc, 4);
+            acc += __shfl_xor(acc, 2);
+            acc += __shfl_xor(acc, 1);
+            if (l16 == 0) qh[r][w * 16 + q * 4 + i] = (f16)((acc + bqr[i]) * a.qscale);
+        }
+    }
+    __syncthreads();
+    for (int r = 0; r < B; ++r) {
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s = dot8(kf[i], *(const half8 *)(qh[r] + half * 32 + 8 * i), s);
+        s += __shfl_xor(s, 1);
+        float *S = a.S + ((int64_t)r * a.H + h) * a.s_stride;
+        if (half == 0 && key < M) S[key] = s;
+        float m = (key < M) ? s : -INFINITY;
+        m = wave_max(m);
+        if (lane == 0) red[r][w] = m;
+    }
+    __syncthreads();
+    if (tid < B)
+        a.cmax[((int64_t)tid * a.H + h) * a.n_chunks + c] =
+            fmaxf(fmaxf(red[tid][0], red[tid][1]), fmaxf(red[tid][2], red[tid][3]));
+    trace_end(a.trace);
+}
+
 __global__ __launch_bounds__(256) void k_dec_attn_pv(DecAttnArgs a) {
     trace_begin(a.trace);
     const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
@@ -2209,6 +2310,27 @@ hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
     // (<= 2 workgroups per CU) and the Wq rows fit the register budget;
     // otherwise the two-kernel form
     const bool coop = a.sync && a.n_chunks * a.H * a.B <= 512 && a.n <= 768;
+    // beam rows sharing one clip: phase A once per (chunk, head) for all rows
+    // (auto: n > 768, where the head's Wq rows dominate a workgroup's reads —
+    // large-v3 x 5 beams 498 -> 448 ms decode; small x 5 beams is faster per
+    // row, 122 vs 132 ms, as 144 workgroups serialising 5 rows under-fill)
+    if (!coop && (g_xattn_rows == 2 || (g_xattn_rows == 1 && a.n > 768)) && a.B > 1 && a.B <= 8 &&
+        a.clip_div == a.B) {
+        const dim3 g1(a.n_chunks, a.H, 1);
+#define XR(KC)                                                                   \
+    case KC:                                                                     \
+        hipLaunchKernelGGL((k_dec_xattn_rows<KC>), g1, dim3(256), 0, s, a);      \
+        break;
+        switch (a.n / 128) {
+            XR(1) XR(2) XR(3) XR(4) XR(5) XR(6) XR(8) XR(10)
+            default: return hipErrorInvalidValue;
+        }
+#undef XR
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_dec_attn_pv, grid, dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
 #define XA(KC)                                                                                  \
     case KC:                                                                                    \
         if (coop) hipLaunchKernelGGL((k_dec_xattn<KC, 1>), grid, dim3(256), 0, s, a);          \
