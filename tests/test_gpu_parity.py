@@ -129,6 +129,28 @@ def test_decoder_teacher_forced_logits(micro_ctx, oracle_micro):
     assert (got.argmax(1) == ref.argmax(1))[decisive].all()
 
 
+def test_decoder_logits_full_text_ctx(micro_ctx, oracle_micro):
+    """Maximum size: teacher-forced logits over the whole text context (448
+    positions), so the self-attention runs every key-capacity bucket (64, 128,
+    256, 512) and the KV cache fills to its last row; one token more is an
+    error, not a silent overrun."""
+    pcm = synth.synth_pcm_f32(2.0, 7)
+    _, ck_ref, cv_ref = _check_encoder(micro_ctx, oracle_micro, pcm, 64)
+    n_ctx = micro_ctx.hparams["n_text_ctx"]
+    rng = np.random.default_rng(1)
+    pr = oracle_micro.prompt()
+    toks = np.array(pr + list(rng.integers(0, 50000, n_ctx - len(pr))), np.int32)
+    ref = oracle_micro.decode_logits(ck_ref, cv_ref, toks, n_threads=threads())
+    got = micro_ctx.decode_logits(toks, 0)
+    err = np.abs(got - ref).max(axis=1)
+    assert err.max() <= 2e-3, (err.max(), int(err.argmax()))
+    top2 = np.sort(ref, axis=1)[:, -2:]
+    decisive = (top2[:, 1] - top2[:, 0]) > 1e-3
+    assert (got.argmax(1) == ref.argmax(1))[decisive].all()
+    with pytest.raises(Exception):
+        micro_ctx.decode_logits(np.concatenate([toks, toks[-1:]]), 0)
+
+
 def test_greedy_tokens_micro(micro_ctx, oracle_micro):
     pcm = synth.synth_pcm_f32(2.0, 99)
     _, ck_ref, cv_ref = _check_encoder(micro_ctx, oracle_micro, pcm, 64)
