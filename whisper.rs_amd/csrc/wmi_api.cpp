@@ -1726,6 +1726,7 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (const char *c = getenv("WMI_DOWN_NW1_B")) g_down_nw1_b = atoi(c);
     if (const char *c = getenv("WMI_LOGITS_CAP2")) g_logits_cap2 = atoi(c) > 0 ? atoi(c) : g_logits_cap2;
     if (const char *c = getenv("WMI_GEMV_NW")) g_gemv_nw = atoi(c) == 1 ? 1 : atoi(c) == 0 ? 0 : 4;
+    if (const char *c = getenv("WMI_COOP_MAX")) g_coop_max = atoi(c) > 0 ? atoi(c) : g_coop_max;
     if (const char *c = getenv("WMI_XATTN_ROWS")) g_xattn_rows = atoi(c);
     if (const char *c = getenv("WMI_SELF_SPLIT")) g_self_split = atoi(c) >= 0 ? atoi(c) : g_self_split;
     if (getenv("WMI_TRACE")) {

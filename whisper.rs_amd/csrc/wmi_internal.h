@@ -143,6 +143,7 @@ extern int g_logits_cap2;
 extern int g_gemv_nw;
 extern int g_self_split;
 extern int g_xattn_rows;
+extern int g_coop_max;
 
 struct DecAttnArgs {
     const uint16_t *q;       // [B][n]

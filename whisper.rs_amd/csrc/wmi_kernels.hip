@@ -1593,6 +1593,7 @@ int g_gemv_nw = 4;
 int g_logits_g = 2;
 int g_logits_cap2 = 1024;
 int g_down_nw1_b = 0;    // MLP-down GEMV with one wave per workgroup up to this many rows (WMI_DOWN_NW1_B)
+int g_coop_max = 512;    // cooperative cross-attention up to this many workgroups (WMI_COOP_MAX)
 int g_xattn_rows = 1;    // beam rows share cross-attention phase A: 1 auto (n > 768), 2 always, 0 never (WMI_XATTN_ROWS)
 int g_self_split = 1;    // self-attention output projection over n / 128 workgroups per head (WMI_SELF_SPLIT=0: one)
 
@@ -2309,7 +2310,7 @@ hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
     // cooperative single kernel while the grid stays far inside residency
     // (<= 2 workgroups per CU) and the Wq rows fit the register budget;
     // otherwise the two-kernel form
-    const bool coop = a.sync && a.n_chunks * a.H * a.B <= 512 && a.n <= 768;
+    const bool coop = a.sync && a.n_chunks * a.H * a.B <= g_coop_max && a.n <= 768;
     // beam rows sharing one clip: phase A once per (chunk, head) for all rows
     // (auto: n > 768, where the head's Wq rows dominate a workgroup's reads —
     // large-v3 x 5 beams 498 -> 448 ms decode; small x 5 beams is faster per
