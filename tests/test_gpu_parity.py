@@ -253,13 +253,42 @@ def test_beam_search_tiny_en_beam5(wmi, model_cache):
         om.close()
 
 
-def test_beam_one_equals_greedy(micro_ctx):
-    micro_ctx.set_audio_ctx(64)
-    micro_ctx.pcm_to_mel_batch([synth.synth_pcm_f32(2.0, 4)])
-    micro_ctx.encode(1, 0)
-    g = micro_ctx.decode_greedy(16, suppress_eot=True)[0]
-    b, _ = micro_ctx.decode_beam(1, 16, suppress_eot=True)[0]
-    np.testing.assert_array_equal(b, g)
+def test_beam_one_equals_greedy(wmi, micro_model):
+    # beam search runs on the kernel chain: compare with the chain's greedy
+    # (the persistent decoder is held to the chain by test_persistent_matches_chain)
+    ctx = _ctx_with_env(wmi, micro_model, {"WMI_PERSIST": "0"})
+    try:
+        ctx.set_audio_ctx(64)
+        ctx.pcm_to_mel_batch([synth.synth_pcm_f32(2.0, 4)])
+        ctx.encode(1, 0)
+        g = ctx.decode_greedy(16, suppress_eot=True)[0]
+        b, _ = ctx.decode_beam(1, 16, suppress_eot=True)[0]
+        np.testing.assert_array_equal(b, g)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("model,n_clips,n_ctx", [("micro", 1, 64), ("micro", 3, 64), ("micro", 2, 1500),
+                                                 ("tiny.en", 1, 1500), ("base", 2, 1500)])
+def test_persistent_matches_chain(wmi, model_cache, model, n_clips, n_ctx):
+    """The persistent decoder (one launch per run of steps, granule hand-offs)
+    computes every decoder op in the kernel chain's order: against the chain
+    with the unfused output projection (WMI_NO_FUSE=1) the greedy token ids
+    of a 40-step run are identical, bit for bit, for one and several rows."""
+    path = synth.model_path(model, model_cache)
+    clips = [synth.synth_pcm_f32(30.0 if n_ctx == 1500 else 2.0, 40 + i) for i in range(n_clips)]
+    out = []
+    for env in ({"WMI_PERSIST": "1"}, {"WMI_PERSIST": "0", "WMI_NO_FUSE": "1"}):
+        ctx = _ctx_with_env(wmi, path, env, max_clips=n_clips)
+        try:
+            ctx.set_audio_ctx(n_ctx)
+            ctx.pcm_to_mel_batch(clips)
+            ctx.encode(1, 0)
+            out.append(ctx.decode_greedy(40, suppress_eot=True))
+        finally:
+            ctx.close()
+    for i in range(n_clips):
+        np.testing.assert_array_equal(out[0][i], out[1][i])
 
 
 @pytest.fixture(scope="module")
@@ -397,12 +426,12 @@ def test_small_q5_1(wmi, model_cache):
         om.close()
 
 
-def _ctx_with_env(wmi, path, env):
+def _ctx_with_env(wmi, path, env, max_clips=1):
     import os
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
-        return wmi.WhisperContext.new(path, 0, max_clips=1)
+        return wmi.WhisperContext.new(path, 0, max_clips=max_clips)
     finally:
         for k, v in old.items():
             if v is None:

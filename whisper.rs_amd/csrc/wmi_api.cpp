@@ -272,6 +272,14 @@ struct wmi_context {
     unsigned long long *d_trace = nullptr;
     std::vector<std::string> trace_names;
     std::vector<std::string> phase_names = std::vector<std::string>(32);  // phase slots 32.. (layer 0 GEMVs, logits)
+    // persistent decoder (wmi_persist.hip): greedy steps in one launch
+    bool use_persist = true;          // WMI_PERSIST=0: kernel chain instead
+    PersistLayer *d_players = nullptr;
+    uint64_t *d_xg = nullptr;         // exchange block (persist_layout at n_audio_ctx)
+    size_t xg_bytes = 0;
+    int32_t *d_curtok = nullptr;      // [8]
+    int persist_G[9] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};  // grid per row count (0: unsupported)
+    unsigned long long *d_ptrace = nullptr;  // WMI_PTRACE=1: phase clocks of the first launch of a run
     // dist
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
@@ -824,6 +832,16 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
                        Q(dq5[i].wqkv), Q(dq5[i].wo), Q(dq5[i].wco), Q(dq5[i].w0), Q(dq5[i].w1)};
     }
     ctx->te5 = q5 ? (const uint8_t *)(base + o_te5) : nullptr;
+    // layer table of the persistent decoder (f16 weights; q5_1 models use the
+    // dequantised f16 copies, the same weights the q5_1 GEMVs dequantise to)
+    std::vector<PersistLayer> pl(Lt);
+    for (int i = 0; i < Lt; ++i) {
+        const DecLayerDev &d = ctx->dec[i];
+        pl[i] = {d.ln1_w, d.ln1_b, d.wqkv, d.bqkv, d.wo, d.bo, d.lnc_w, d.lnc_b, d.wcq, d.bcq,
+                 d.wco, d.bco, d.ln2_w, d.ln2_b, d.w0, d.b0, d.w1, d.b1};
+    }
+    HIPCHK(ctx, hipMalloc(&ctx->d_players, pl.size() * sizeof(PersistLayer)));
+    HIPCHK(ctx, hipMemcpy(ctx->d_players, pl.data(), pl.size() * sizeof(PersistLayer), hipMemcpyHostToDevice));
     return WMI_OK;
 }
 
@@ -872,6 +890,9 @@ int alloc_workspace(wmi_context *ctx) {
     const size_t o_sync = A.take(sync_bytes + 256);
     const size_t o_amax = A.take(8 * AMAX_SHARDS * 8);
     const size_t o_st = A.take(sizeof(DecState));
+    const XLayout xl = persist_layout((int)nt, (int)Hd, (int)T);
+    const size_t o_xg = A.take((size_t)xl.total * 8);
+    const size_t o_ct = A.take(8 * 4);
     const size_t o_ptrs = A.take(B * sizeof(float *));
     const size_t o_ns = A.take(B * 8);
     const size_t o_nl = A.take(B * 8);
@@ -920,6 +941,9 @@ int alloc_workspace(wmi_context *ctx) {
     ctx->n_chunks_max = (int)Cmax;
     ctx->damax = (unsigned long long *)(b + o_amax);
     ctx->dstate = (DecState *)(b + o_st);
+    ctx->d_xg = (uint64_t *)(b + o_xg);
+    ctx->xg_bytes = (size_t)xl.total * 8;
+    ctx->d_curtok = (int32_t *)(b + o_ct);
     ctx->d_pcm_ptrs = (float **)(b + o_ptrs);
     ctx->d_nsamp = (int64_t *)(b + o_ns);
     ctx->d_nlen = (int64_t *)(b + o_nl);
@@ -1280,6 +1304,7 @@ int ensure_decode_buffers(wmi_context *ctx, int feed_elems, size_t token_elems) 
 // bit 1 self-attention launched with too small a key capacity
 int dec_err(wmi_context *ctx, uint32_t err) {
     if (err & 1u) return set_err(ctx, WMI_E_HIP, "cross-attention exchange timed out (workgroups not co-resident)");
+    if (err & 8u) return set_err(ctx, WMI_E_HIP, "persistent decoder exchange timed out (workgroups not co-resident)");
     return set_err(ctx, WMI_E_HIP, "internal: self-attention key capacity below pos + 1 (err word %u)", err);
 }
 
@@ -1340,6 +1365,76 @@ int run_dec_steps(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride
     return WMI_OK;
 }
 
+size_t hp_ptrace_slots(const wmi_hparams &hp) { return (size_t)hp.n_text_ctx * (hp.n_text_layer + 1) * 16 * 2; }
+
+// WMI_PTRACE: average phase durations of the persistent decoder's first
+// launch (workgroups 0 and G / 2), from the phase-end clocks (100 MHz)
+int ptrace_dump(wmi_context *ctx, int steps) {
+    const int L = ctx->hp.n_text_layer;
+    std::vector<unsigned long long> t(hp_ptrace_slots(ctx->hp));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipMemcpy(t.data(), ctx->d_ptrace, t.size() * 8, hipMemcpyDeviceToHost));
+    auto at = [&](int st, int l, int k, int w) { return t[(((size_t)st * (L + 1) + l) * 16 + k) * 2 + w]; };
+    static const char *nm[10] = {"A qkv", "B self", "C wo", "D xq", "E xscore", "F xpv", "G1 xred", "G2 wco", "H mlp0", "I mlp1"};
+    for (int w = 0; w < 2; ++w) {
+        double ph[10] = {0}, lg = 0, tot = 0;
+        int ns = 0;
+        for (int st = 1; st < steps; ++st) {  // step 0 includes the launch
+            unsigned long long prev = at(st - 1, L, 0, w);
+            const unsigned long long s0 = prev;
+            for (int l = 0; l < L; ++l)
+                for (int k = 0; k < 10; ++k) {
+                    const unsigned long long v = at(st, l, k, w);
+                    ph[k] += (double)(v - prev) * 0.01;
+                    prev = v;
+                }
+            lg += (double)(at(st, L, 0, w) - prev) * 0.01;
+            tot += (double)(at(st, L, 0, w) - s0) * 0.01;
+            ++ns;
+        }
+        if (!ns) return WMI_OK;
+        fprintf(stderr, "[wmi ptrace] wg %s: step %.2f us =", w ? "G/2" : "0", tot / ns);
+        for (int k = 0; k < 10; ++k) fprintf(stderr, " %s %.2f", nm[k], ph[k] / ns / L);
+        fprintf(stderr, " (per layer) + logits %.2f\n", lg / ns);
+    }
+    return WMI_OK;
+}
+
+// grid of the persistent decoder for B rows (0: not supported -> kernel chain)
+int persist_grid_for(wmi_context *ctx, int B) {
+    if (!ctx->use_persist || B < 1 || B > 8) return 0;
+    if (ctx->persist_G[B] < 0) ctx->persist_G[B] = persist_grid(ctx->device, ctx->hp.n_text_state, B, ctx->hp.n_audio_ctx);
+    return ctx->persist_G[B];
+}
+
+// launch arguments of the persistent decoder for rows [b0, b0 + B)
+PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, int feed_stride, int suppress_eot,
+                         int out_stride) {
+    const wmi_hparams &hp = ctx->hp;
+    const int n = hp.n_text_state, H = hp.n_text_head, T = ctx->enc_T;
+    PersistArgs a{};
+    a.layers = ctx->d_players; a.te = ctx->te; a.pe = ctx->d_pe; a.dln_w = ctx->dln_w; a.dln_b = ctx->dln_b;
+    a.gelu_tab = ctx->gelu_tab; a.exp_tab = ctx->exp_tab; a.n_exp = ctx->n_exp;
+    a.kcache = ctx->kcache; a.vcache = ctx->vcache; a.ck = ctx->ck; a.cv = ctx->cv;
+    a.L = hp.n_text_layer; a.n = n; a.V = hp.n_vocab; a.B = B; a.T = T; a.tctx = hp.n_text_ctx;
+    a.Bt = ctx->enc_clips; a.b0 = b0;
+    // key chunks of 128 keys per (row, head), the chain's chunking (so the
+    // cross-attention sums group exactly as k_dec_xattn's, and the result
+    // does not depend on the row count); wider only where the task table
+    // would overflow (large-v3 x 8 rows)
+    int cl = 128;
+    while ((int64_t)B * H * ((T + cl - 1) / cl) > PX_TASKS && cl < 512) cl *= 2;
+    a.cl = cl;
+    a.nch = (T + cl - 1) / cl;
+    (void)G;
+    a.qscale = powf((float)n / (float)H, -0.25f);
+    a.st = ctx->dstate; a.feed = ctx->dfeed; a.feed_len = feed_len; a.feed_stride = feed_stride;
+    a.tokens_out = ctx->dtokens + (size_t)b0 * out_stride; a.out_stride = out_stride;
+    a.cur_tok = ctx->d_curtok; a.suppress_id = suppress_eot ? ctx->sp.eot : -1;
+    a.xg = ctx->d_xg; a.err = ctx->derr;
+    return a;
+}
+
 // greedy decode of every encoded clip; tokens stay in ctx->dtokens
 // ([enc_clips][n_gen]); returns after enqueueing (no sync) unless early stop.
 int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, std::vector<int32_t> *host_tokens,
@@ -1365,11 +1460,22 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
         HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * AMAX_SHARDS * 8, ctx->stream));
         HIPCHK(ctx, hipMemsetAsync(ctx->dsync, 0, ctx->sync_bytes, ctx->stream));
         const int total_steps = np + n_gen - 1;
+        const int G = persist_grid_for(ctx, B);
+        if (G > 0) HIPCHK(ctx, hipMemsetAsync(ctx->d_xg, 0, ctx->xg_bytes, ctx->stream));
         int done_steps = 0;
         while (done_steps < total_steps) {
             int chunk = total_steps - done_steps;
             if (early_stop && chunk > 32) chunk = 32;
-            rc = run_dec_steps(ctx, b0, B, np, np, suppress_eot, n_gen, done_steps, chunk);
+            if (G > 0) {  // persistent decoder: the chunk's steps in one launch
+                PersistArgs pa = persist_args(ctx, b0, B, G, np, np, suppress_eot, n_gen);
+                pa.n_steps = chunk;
+                if (ctx->d_ptrace && done_steps == 0 && b0 == 0) pa.ptrace = ctx->d_ptrace;
+                HIPCHK(ctx, launch_dec_persist(ctx->stream, pa, G));
+                if (pa.ptrace) rc = ptrace_dump(ctx, chunk);
+                else rc = 0;
+            } else {
+                rc = run_dec_steps(ctx, b0, B, np, np, suppress_eot, n_gen, done_steps, chunk);
+            }
             if (rc) return rc;
             done_steps += chunk;
             if (early_stop && done_steps < total_steps && done_steps >= np) {
@@ -1389,7 +1495,9 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
                 if (all) break;
             }
         }
-        // record the last argmax (embed kernel in record-only mode)
+        // record the last argmax (embed kernel in record-only mode; the
+        // persistent decoder records every token itself)
+        if (G > 0) continue;
         DecEmbedArgs em{};
         em.te = ctx->te; em.pe = ctx->d_pe; em.x = ctx->dx; em.feed = ctx->dfeed; em.feed_len = np; em.feed_stride = np;
         em.amax = ctx->damax; em.tokens_out = ctx->dtokens + (size_t)b0 * n_gen; em.out_stride = n_gen;
@@ -1719,6 +1827,12 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (getenv("WMI_NO_COOP")) ctx->use_coop = false;
     if (getenv("WMI_NO_Q5")) ctx->use_q5 = false;
     if (getenv("WMI_NO_FUSE")) ctx->fuse_wo = false;
+    if (const char *c = getenv("WMI_PERSIST")) ctx->use_persist = atoi(c) != 0;
+    if (getenv("WMI_PTRACE")) {
+        const size_t nb = (size_t)hp_ptrace_slots(ctx->hp) * 8;
+        HIPCHK(ctx.get(), hipMalloc(&ctx->d_ptrace, nb));
+        HIPCHK(ctx.get(), hipMemset(ctx->d_ptrace, 0, nb));
+    }
     if (const char *c = getenv("WMI_ATTN_V1")) g_attn_v1 = atoi(c) == 2 ? 2 : 1;
     if (const char *c = getenv("WMI_LOGITS_CAP")) g_logits_cap = atoi(c) > 0 ? atoi(c) : g_logits_cap;
     if (const char *c = getenv("WMI_LOGITS_G")) g_logits_g = atoi(c);
@@ -1752,6 +1866,8 @@ void wmi_free(wmi_context *ctx) {
     if (ctx->d_ws) (void)hipFree(ctx->d_ws);
     if (ctx->d_trace) (void)hipFree(ctx->d_trace);
     if (ctx->d_model) (void)hipFree(ctx->d_model);
+    if (ctx->d_players) (void)hipFree(ctx->d_players);
+    if (ctx->d_ptrace) (void)hipFree(ctx->d_ptrace);
     for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -2236,6 +2352,7 @@ int wmi_selftest(wmi_context *ctx, int32_t *n_mismatch) {
     HIPCHK(ctx, hipSetDevice(ctx->device));
     HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));
     HIPCHK(ctx, launch_selftest(ctx->stream, ctx->exp_tab, ctx->n_exp, ctx->derr));
+    HIPCHK(ctx, launch_persist_selftest(ctx->stream, ctx->exp_tab, ctx->n_exp, ctx->derr));
     uint32_t mm = 0;
     HIPCHK(ctx, hipMemcpyAsync(&mm, ctx->derr, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));

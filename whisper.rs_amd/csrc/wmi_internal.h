@@ -252,4 +252,85 @@ struct DecEmbedArgs {
 };
 hipError_t launch_dec_embed(hipStream_t s, const DecEmbedArgs &a);
 
+// ---- persistent decoder: one launch runs n_steps greedy decoder steps -------
+// (wmi_persist.hip).  Every decoder step is a fixed sequence of phases; the
+// workgroups of the launch (all co-resident, one per CU) hand each phase's
+// outputs to the next through epoch-tagged 8-byte granules {tag, value}
+// written and read with agent-scope (sc1) accesses — the data is its own flag,
+// so a seam costs one write-through store plus the consumer's poll, not a
+// kernel boundary (MI355X_MICROARCH.md handoff / allgather rows; measured
+// 1.8 us per all-to-all seam at 256 workgroups vs 2.1 us per graph kernel
+// boundary, scripts/seam_probe.hip).
+struct PersistLayer {          // decoder layer weights (device pointers)
+    const float *ln1_w, *ln1_b;
+    const uint16_t *wqkv; const float *bqkv;   // [3n][n], bias [3n] (zero for K)
+    const uint16_t *wo; const float *bo;
+    const float *lnc_w, *lnc_b;
+    const uint16_t *wcq; const float *bcq;
+    const uint16_t *wco; const float *bco;
+    const float *ln2_w, *ln2_b;
+    const uint16_t *w0; const float *b0;       // [4n][n]
+    const uint16_t *w1; const float *b1;       // [n][4n]
+};
+
+// exchange block layout in granules (host and device agree)
+struct XLayout {
+    int x1, x2, x3, q, k, v, o, xq, oc, h, s, m, p, a, ctl, total;
+};
+constexpr int PX_TASKS = 1024;   // cross-attention (row, head, chunk) tasks
+constexpr int PX_GMAX = 256;     // workgroups
+__host__ __device__ inline XLayout persist_layout(int n, int H, int T) {
+    XLayout L{};
+    int o = 0;
+    const int R = 8;  // DEC_ROWS
+    L.x1 = o; o += R * n;
+    L.x2 = o; o += R * n;
+    L.x3 = o; o += R * n;
+    L.q = o; o += R * n / 2;
+    L.k = o; o += R * n / 2;
+    L.v = o; o += R * n / 2;
+    L.o = o; o += R * n / 2;
+    L.xq = o; o += R * n / 2;
+    L.oc = o; o += R * n / 2;
+    L.h = o; o += R * 2 * n;
+    L.s = o; o += R * H * T;
+    L.m = o; o += PX_TASKS;
+    L.p = o; o += PX_TASKS * 64;
+    L.a = o; o += R * PX_GMAX * 2;
+    L.ctl = o; o += 16;             // ctl[0] low word: abort flag
+    L.total = (o + 15) / 16 * 16;   // whole 128-byte lines (memset size a multiple of 16 B)
+    return L;
+}
+
+struct PersistArgs {
+    const PersistLayer *layers;  // device array [L]
+    const uint16_t *te;          // token embedding [V][n]
+    const float *pe;             // positional embedding [n_text_ctx][n]
+    const float *dln_w, *dln_b;  // final LayerNorm
+    const uint16_t *gelu_tab;    // ggml GELU table [65536]
+    const uint16_t *exp_tab;     // ggml exp table, non-positive half [n_exp]
+    int n_exp;
+    uint16_t *kcache, *vcache;   // [L][DEC_ROWS][tctx][n]
+    const uint16_t *ck, *cv;     // cross K/V [L][Bt][T][n]; row b uses clip b0 + b
+    int L, n, V, B, T, tctx, Bt, b0;
+    int nch, cl;                 // cross-attention chunks per (row, head), keys per chunk
+    float qscale;                // (n / H)^-0.25
+    DecState *st;                // pos advanced by n_steps at the end
+    const int32_t *feed;         // [B][feed_stride] prompt tokens
+    int feed_len, feed_stride;
+    int32_t *tokens_out;         // [B][out_stride] generated tokens (index pos - feed_len)
+    int out_stride;
+    int32_t *cur_tok;            // [8] last argmax, carried to the next launch
+    int suppress_id;
+    int n_steps;
+    uint64_t *xg;                // exchange block (persist_layout), zeroed before a run
+    uint32_t *err;               // bit 3: exchange timeout
+    unsigned long long *ptrace;  // WMI_PTRACE: [n_steps][L + 1][16][2] phase-end clocks, or null
+};
+hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G);
+// the persistent decoder's exp vs the host ggml table, every non-positive f16 input
+hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *mismatch);
+// largest co-resident grid for the model (0: not supported for this n / B / T)
+int persist_grid(int device, int n, int B, int T);
+
 }  // namespace wmi

@@ -1,0 +1,934 @@
+// wmi_persist.hip — the whole greedy decoder step as ONE
+// persistent launch that runs n_steps steps back to back.
+//
+// Why: a base decoder step is ~40 dependent operations on ~110 MB that sits in
+// the 256 MiB Infinity Cache; as a chain of kernels every seam costs a kernel
+// boundary plus the next kernel's cold start (236 us per step in round 1 for a
+// 14 us byte roofline).  Here all workgroups stay resident (one per CU) and a
+// seam is an all-to-all hand-off of epoch-tagged 8-byte granules {tag, value}:
+// the producer stores them write-through (agent-scope relaxed store = `sc1`),
+// the consumer re-reads them with `sc1` loads until every tag matches
+// (MI355X_MICROARCH.md, Valid forms, R2 granules; cdna_hip_programming.md
+// Guideline 16).  Each phase issues its weight loads BEFORE it polls for its
+// input, so the weight stream of a phase overlaps the seam in front of it.
+//
+// Phases of one decoder layer l (rows b < B <= 8; tag = epoch of the phase):
+//   A  LN1(x) -> Wqkv rows (all WGs)            -> q, k, v granules + KV cache
+//   B  self-attention per (b, head)              -> o (f16 pairs)
+//   C  Wo rows + residual                        -> x'
+//   D  LNc(x') -> Wcq rows                       -> cross q (f16 pairs)
+//   E  cross scores per (b, head, key chunk)     -> scores, chunk max
+//   F  exact softmax (global max, double sum) + P16.V per chunk -> partials
+//   G1 chunk partials summed in order per (b, head) -> cross o (f16 pairs)
+//   G2 Wco rows + residual                       -> x''
+//   H  LN2(x'') -> W0 rows -> GELU               -> hidden (f16 pairs)
+//   I  W1 rows + residual                        -> x''' (next layer's x)
+// then LN_final -> vocabulary rows -> per-WG argmax -> every WG reduces the
+// G candidates -> next token -> embedding (te[tok] + pe[pos]).
+//
+// Numerics are the decoder chain's (wmi_kernels.hip k_dec_*): the same f16
+// rounding points, double LayerNorm statistics, ggml exp/GELU tables, exact
+// softmax; only the grouping of f32 partial sums of the cross-attention
+// differs (key chunks of cl keys instead of 128).
+#include <hip/hip_runtime.h>
+
+#include "wmi_device.h"
+#include "wmi_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace wmi {
+namespace {
+
+constexpr int PT = 256;                 // threads per workgroup
+constexpr uint32_t PSPIN = 1u << 19;    // polls before a seam is declared dead
+constexpr int NPH = 10;                 // phases per decoder layer
+constexpr int PMAXB = 8;                // decoder rows
+constexpr int RNMAX = 16;               // rows of an n-row GEMV per workgroup
+constexpr int SCR_BYTES = 24 * 1024;    // attention / argmax scratch in LDS
+constexpr int NKP = 4;                  // 128-key passes per cross-attention chunk (cl <= 512)
+
+__device__ __forceinline__ uint64_t gld(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gput(uint64_t *p, uint32_t tag, uint32_t v) {
+    __hip_atomic_store(p, ((uint64_t)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld32(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st32(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+    return (uint32_t)f2h_bits(a) | ((uint32_t)f2h_bits(b) << 16);
+}
+// tags: unique per (position, layer, phase) within a decode run; 0 = never written
+__device__ __forceinline__ uint32_t ptag(int pos, int L, int l, int ph) {
+    return (uint32_t)(pos * (L * NPH + 2) + l * NPH + ph + 1);
+}
+__device__ __forceinline__ uint32_t atag(int pos, int L) { return (uint32_t)(pos * (L * NPH + 2) + L * NPH + 1); }
+
+// 16-byte write-through-coherent load (buffer_load_dwordx4 ... sc1): KV-cache
+// rows written earlier in this launch by other workgroups
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ half8 bload_sc1(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+    const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16);
+    return __builtin_bit_cast(half8, v);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+struct PShared {
+    float xres[PMAXB][RNMAX];   // this workgroup's rows of the residual stream
+    int32_t tok[PMAXB];
+    float redf[4];
+    double redd[4];
+    unsigned long long best[4][PMAXB];
+    float ored[4][64];
+    int abort_;
+};
+
+// Poll cnt granules (granule i at addr(i)) until every tag equals `tag`,
+// storing the values to dst[i] (LDS).  Bounded: a dead seam sets the abort
+// word (every poller checks it) and err bit 3, so the grid always drains.
+template <typename F>
+__device__ __forceinline__ bool gpoll(int cnt, uint32_t tag, F addr, uint32_t *dst, uint32_t *abortw, uint32_t *err) {
+    bool ok = true;
+    int tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    constexpr int PU = 4;  // granules in flight per thread
+    for (int base = tid; base < cnt && ok; base += PT * PU) {
+        uint64_t v[PU];
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            const int i = base + PT * u;
+            v[u] = i < cnt ? gld(addr(i)) : ((uint64_t)tag << 32);
+        }
+        for (uint32_t it = 0;; ++it) {
+            bool all = true;
+#pragma unroll
+            for (int u = 0; u < PU; ++u)
+                if ((uint32_t)(v[u] >> 32) != tag) {
+                    all = false;
+                    v[u] = gld(addr(base + PT * u));
+                }
+            if (all) break;
+            if ((it & 15) == 15) {
+                if (ld32(abortw)) { ok = false; break; }
+                if (it > PSPIN) {
+                    st32(abortw, 1u);
+                    atomicOr(err, 8u);
+                    ok = false;
+                    break;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            const int i = base + PT * u;
+            if (i < cnt) dst[i] = (uint32_t)v[u];
+        }
+    }
+    return ok;
+}
+
+// ---- GEMV over this workgroup's rows: quarter-wave (16 lanes) per row, row
+// slot = wave * 4 + quarter; pass p covers rows rb + 16 p + slot.  Lane l16
+// holds K chunks c * 128 + l16 * 8 (8 f16 each), the decoder chain's layout.
+template <int KCH, int NP>
+struct WSet {
+    half8 w[NP][KCH];
+    float bias[NP];
+};
+
+template <int KCH, int NP>
+__device__ __forceinline__ void wset_load(WSet<KCH, NP> &S, const uint16_t *W, const float *bias, int K, int rb, int r1,
+                                          int slot, int l16) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        int row = rb + 16 * p + slot;
+        row = row < r1 ? row : r1 - 1;  // clamped: every load unconditional
+        row = row > 0 ? row : 0;
+        const f16 *wr = (const f16 *)W + (int64_t)row * K + l16 * 8;
+#pragma unroll
+        for (int c = 0; c < KCH; ++c) S.w[p][c] = *(const half8 *)(wr + c * 128);
+        S.bias[p] = bias ? bias[row] : 0.0f;
+    }
+}
+
+// epi(row, b, v, bias, valid) is called by EVERY lane (pairing shuffles);
+// lane l16 carries the reduced value of row `row` for decoder row b = l16
+template <int KCH, int NP, typename Epi>
+__device__ __forceinline__ void wset_dot(const WSet<KCH, NP> &S, const f16 *xs, int K, int B, int rb, int r1, int slot,
+                                         int l16, Epi &&epi) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        if (rb + 16 * p >= r1) break;  // workgroup-uniform
+        const int row = rb + 16 * p + slot;
+        float acc[PMAXB];
+#pragma unroll
+        for (int b = 0; b < PMAXB; ++b) acc[b] = 0.0f;
+#pragma unroll
+        for (int c = 0; c < KCH; ++c)
+#pragma unroll
+            for (int b = 0; b < PMAXB; ++b)
+                if (b < B) acc[b] = dot8(S.w[p][c], *(const half8 *)(xs + b * K + c * 128 + l16 * 8), acc[b]);
+        float v = 0.0f;
+#pragma unroll
+        for (int b = 0; b < PMAXB; ++b)
+            if (b < B) {
+                float t = acc[b];
+                t += __shfl_xor(t, 8);
+                t += __shfl_xor(t, 4);
+                t += __shfl_xor(t, 2);
+                t += __shfl_xor(t, 1);
+                if (l16 == b) v = t;
+            }
+        epi(row, l16, v, S.bias[p], row < r1 && l16 < B);
+    }
+}
+
+// LayerNorm (ggml norm: double mean / variance, eps 1e-5; then * w + b) of
+// rows b < B of xf [B][NS] into xs [B][NS] f16 — wave w takes rows w, w + 4
+template <int NS>
+struct LnP {
+    static constexpr int V = (NS + 255) / 256;
+    float4 w[V], b[V];
+};
+template <int NS>
+__device__ __forceinline__ void ln_params(const float *lw, const float *lb, LnP<NS> &P, int lane) {
+#pragma unroll
+    for (int i = 0; i < LnP<NS>::V; ++i) {
+        const int e = (lane + 64 * i) * 4, ec = e < NS ? e : 0;
+        P.w[i] = *(const float4 *)(lw + ec);
+        P.b[i] = *(const float4 *)(lb + ec);
+    }
+}
+template <int NS>
+__device__ __forceinline__ void ln_rows(const float *xf, const LnP<NS> &P, f16 *xs, int B, int w, int lane) {
+    constexpr int LV = LnP<NS>::V;
+    for (int b = w; b < B; b += 4) {
+        float4 xv[LV];
+#pragma unroll
+        for (int i = 0; i < LV; ++i) {
+            const int e = (lane + 64 * i) * 4;
+            xv[i] = e < NS ? *(const float4 *)(xf + b * NS + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        double s1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < LV; ++i)
+            if ((lane + 64 * i) * 4 < NS)
+                s1 += ((double)xv[i].x + (double)xv[i].y) + ((double)xv[i].z + (double)xv[i].w);
+        s1 = wave_sum(s1);
+        const double mean = s1 / NS;
+        double s2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < LV; ++i)
+            if ((lane + 64 * i) * 4 < NS) {
+                const double d0 = (double)xv[i].x - mean, d1 = (double)xv[i].y - mean;
+                const double d2 = (double)xv[i].z - mean, d3 = (double)xv[i].w - mean;
+                s2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+            }
+        s2 = wave_sum(s2);
+        const float scale = (float)(1.0 / sqrt(s2 / NS + (double)1e-5f));
+#pragma unroll
+        for (int i = 0; i < LV; ++i) {
+            const int e = (lane + 64 * i) * 4;
+            if (e < NS) {
+                const float xx[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+                const float ww[4] = {P.w[i].x, P.w[i].y, P.w[i].z, P.w[i].w};
+                const float bb[4] = {P.b[i].x, P.b[i].y, P.b[i].z, P.b[i].w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float t = (float)((double)xx[u] - mean) * scale;
+                    xs[b * NS + e + u] = (f16)(bb[u] + ww[u] * t);
+                }
+            }
+        }
+    }
+}
+
+// ggml's table_exp_f16 value f16(exp(double(f16 x))) for x <= 0 without a
+// double exp (whose polynomial constants the compiler would keep live in
+// registers across the whole persistent loop): the f32 exp rounds to the same
+// f16 unless it lies within 4 f32 ulps of an f16 rounding midpoint — 16 of the
+// 31744 non-positive inputs (checked exhaustively on the host) — and those
+// read the host-built table.
+__device__ __forceinline__ float exp_f16_fast(float arg, const uint16_t *tab, int n_exp) {
+    const f16 hx = (f16)arg;
+    const float r = expf((float)hx);
+    const uint16_t hr = f2h_bits(r);
+    const float hv = h2f_bits(hr);
+    const float nb = h2f_bits(r >= hv ? (uint16_t)(hr + 1) : (uint16_t)(hr - 1));
+    const float mid = 0.5f * (hv + nb);
+    const float ulp = __uint_as_float(__float_as_uint(r) & 0x7f800000u) * 1.1920928955078125e-7f;
+    if (fabsf(r - mid) > 4.0f * ulp) return hv;
+    const int j = __builtin_bit_cast(uint16_t, hx) & 0x7fff;
+    return j < n_exp ? h2f_bits(tab[j]) : 0.0f;
+}
+
+// Every phase re-derives its lane indices from an opaque copy of threadIdx.x
+// behind a compiler memory barrier: __syncthreads() fences only LDS, so
+// without it the compiler hoists later phases' weight loads and lane
+// addresses into earlier phases and keeps all of them live at once (512
+// VGPRs and scratch spills for phases that each need < 256).
+#define PHASE_IDS                                                                              \
+    int tid = (int)threadIdx.x;                                                                \
+    asm volatile("" : "+v"(tid) : : "memory");                                                 \
+    const int lane = tid & 63, w = tid >> 6, q = lane >> 4, l16 = lane & 15, slot = w * 4 + q; \
+    (void)q; (void)l16; (void)slot;
+
+// WMI_PTRACE: thread 0 of workgroups 0 and G / 2 stamps the 100 MHz device
+// clock at the end of every phase of the first launch (host prints averages)
+#define PSTAMP(ph)                                                                                    \
+    if (a.ptrace && threadIdx.x == 0 && (wg == 0 || wg == G / 2))                                     \
+        a.ptrace[(((int64_t)step * (L + 1) + (ph) / 16) * 16 + ((ph) & 15)) * 2 + (wg == 0 ? 0 : 1)] = \
+            __builtin_amdgcn_s_memrealtime();
+
+template <int NS>
+__global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
+    constexpr int KC = NS / 128;        // 128-element chunks of a K = n row
+    constexpr int H = NS / 64;
+    constexpr int NPL = KC <= 4 ? 2 : 1;  // logits passes per register set
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ PShared sh;
+    const int B = a.B, G = gridDim.x, wg = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int L = a.L, T = a.T, tctx = a.tctx, nch = a.nch, CL = a.cl;
+    float *xf = (float *)smem;                                          // [B][NS] f32
+    f16 *xs = (f16 *)(smem + (size_t)B * NS * 4);                       // [B][4 NS] f16
+    unsigned char *scr = smem + (size_t)B * NS * 4 + (size_t)B * NS * 8;  // SCR_BYTES
+    // exchange offsets as plain scalars (a struct captured by the lambdas
+    // below would be kept in scratch memory)
+    int oX1, oX2, oX3, oQ, oK, oV, oO, oXQ, oOC, oH, oS, oM, oP, oA;
+    {
+        const XLayout X = persist_layout(NS, H, T);
+        oX1 = X.x1; oX2 = X.x2; oX3 = X.x3; oQ = X.q; oK = X.k; oV = X.v; oO = X.o; oXQ = X.xq;
+        oOC = X.oc; oH = X.h; oS = X.s; oM = X.m; oP = X.p; oA = X.a;
+    }
+    uint64_t *xg = a.xg;
+    uint32_t *abortw = (uint32_t *)(xg + persist_layout(NS, H, T).ctl);
+    const float qs = a.qscale;
+    // row partitions (f16-pair outputs need even row starts)
+    auto part = [&](int N, bool even, int &r0, int &r1) {
+        int rpw = (N + G - 1) / G;
+        if (even) rpw = (rpw + 1) & ~1;
+        r0 = wg * rpw < N ? wg * rpw : N;
+        r1 = r0 + rpw < N ? r0 + rpw : N;
+    };
+    int rn0, rn1, ra0, ra1, rh0, rh1, rv0, rv1;
+    part(NS, true, rn0, rn1);      // Wo / Wcq / Wco / W1 rows = this WG's residual rows
+    part(3 * NS, true, ra0, ra1);  // Wqkv rows
+    part(4 * NS, true, rh0, rh1);  // W0 rows
+    part(a.V, false, rv0, rv1);    // vocabulary rows
+    const int rn = rn1 - rn0;
+    if (tid == 0) sh.abort_ = 0;
+    __syncthreads();
+    auto check = [&](bool ok) -> bool {  // workgroup-uniform abort after a poll
+        if (!ok) sh.abort_ = 1;
+        __syncthreads();
+        return sh.abort_ != 0;
+    };
+    auto ptr_u64 = [](uint64_t *base) { return [base](int i) { return base + i; }; };
+
+    // every workgroup reduces the G per-workgroup argmax candidates of the
+    // logits at position pp: sh.tok[b]
+    auto argmax_gather = [&](int pp) -> bool {
+        uint32_t *ga = (uint32_t *)scr;  // [B][G][2]
+        const bool ok = gpoll(B * G * 2, atag(pp, L), ptr_u64(xg + oA), ga, abortw, a.err);
+        if (check(ok)) return false;
+        for (int b = 0; b < B; ++b) {
+            unsigned long long k = 0ull;
+            if (tid < G) k = ((unsigned long long)ga[(b * G + tid) * 2] << 32) | ga[(b * G + tid) * 2 + 1];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const unsigned long long t = __shfl_xor(k, o);
+                k = t > k ? t : k;
+            }
+            if (lane == 0) sh.best[w][b] = k;
+        }
+        __syncthreads();
+        if (tid < B) {
+            unsigned long long k = sh.best[0][tid];
+            for (int i = 1; i < 4; ++i) k = sh.best[i][tid] > k ? sh.best[i][tid] : k;
+            sh.tok[tid] = (int32_t)(0xffffffffu - (uint32_t)(k & 0xffffffffull));
+        }
+        __syncthreads();
+        return true;
+    };
+
+    int pos = a.st->pos;
+    for (int step = 0; step < a.n_steps; ++step, ++pos) {
+        for (int l = 0; l < L; ++l) {
+            const PersistLayer &P = a.layers[l];
+            uint16_t *kc = a.kcache + (size_t)l * DEC_ROWS * tctx * NS;
+            uint16_t *vc = a.vcache + (size_t)l * DEC_ROWS * tctx * NS;
+
+            // ---- A: LN1 + QKV rows ------------------------------------
+            {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 0);
+                WSet<KC, 2> S;
+                const bool act = ra0 < ra1;
+                wset_load(S, P.wqkv, P.bqkv, NS, ra0, ra1, slot, l16);
+                LnP<NS> lp;
+                ln_params<NS>(P.ln1_w, P.ln1_b, lp, lane);
+                __syncthreads();
+                if (l == 0) {
+                    const bool fed = pos < a.feed_len;
+                    if (fed) {
+                        if (tid < B) sh.tok[tid] = a.feed[tid * a.feed_stride + pos];
+                        __syncthreads();
+                    } else if (step == 0) {
+                        if (tid < B) sh.tok[tid] = a.cur_tok[tid];
+                        __syncthreads();
+                    } else {
+                        if (!argmax_gather(pos - 1)) return;
+                        if (wg == 0 && tid < B && pos - a.feed_len < a.out_stride)
+                            a.tokens_out[tid * a.out_stride + (pos - a.feed_len)] = sh.tok[tid];
+                    }
+                    // x = te[tok] + pe[pos]  (get_rows f16 -> f32, add)
+                    for (int i = tid; i < B * NS / 4; i += PT) {
+                        const int b = (i * 4) / NS, e = i * 4 - b * NS;
+                        const half4 tv = *(const half4 *)((const f16 *)a.te + (int64_t)sh.tok[b] * NS + e);
+                        const float4 pv = *(const float4 *)(a.pe + (int64_t)pos * NS + e);
+                        *(float4 *)(xf + b * NS + e) = make_float4((float)tv[0] + pv.x, (float)tv[1] + pv.y,
+                                                                   (float)tv[2] + pv.z, (float)tv[3] + pv.w);
+                    }
+                } else {
+                    const bool ok = gpoll(B * NS, ptag(pos, L, l - 1, 9), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
+                    if (check(ok)) return;
+                }
+                __syncthreads();
+                for (int i = tid; i < B * rn; i += PT) {
+                    const int b = i / rn, r = i - b * rn;
+                    sh.xres[b][r] = xf[b * NS + rn0 + r];
+                }
+                ln_rows<NS>(xf, lp, xs, B, w, lane);
+                __syncthreads();
+                if (act)
+                    wset_dot(S, xs, NS, B, ra0, ra1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                        const float vn = __shfl_down(v, 16), ebn = __shfl_down(eb, 16);
+                        if (!valid || (q & 1)) return;
+                        const int which = row / NS, c = row - which * NS;
+                        uint32_t pk;
+                        if (which == 0) pk = pack2((v + eb) * qs, (vn + ebn) * qs);
+                        else if (which == 1) pk = pack2(v * qs, vn * qs);
+                        else pk = pack2(eb + v, ebn + vn);
+                        const int64_t gi = (which == 0 ? oQ : which == 1 ? oK : oV) + b * (NS / 2) + c / 2;
+                        if (which > 0)
+                            st32((uint32_t *)((which == 1 ? kc : vc) + ((int64_t)b * tctx + pos) * NS + c), pk);
+                        gput(xg + gi, tag, pk);
+                    });
+            }
+
+            PSTAMP(l * 16 + 0)
+            // ---- B: self-attention per (row, head) ---------------------
+            {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 1);
+                const int M = pos + 1;
+                const __amdgpu_buffer_rsrc_t rk = rsrc_of(kc, (uint32_t)(DEC_ROWS * tctx * NS * 2));
+                const __amdgpu_buffer_rsrc_t rv = rsrc_of(vc, (uint32_t)(DEC_ROWS * tctx * NS * 2));
+                f16 *qn = (f16 *)scr, *kn = qn + 64, *vn = qn + 128;  // this step's q, k, v of the head
+                uint16_t *P16 = (uint16_t *)(scr + 512);                 // [512]
+                for (int t = wg; t < B * H; t += G) {
+                    const int b = t / H, h = t - b * H;
+                    const int doct = tid & 7, jg = tid >> 3;
+                    // cache rows j < pos (this step's row comes from the granules)
+                    half8 kv[2][8];
+                    // (every register array is loaded unconditionally, rows
+                    // clamped: a conditionally-defined array becomes an undef
+                    // value carried around the step loop and stays live across
+                    // every other phase)
+                    const int jmax = pos > 0 ? pos - 1 : 0;
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        const int j = min(tid + 256 * r, jmax);
+                        const uint32_t off = (uint32_t)((((int64_t)b * tctx + j) * NS + h * 64) * 2);
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) kv[r][i] = bload_sc1(rk, off + 16 * i);
+                    }
+                    __syncthreads();
+                    const int64_t hq = b * (NS / 2) + h * 32;  // q, k, v granule blocks lie 4 NS apart
+                    const bool ok = gpoll(96, ptag(pos, L, l, 0),
+                                          [=](int i) { return xg + oQ + (i >> 5) * (4 * NS) + hq + (i & 31); },
+                                          (uint32_t *)qn, abortw, a.err);
+                    if (check(ok)) return;
+                    float sc[2];
+                    float mx = -INFINITY;
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        const int j = tid + 256 * r;
+                        float s = 0.0f;
+                        if (j < pos) {
+#pragma unroll
+                            for (int i = 0; i < 8; ++i) s = dot8(kv[r][i], *(const half8 *)(qn + 8 * i), s);
+                        } else if (j == pos) {
+#pragma unroll
+                            for (int i = 0; i < 8; ++i) s = dot8(*(const half8 *)(kn + 8 * i), *(const half8 *)(qn + 8 * i), s);
+                        }
+                        sc[r] = s;
+                        if (j < M) mx = fmaxf(mx, s);
+                    }
+                    // value rows (the key registers are dead now): in flight
+                    // while the softmax runs
+                    asm volatile("" : "+v"(sc[0]), "+v"(sc[1]), "+v"(mx) : : "memory");
+                    half8 vv[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int j = min(jg + 32 * i, jmax);
+                        vv[i] = bload_sc1(rv, (uint32_t)((((int64_t)b * tctx + j) * NS + h * 64 + doct * 8) * 2));
+                    }
+                    mx = wave_max(mx);
+                    if (lane == 0) sh.redf[w] = mx;
+                    __syncthreads();
+                    mx = fmaxf(fmaxf(sh.redf[0], sh.redf[1]), fmaxf(sh.redf[2], sh.redf[3]));
+                    double sum = 0.0;
+                    float p[2];
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        p[r] = 0.0f;
+                        if (tid + 256 * r < M) {
+                            p[r] = exp_f16_fast(sc[r] - mx, a.exp_tab, a.n_exp);
+                            sum += (double)p[r];
+                        }
+                    }
+                    sum = wave_sum(sum);
+                    if (lane == 0) sh.redd[w] = sum;
+                    __syncthreads();
+                    const float inv = (float)(1.0 / (((sh.redd[0] + sh.redd[1]) + sh.redd[2]) + sh.redd[3]));
+#pragma unroll
+                    for (int r = 0; r < 2; ++r)
+                        if (tid + 256 * r < M) P16[tid + 256 * r] = f2h_bits(p[r] * inv);
+                    __syncthreads();
+                    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int j = jg + 32 * i;
+                        if (j < M) {
+                            const float pj = h2f_bits(P16[j]);
+                            const half8 vr = j < pos ? vv[i] : *(const half8 *)(vn + doct * 8);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vr[e];
+                        }
+                    }
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        o[e] += __shfl_xor(o[e], 8);
+                        o[e] += __shfl_xor(o[e], 16);
+                        o[e] += __shfl_xor(o[e], 32);
+                    }
+                    if (lane < 8)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) sh.ored[w][lane * 8 + e] = o[e];
+                    __syncthreads();
+                    if (tid < 32) {
+                        const int d = 2 * tid;
+                        const float o0 = ((sh.ored[0][d] + sh.ored[1][d]) + sh.ored[2][d]) + sh.ored[3][d];
+                        const float o1 = ((sh.ored[0][d + 1] + sh.ored[1][d + 1]) + sh.ored[2][d + 1]) + sh.ored[3][d + 1];
+                        gput(xg + oO + b * (NS / 2) + h * 32 + tid, tag, pack2(o0, o1));
+                    }
+                }
+            }
+
+            PSTAMP(l * 16 + 1)
+            // ---- C: Wo rows + residual -> x' ---------------------------
+            {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 2);
+                WSet<KC, 1> S;
+                const bool act = rn0 < rn1;
+                wset_load(S, P.wo, P.bo, NS, rn0, rn1, slot, l16);
+                __syncthreads();
+                const bool ok = gpoll(B * NS / 2, ptag(pos, L, l, 1), ptr_u64(xg + oO), (uint32_t *)xs, abortw, a.err);
+                if (check(ok)) return;
+                if (act)
+                    wset_dot(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                        if (!valid) return;
+                        const float x = (v + eb) + sh.xres[b][row - rn0];
+                        sh.xres[b][row - rn0] = x;
+                        gput(xg + oX2 + b * NS + row, tag, __float_as_uint(x));
+                    });
+            }
+
+            PSTAMP(l * 16 + 2)
+            // ---- D: LNc(x') + Wcq rows -> cross q ------------------------
+            {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 3);
+                WSet<KC, 1> S;
+                const bool act = rn0 < rn1;
+                wset_load(S, P.wcq, P.bcq, NS, rn0, rn1, slot, l16);
+                LnP<NS> lp;
+                ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
+                __syncthreads();
+                const bool ok = gpoll(B * NS, ptag(pos, L, l, 2), ptr_u64(xg + oX2), (uint32_t *)xf, abortw, a.err);
+                if (check(ok)) return;
+                ln_rows<NS>(xf, lp, xs, B, w, lane);
+                __syncthreads();
+                if (act)
+                    wset_dot(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                        const float vn = __shfl_down(v, 16), ebn = __shfl_down(eb, 16);
+                        if (!valid || (q & 1)) return;
+                        gput(xg + oXQ + b * (NS / 2) + row / 2, tag, pack2((v + eb) * qs, (vn + ebn) * qs));
+                    });
+            }
+
+            PSTAMP(l * 16 + 3)
+            // ---- E: cross scores per (row, head, key chunk) ----------------
+            {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 4);
+                f16 *qh = (f16 *)scr;
+                const int ntask = B * H * nch;
+                for (int t = wg; t < ntask; t += G) {
+                    const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
+                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
+                    const f16 *Kb = (const f16 *)a.ck + ((int64_t)l * a.Bt + a.b0 + b) * T * NS + h * 64 + (tid & 1) * 32;
+                    half8 kf[NKP][4];
+#pragma unroll
+                    for (int p = 0; p < NKP; ++p) {
+                        int key = j0 + 128 * p + (tid >> 1);
+                        key = key < j1 ? key : j1 - 1;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) kf[p][i] = *(const half8 *)(Kb + (int64_t)key * NS + 8 * i);
+                    }
+                    __syncthreads();
+                    const bool ok = gpoll(32, ptag(pos, L, l, 3), [=](int i) { return xg + oXQ + b * (NS / 2) + h * 32 + i; },
+                                          (uint32_t *)qh, abortw, a.err);
+                    if (check(ok)) return;
+                    float m = -INFINITY;
+#pragma unroll
+                    for (int p = 0; p < NKP; ++p)
+                        if (j0 + 128 * p < j1) {
+                            const int key = j0 + 128 * p + (tid >> 1);
+                            float s = 0.0f;
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) s = dot8(kf[p][i], *(const half8 *)(qh + (tid & 1) * 32 + 8 * i), s);
+                            s += __shfl_xor(s, 1);
+                            if (key < j1) {
+                                if ((tid & 1) == 0) gput(xg + oS + (int64_t)bh * T + key, tag, __float_as_uint(s));
+                                m = fmaxf(m, s);
+                            }
+                        }
+                    m = wave_max(m);
+                    if (lane == 0) sh.redf[w] = m;
+                    __syncthreads();
+                    if (tid == 0)
+                        gput(xg + oM + t, tag,
+                             __float_as_uint(fmaxf(fmaxf(sh.redf[0], sh.redf[1]), fmaxf(sh.redf[2], sh.redf[3]))));
+                }
+            }
+
+            PSTAMP(l * 16 + 4)
+            // ---- F: exact softmax + P16.V partial per chunk ----------------
+            {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 5);
+                float *cm = (float *)scr;          // [nch]  (nch <= 64)
+                float *Sv = cm + 64;               // [T]    scores, then p
+                const int ntask = B * H * nch;
+                for (int t = wg; t < ntask; t += G) {
+                    const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
+                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
+                    const int doct = tid & 7, jg = tid >> 3;
+                    const f16 *Vb = (const f16 *)a.cv + ((int64_t)l * a.Bt + a.b0 + b) * T * NS + h * 64 + doct * 8;
+                    half8 vf[NKP][4];
+#pragma unroll
+                    for (int p = 0; p < NKP; ++p)
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            int key = j0 + 128 * p + jg * 4 + u;
+                            key = key < j1 ? key : j1 - 1;
+                            vf[p][u] = *(const half8 *)(Vb + (int64_t)key * NS);
+                        }
+                    __syncthreads();
+                    const uint32_t tg = ptag(pos, L, l, 4);
+                    const bool ok = gpoll(nch + T, tg,
+                                          [=](int i) {
+                                              return i < nch ? xg + oM + (int64_t)bh * nch + i
+                                                             : xg + oS + (int64_t)bh * T + (i - nch);
+                                          },
+                                          (uint32_t *)cm, abortw, a.err);
+                    // (cm[0..nch) then the scores: Sv = cm + nch; moved below)
+                    if (check(ok)) return;
+                    float *Sx = cm + nch;
+                    float m = cm[0];
+                    for (int i = 1; i < nch; ++i) m = fmaxf(m, cm[i]);
+                    double sum = 0.0;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int j = tid + 256 * u;
+                        if (j < T) {
+                            const float pj = exp_f16_fast(Sx[j] - m, a.exp_tab, a.n_exp);
+                            sum += (double)pj;
+                            Sx[j] = pj;
+                        }
+                    }
+                    sum = wave_sum(sum);
+                    if (lane == 0) sh.redd[w] = sum;
+                    __syncthreads();
+                    const float inv = (float)(1.0 / (((sh.redd[0] + sh.redd[1]) + sh.redd[2]) + sh.redd[3]));
+                    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int p = 0; p < NKP; ++p)
+                        if (j0 + 128 * p < j1)
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const int key = j0 + 128 * p + jg * 4 + u;
+                                if (key < j1) {
+                                    const float pj = h2f_bits(f2h_bits(Sx[key] * inv));
+#pragma unroll
+                                    for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vf[p][u][e];
+                                }
+                            }
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        o[e] += __shfl_xor(o[e], 8);
+                        o[e] += __shfl_xor(o[e], 16);
+                        o[e] += __shfl_xor(o[e], 32);
+                    }
+                    if (lane < 8)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) sh.ored[w][lane * 8 + e] = o[e];
+                    __syncthreads();
+                    if (tid < 64)
+                        gput(xg + oP + (int64_t)t * 64 + tid, tag,
+                             __float_as_uint(((sh.ored[0][tid] + sh.ored[1][tid]) + sh.ored[2][tid]) + sh.ored[3][tid]));
+                    (void)Sv;
+                }
+            }
+
+            PSTAMP(l * 16 + 5)
+            // ---- G1: chunk partials summed in chunk order -> cross o ---------
+            {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 6);
+                float *pp = (float *)scr;  // [nch][64]
+                for (int t = wg; t < B * H; t += G) {
+                    const int b = t / H, h = t - b * H;
+                    __syncthreads();
+                    const bool ok = gpoll(nch * 64, ptag(pos, L, l, 5), ptr_u64(xg + oP + (int64_t)t * nch * 64),
+                                          (uint32_t *)pp, abortw, a.err);
+                    if (check(ok)) return;
+                    if (tid < 64) {
+                        float s = pp[tid];
+                        for (int c = 1; c < nch; ++c) s = s + pp[c * 64 + tid];
+                        sh.ored[0][tid] = s;
+                    }
+                    __syncthreads();
+                    if (tid < 32)
+                        gput(xg + oOC + b * (NS / 2) + h * 32 + tid, tag, pack2(sh.ored[0][2 * tid], sh.ored[0][2 * tid + 1]));
+                }
+            }
+
+            PSTAMP(l * 16 + 6)
+            // ---- G2: Wco rows + residual -> x'' -------------------------
+            {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 7);
+                WSet<KC, 1> S;
+                const bool act = rn0 < rn1;
+                wset_load(S, P.wco, P.bco, NS, rn0, rn1, slot, l16);
+                __syncthreads();
+                const bool ok = gpoll(B * NS / 2, ptag(pos, L, l, 6), ptr_u64(xg + oOC), (uint32_t *)xs, abortw, a.err);
+                if (check(ok)) return;
+                if (act)
+                    wset_dot(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                        if (!valid) return;
+                        const float x = (v + eb) + sh.xres[b][row - rn0];
+                        sh.xres[b][row - rn0] = x;
+                        gput(xg + oX3 + b * NS + row, tag, __float_as_uint(x));
+                    });
+            }
+
+            PSTAMP(l * 16 + 7)
+            // ---- H: LN2(x'') + W0 rows + GELU -> hidden ---------------------
+            {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 8);
+                WSet<KC, 2> S;
+                const bool act = rh0 < rh1;
+                wset_load(S, P.w0, P.b0, NS, rh0, rh1, slot, l16);
+                LnP<NS> lp;
+                ln_params<NS>(P.ln2_w, P.ln2_b, lp, lane);
+                __syncthreads();
+                const bool ok = gpoll(B * NS, ptag(pos, L, l, 7), ptr_u64(xg + oX3), (uint32_t *)xf, abortw, a.err);
+                if (check(ok)) return;
+                ln_rows<NS>(xf, lp, xs, B, w, lane);
+                __syncthreads();
+                if (act)
+                    wset_dot(S, xs, NS, B, rh0, rh1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                        const float vn = __shfl_down(v, 16), ebn = __shfl_down(eb, 16);
+                        if (!valid || (q & 1)) return;
+                        const uint16_t h0 = f2h_bits(v + eb), h1 = f2h_bits(vn + ebn);
+                        const uint16_t g0 = a.gelu_tab[h0], g1 = a.gelu_tab[h1];
+                        gput(xg + oH + b * (2 * NS) + row / 2, tag, (uint32_t)g0 | ((uint32_t)g1 << 16));
+                    });
+            }
+
+            PSTAMP(l * 16 + 8)
+            // ---- I: W1 rows + residual -> next layer's x --------------------
+            {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 9);
+                WSet<4 * KC, 1> S;
+                const bool act = rn0 < rn1;
+                wset_load(S, P.w1, P.b1, 4 * NS, rn0, rn1, slot, l16);
+                __syncthreads();
+                const bool ok = gpoll(B * 2 * NS, ptag(pos, L, l, 8), ptr_u64(xg + oH), (uint32_t *)xs, abortw, a.err);
+                if (check(ok)) return;
+                if (act)
+                    wset_dot(S, xs, 4 * NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                        if (!valid) return;
+                        const float x = (v + eb) + sh.xres[b][row - rn0];
+                        sh.xres[b][row - rn0] = x;
+                        gput(xg + oX1 + b * NS + row, tag, __float_as_uint(x));
+                    });
+            }
+            PSTAMP(l * 16 + 9)
+        }
+
+        // ---- logits: LN_final + vocabulary rows + per-WG argmax -------------
+        {
+                PHASE_IDS
+            WSet<KC, NPL> S0, S1;
+            const bool act = rv0 < rv1;
+            constexpr int RS = 16 * NPL;  // rows per register set
+            wset_load(S0, a.te, nullptr, NS, rv0, rv1, slot, l16);
+            wset_load(S1, a.te, nullptr, NS, rv0 + RS, rv1, slot, l16);
+            LnP<NS> lp;
+            ln_params<NS>(a.dln_w, a.dln_b, lp, lane);
+            __syncthreads();
+            const bool ok = gpoll(B * NS, ptag(pos, L, L - 1, 9), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
+            if (check(ok)) return;
+            ln_rows<NS>(xf, lp, xs, B, w, lane);
+            __syncthreads();
+            unsigned long long best = 0ull;
+            auto epi = [&](int row, int b, float v, float eb, bool valid) {
+                if (!valid || row == a.suppress_id) return;
+                const unsigned long long k =
+                    ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)row);
+                best = k > best ? k : best;
+            };
+            if (act)
+                for (int rb = rv0;;) {
+                    wset_dot(S0, xs, NS, B, rb, rv1, slot, l16, epi);
+                    wset_load(S0, a.te, nullptr, NS, rb + 2 * RS, rv1, slot, l16);
+                    if (rb + RS >= rv1) break;
+                    wset_dot(S1, xs, NS, B, rb + RS, rv1, slot, l16, epi);
+                    wset_load(S1, a.te, nullptr, NS, rb + 3 * RS, rv1, slot, l16);
+                    rb += 2 * RS;
+                    if (rb >= rv1) break;
+                }
+            // lane l16 = b holds its quarter's best: reduce the 4 quarters, then the waves
+            {
+                unsigned long long t = __shfl_xor(best, 16);
+                best = t > best ? t : best;
+                t = __shfl_xor(best, 32);
+                best = t > best ? t : best;
+            }
+            if (lane < PMAXB) sh.best[w][lane] = best;
+            __syncthreads();
+            if (tid < B) {
+                unsigned long long k = sh.best[0][tid];
+                for (int i = 1; i < 4; ++i) k = sh.best[i][tid] > k ? sh.best[i][tid] : k;
+                const uint32_t tg = atag(pos, L);
+                gput(xg + oA + ((int64_t)tid * G + wg) * 2, tg, (uint32_t)(k >> 32));
+                gput(xg + oA + ((int64_t)tid * G + wg) * 2 + 1, tg, (uint32_t)k);
+            }
+        }
+        PSTAMP(L * 16 + 0)
+    }
+    // the last step's token: recorded by workgroup 0 and carried to the next launch
+    if (wg != 0 || a.n_steps < 1) return;
+    __syncthreads();
+    if (!argmax_gather(pos - 1)) return;
+    if (tid < B) {
+        if (pos >= a.feed_len && pos - a.feed_len < a.out_stride) a.tokens_out[tid * a.out_stride + (pos - a.feed_len)] = sh.tok[tid];
+        a.cur_tok[tid] = sh.tok[tid];
+    }
+    if (tid == 0) a.st->pos = pos;
+}
+
+template <int NS>
+size_t persist_lds(int B) {
+    return (size_t)B * NS * 4 + (size_t)B * NS * 8 + SCR_BYTES;
+}
+
+template <int NS>
+hipError_t launch_ns(hipStream_t s, const PersistArgs &a, int G) {
+    const size_t lds = persist_lds<NS>(a.B);
+    hipError_t e = hipFuncSetAttribute((const void *)k_dec_persist<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_dec_persist<NS>, dim3(G), dim3(PT), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int NS>
+int grid_ns(int device, int B) {
+    const size_t lds = persist_lds<NS>(B);
+    if (hipFuncSetAttribute((const void *)k_dec_persist<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+        return 0;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dec_persist<NS>, PT, lds) != hipSuccess || per_cu < 1)
+        return 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
+    const int G = prop.multiProcessorCount < PX_GMAX ? prop.multiProcessorCount : PX_GMAX;
+    // row-partition limits of the register sets (see wset_dot users)
+    if ((3 * NS + G - 1) / G > 31 || (4 * NS + G - 1) / G > 31 || (NS + G - 1) / G > RNMAX - 1) return 0;
+    return G;
+}
+
+// exp_f16_fast against the host-built ggml exp table over every non-positive f16 input
+__global__ void k_persist_selftest(const uint16_t *tab, int n_exp, uint32_t *mismatch) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > 0x7c00) return;
+    const float x = h2f_bits((uint16_t)(0x8000u | (uint32_t)j));
+    const uint16_t got = f2h_bits(exp_f16_fast(x, tab, n_exp));
+    const uint16_t want = j < n_exp ? tab[j] : (uint16_t)0;
+    if (got != want) atomicAdd(mismatch, 1u);
+}
+
+}  // namespace
+
+hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *mismatch) {
+    hipLaunchKernelGGL(k_persist_selftest, dim3((0x7c01 + 255) / 256), dim3(256), 0, s, exp_tab, n_exp, mismatch);
+    return hipGetLastError();
+}
+
+int persist_grid(int device, int n, int B, int T) {
+    if (B < 1 || B > PMAXB || T < 1 || T > 2048) return 0;
+    switch (n) {
+        case 128: return grid_ns<128>(device, B);
+        case 384: return grid_ns<384>(device, B);
+        case 512: return grid_ns<512>(device, B);
+        case 768: return grid_ns<768>(device, B);
+        case 1024: return grid_ns<1024>(device, B);
+        case 1280: return grid_ns<1280>(device, B);
+        default: return 0;
+    }
+}
+
+hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G) {
+    if (G < 1 || G > PX_GMAX || a.B < 1 || a.B > PMAXB || a.T > 2048 || a.nch < 1 || a.nch > 64 ||
+        a.cl > 128 * NKP || (int64_t)a.nch * a.cl < a.T || (int64_t)a.B * (a.n / 64) * a.nch > PX_TASKS ||
+        a.tctx > 512)
+        return hipErrorInvalidValue;
+    switch (a.n) {
+        case 128: return launch_ns<128>(s, a, G);
+        case 384: return launch_ns<384>(s, a, G);
+        case 512: return launch_ns<512>(s, a, G);
+        case 768: return launch_ns<768>(s, a, G);
+        case 1024: return launch_ns<1024>(s, a, G);
+        case 1280: return launch_ns<1280>(s, a, G);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace wmi
