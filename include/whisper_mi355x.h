@@ -219,6 +219,13 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
  * f16 inputs) where the computed value differs from the host-built table. */
 int wmi_selftest(wmi_context *ctx, int32_t *n_mismatch);
 
+/* Debug: copy a device buffer of the last decode into out (min of its size
+ * and bytes).  which: 0 / 1 = the kernel chain's residual-stream buffers
+ * [8][n_text_state] f32, 2 = logits [8][n_vocab] f32 (the persistent
+ * decoder fills them only with WMI_PERSIST_LOGITS=1), 3 = the persistent
+ * decoder's exchange block (8-byte {tag, value} granules). */
+int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes);
+
 /* ---- parity getters (copy device results into caller-owned buffers) --- */
 
 /* ctx.mel (main.rs:1574-1578): [n_mel][n_len] f32. */

@@ -274,11 +274,14 @@ struct wmi_context {
     std::vector<std::string> phase_names = std::vector<std::string>(32);  // phase slots 32.. (layer 0 GEMVs, logits)
     // persistent decoder (wmi_persist.hip): greedy steps in one launch
     bool use_persist = true;          // WMI_PERSIST=0: kernel chain instead
+    bool persist_logits = false;      // WMI_PERSIST_LOGITS=1: also store every step's logits (dlogits)
+    int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
     PersistLayer *d_players = nullptr;
     uint64_t *d_xg = nullptr;         // exchange block (persist_layout at n_audio_ctx)
     size_t xg_bytes = 0;
     int32_t *d_curtok = nullptr;      // [8]
     int persist_G[9] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};  // grid per row count (0: unsupported)
+    int persist_nres[9] = {};                                 // resident vocabulary rows per workgroup
     unsigned long long *d_ptrace = nullptr;  // WMI_PTRACE=1: phase clocks of the first launch of a run
     // dist
     ncclComm_t comm = nullptr;
@@ -1164,7 +1167,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     // base 8 clips), not at large-v3 x 5 beams (12 H^2 B n 4 B = 123 MB a
     // layer; measured 554 -> 498 ms decode unfused)
     const bool fuse_wo = ctx->fuse_wo && (int64_t)H * H * B * n <= ((int64_t)1 << 20);
-    for (int l = 0; l < hp.n_text_layer; ++l) {
+    for (int l = 0; l < ctx->dec_layers; ++l) {
         const DecLayerDev &d = ctx->dec[l];
         uint16_t *kc = ctx->kcache + (size_t)l * DEC_ROWS * hp.n_text_ctx * n;
         uint16_t *vc = ctx->vcache + (size_t)l * DEC_ROWS * hp.n_text_ctx * n;
@@ -1365,7 +1368,7 @@ int run_dec_steps(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride
     return WMI_OK;
 }
 
-size_t hp_ptrace_slots(const wmi_hparams &hp) { return (size_t)hp.n_text_ctx * (hp.n_text_layer + 1) * 16 * 2; }
+size_t hp_ptrace_slots(const wmi_hparams &hp) { return (size_t)hp.n_text_ctx * (hp.n_text_layer + 1) * 32 * 2; }
 
 // WMI_PTRACE: average phase durations of the persistent decoder's first
 // launch (workgroups 0 and G / 2), from the phase-end clocks (100 MHz)
@@ -1374,28 +1377,45 @@ int ptrace_dump(wmi_context *ctx, int steps) {
     std::vector<unsigned long long> t(hp_ptrace_slots(ctx->hp));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     HIPCHK(ctx, hipMemcpy(t.data(), ctx->d_ptrace, t.size() * 8, hipMemcpyDeviceToHost));
-    auto at = [&](int st, int l, int k, int w) { return t[(((size_t)st * (L + 1) + l) * 16 + k) * 2 + w]; };
-    static const char *nm[10] = {"A qkv", "B self", "C wo", "D xq", "E xscore", "F xpv", "G1 xred", "G2 wco", "H mlp0", "I mlp1"};
+    auto at = [&](int st, int l, int k, int w) { return t[(((size_t)st * (L + 1) + l) * 32 + k) * 2 + w]; };
+    static const char *nm[11] = {"A qkv", "B self", "C wo", "D xq", "E xscore", "F xpv", "G1 xred", "G2 wco", "H mlp0", "I mlp1", "logits"};
     for (int w = 0; w < 2; ++w) {
-        double ph[10] = {0}, lg = 0, tot = 0;
+        double ph[11] = {0}, pw[11] = {0}, tot = 0;
         int ns = 0;
         for (int st = 1; st < steps; ++st) {  // step 0 includes the launch
             unsigned long long prev = at(st - 1, L, 0, w);
             const unsigned long long s0 = prev;
-            for (int l = 0; l < L; ++l)
-                for (int k = 0; k < 10; ++k) {
-                    const unsigned long long v = at(st, l, k, w);
-                    ph[k] += (double)(v - prev) * 0.01;
+            for (int l = 0; l <= L; ++l)
+                for (int k = 0; k < (l < L ? 10 : 1); ++k) {
+                    const unsigned long long v = at(st, l, k, w), pd = at(st, l, 16 + k, w);
+                    const int kk = l < L ? k : 10;
+                    ph[kk] += (double)(v - prev) * 0.01;
+                    if (pd) pw[kk] += (double)((long long)pd - (long long)prev) * 0.01;  // phase start -> poll done
                     prev = v;
                 }
-            lg += (double)(at(st, L, 0, w) - prev) * 0.01;
-            tot += (double)(at(st, L, 0, w) - s0) * 0.01;
+            tot += (double)(prev - s0) * 0.01;
             ++ns;
         }
         if (!ns) return WMI_OK;
-        fprintf(stderr, "[wmi ptrace] wg %s: step %.2f us =", w ? "G/2" : "0", tot / ns);
-        for (int k = 0; k < 10; ++k) fprintf(stderr, " %s %.2f", nm[k], ph[k] / ns / L);
-        fprintf(stderr, " (per layer) + logits %.2f\n", lg / ns);
+        double l1 = 0, l2 = 0, l3 = 0;
+        for (int st = 1; st < steps; ++st) {
+            const unsigned long long e = at(st, L - 1, 9, w);
+            l1 += (double)(at(st, L, 1, w) - e) * 0.01;
+            l2 += (double)(at(st, L, 2, w) - e) * 0.01;
+            l3 += (double)(at(st, L, 3, w) - e) * 0.01;
+        }
+        fprintf(stderr, "[wmi ptrace] wg %s: logits LN done %.2f, resident rows done %.2f, streamed rows done %.2f us\n",
+                w ? "G/2" : "0", l1 / ns, l2 / ns, l3 / ns);
+        if (steps > 2) {
+            const double dc = (double)(at(steps - 1, L, 4, w) - at(1, L, 4, w));
+            const double dt = (double)(at(steps - 1, L, 0, w) - at(1, L, 0, w)) * 10e-9;
+            fprintf(stderr, "[wmi ptrace] wg %s: shader clock %.3f GHz\n", w ? "G/2" : "0", dc / dt * 1e-9);
+        }
+        fprintf(stderr, "[wmi ptrace] wg %s: step %.2f us; per phase (per layer) total / until input arrived:\n", w ? "G/2" : "0", tot / ns);
+        for (int k = 0; k < 11; ++k) {
+            const double d = k < 10 ? (double)ns * L : (double)ns;
+            fprintf(stderr, "[wmi ptrace]   %-9s %6.2f / %6.2f\n", nm[k], ph[k] / d, pw[k] / d);
+        }
     }
     return WMI_OK;
 }
@@ -1403,7 +1423,9 @@ int ptrace_dump(wmi_context *ctx, int steps) {
 // grid of the persistent decoder for B rows (0: not supported -> kernel chain)
 int persist_grid_for(wmi_context *ctx, int B) {
     if (!ctx->use_persist || B < 1 || B > 8) return 0;
-    if (ctx->persist_G[B] < 0) ctx->persist_G[B] = persist_grid(ctx->device, ctx->hp.n_text_state, B, ctx->hp.n_audio_ctx);
+    if (ctx->persist_G[B] < 0)
+        ctx->persist_G[B] = persist_grid(ctx->device, ctx->hp.n_text_state, B, ctx->hp.n_audio_ctx, ctx->hp.n_vocab,
+                                         &ctx->persist_nres[B]);
     return ctx->persist_G[B];
 }
 
@@ -1416,7 +1438,7 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     a.layers = ctx->d_players; a.te = ctx->te; a.pe = ctx->d_pe; a.dln_w = ctx->dln_w; a.dln_b = ctx->dln_b;
     a.gelu_tab = ctx->gelu_tab; a.exp_tab = ctx->exp_tab; a.n_exp = ctx->n_exp;
     a.kcache = ctx->kcache; a.vcache = ctx->vcache; a.ck = ctx->ck; a.cv = ctx->cv;
-    a.L = hp.n_text_layer; a.n = n; a.V = hp.n_vocab; a.B = B; a.T = T; a.tctx = hp.n_text_ctx;
+    a.L = ctx->dec_layers; a.n = n; a.V = hp.n_vocab; a.B = B; a.T = T; a.tctx = hp.n_text_ctx;
     a.Bt = ctx->enc_clips; a.b0 = b0;
     // key chunks of 128 keys per (row, head), the chain's chunking (so the
     // cross-attention sums group exactly as k_dec_xattn's, and the result
@@ -1432,6 +1454,8 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     a.tokens_out = ctx->dtokens + (size_t)b0 * out_stride; a.out_stride = out_stride;
     a.cur_tok = ctx->d_curtok; a.suppress_id = suppress_eot ? ctx->sp.eot : -1;
     a.xg = ctx->d_xg; a.err = ctx->derr;
+    a.nres = ctx->persist_nres[B];
+    a.logits_out = ctx->persist_logits ? ctx->dlogits : nullptr;
     return a;
 }
 
@@ -1828,6 +1852,9 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (getenv("WMI_NO_Q5")) ctx->use_q5 = false;
     if (getenv("WMI_NO_FUSE")) ctx->fuse_wo = false;
     if (const char *c = getenv("WMI_PERSIST")) ctx->use_persist = atoi(c) != 0;
+    if (getenv("WMI_PERSIST_LOGITS")) ctx->persist_logits = true;
+    ctx->dec_layers = ctx->hp.n_text_layer;
+    if (const char *c = getenv("WMI_DEC_LAYERS")) ctx->dec_layers = std::max(1, std::min(atoi(c), ctx->hp.n_text_layer));
     if (getenv("WMI_PTRACE")) {
         const size_t nb = (size_t)hp_ptrace_slots(ctx->hp) * 8;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_ptrace, nb));
@@ -2102,9 +2129,18 @@ int wmi_decode_logits(wmi_context *ctx, int clip, const int32_t *tokens, int n_t
     HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * AMAX_SHARDS * 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->dsync, 0, ctx->sync_bytes, ctx->stream));
     const size_t V = ctx->hp.n_vocab;
+    const int G = persist_grid_for(ctx, 1);
+    if (G > 0) HIPCHK(ctx, hipMemsetAsync(ctx->d_xg, 0, ctx->xg_bytes, ctx->stream));
     for (int i = 0; i < n_tokens; ++i) {
-        rc = run_dec_steps(ctx, clip, 1, n_tokens, n_tokens, 0, 1, i, 1);
-        if (rc) return rc;
+        if (G > 0) {  // persistent decoder, one step per launch, logits stored
+            PersistArgs pa = persist_args(ctx, clip, 1, G, n_tokens, n_tokens, 0, 1);
+            pa.n_steps = 1;
+            pa.logits_out = ctx->dlogits;
+            HIPCHK(ctx, launch_dec_persist(ctx->stream, pa, G));
+        } else {
+            rc = run_dec_steps(ctx, clip, 1, n_tokens, n_tokens, 0, 1, i, 1);
+            if (rc) return rc;
+        }
         HIPCHK(ctx, hipMemcpyAsync(logits + (size_t)i * V, ctx->dlogits, V * 4, hipMemcpyDeviceToHost, ctx->stream));
     }
     uint32_t err = 0;
@@ -2344,6 +2380,28 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
         out->alg_bytes = (double)M * n * 2 + N * n * 2 + (double)M * N * 2;
         snprintf(out->name, sizeof out->name, "k_gemm<EPI_CROSSKV>");
     }
+    return WMI_OK;
+}
+
+int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes) {
+    if (!ctx || !out) return WMI_E_INVALID_ARG;
+    const size_t R = DEC_ROWS, n = ctx->hp.n_text_state;
+    const void *src = nullptr;
+    size_t have = 0;
+    switch (which) {
+        case 0: src = ctx->dx; have = R * n * 4; break;
+        case 1: src = ctx->dx2; have = R * n * 4; break;
+        case 2: src = ctx->dlogits; have = R * (size_t)ctx->hp.n_vocab * 4; break;
+        case 3: src = ctx->d_xg; have = ctx->xg_bytes; break;
+        case 4: src = ctx->dq16; have = R * n * 2; break;
+        case 5: src = ctx->dhid16; have = R * 4 * n * 2; break;
+        case 6: src = ctx->kcache; have = (size_t)ctx->hp.n_text_layer * R * ctx->hp.n_text_ctx * n * 2; break;
+        case 7: src = ctx->vcache; have = (size_t)ctx->hp.n_text_layer * R * ctx->hp.n_text_ctx * n * 2; break;
+        case 8: src = ctx->dS; have = R * (size_t)ctx->hp.n_text_head * ctx->s_stride * 4; break;
+        case 9: src = ctx->dopart; have = R * (size_t)ctx->n_chunks_max * n * 4; break;
+        default: return WMI_E_INVALID_ARG;
+    }
+    if (hipMemcpy(out, src, std::min(have, bytes), hipMemcpyDeviceToHost) != hipSuccess) return WMI_E_HIP;
     return WMI_OK;
 }
 

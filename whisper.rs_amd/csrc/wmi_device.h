@@ -30,16 +30,143 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
+// ---- cross-lane exchange without the LDS ------------------------------------
+// __shfl_xor lowers to ds_bpermute_b32, an LDS round trip (~100+ cycles) per
+// butterfly step.  These use DPP (row_ror / quad_perm within 16-lane rows) and
+// gfx950's v_permlane16_swap / v_permlane32_swap across rows.  Every reduction
+// reproduces its __shfl_xor butterfly bit for bit: each step adds (or maxes)
+// the same two values in the same order —
+//   xor 32 / xor 16: the swap hands every lane its partner's value;
+//   xor 8: row_ror 8 IS lane ^ 8 within a 16-lane row;
+//   xor 4 after xor 8: values are symmetric under ^ 8, so row_ror 4 (lane - 4
+//     mod 16) carries the value of lane ^ 4;
+//   xor 2 / xor 1: quad_perm [2,3,0,1] / [1,0,3,2] are exact.
+template <int N>
+__device__ __forceinline__ uint32_t dpp_ror(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x120 + N, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_xor2(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4e, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_xor1(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xb1, 0xf, 0xf, false);
+}
+// {own, partner} in some order for lane ^ 16 / lane ^ 32
+__device__ __forceinline__ void swap16(uint32_t x, uint32_t &a, uint32_t &b) {
+    const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    a = p[0];
+    b = p[1];
+}
+__device__ __forceinline__ void swap32(uint32_t x, uint32_t &a, uint32_t &b) {
+    const auto p = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    a = p[0];
+    b = p[1];
+}
+// value of lane + 16 (rows 0 and 2 receive rows 1 and 3; rows 1 and 3 get junk)
+__device__ __forceinline__ float from_next_row(float v) {
+    uint32_t a, b;
+    swap16(__float_as_uint(v), a, b);
+    return __uint_as_float(b);
+}
+
+struct XSum {
+    __device__ static float op(float a, float b) { return a + b; }
+    __device__ static double op(double a, double b) { return a + b; }
+};
+struct XMax {
+    __device__ static float op(float a, float b) { return fmaxf(a, b); }
+};
+__device__ __forceinline__ uint32_t lo32(double d) { return (uint32_t)__double_as_longlong(d); }
+__device__ __forceinline__ uint32_t hi32(double d) { return (uint32_t)((uint64_t)__double_as_longlong(d) >> 32); }
+__device__ __forceinline__ double mk64(uint32_t hi, uint32_t lo) {
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+template <typename Op, int STEP>
+__device__ __forceinline__ float xstep(float v) {
+    const uint32_t u = __float_as_uint(v);
+    if constexpr (STEP == 32 || STEP == 16) {
+        uint32_t a, b;
+        if constexpr (STEP == 32) swap32(u, a, b);
+        else swap16(u, a, b);
+        return Op::op(__uint_as_float(a), __uint_as_float(b));
+    } else {
+        const uint32_t t = STEP == 8 ? dpp_ror<8>(u) : STEP == 4 ? dpp_ror<4>(u) : STEP == 2 ? dpp_xor2(u) : dpp_xor1(u);
+        return Op::op(v, __uint_as_float(t));
+    }
+}
+template <typename Op, int STEP>
+__device__ __forceinline__ double xstep(double v) {
+    const uint32_t l = lo32(v), h = hi32(v);
+    if constexpr (STEP == 32 || STEP == 16) {
+        uint32_t la, lb, ha, hb;
+        if constexpr (STEP == 32) { swap32(l, la, lb); swap32(h, ha, hb); }
+        else { swap16(l, la, lb); swap16(h, ha, hb); }
+        return Op::op(mk64(ha, la), mk64(hb, lb));
+    } else {
+        const uint32_t tl = STEP == 8 ? dpp_ror<8>(l) : STEP == 4 ? dpp_ror<4>(l) : STEP == 2 ? dpp_xor2(l) : dpp_xor1(l);
+        const uint32_t th = STEP == 8 ? dpp_ror<8>(h) : STEP == 4 ? dpp_ror<4>(h) : STEP == 2 ? dpp_xor2(h) : dpp_xor1(h);
+        return Op::op(v, mk64(th, tl));
+    }
+}
+// sum over the 16 lanes of a row, butterfly order 8, 4, 2, 1
+__device__ __forceinline__ float red16_sum(float v) {
+    v = xstep<XSum, 8>(v);
+    v = xstep<XSum, 4>(v);
+    v = xstep<XSum, 2>(v);
+    return xstep<XSum, 1>(v);
+}
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    v = xstep<XSum, 32>(v);
+    v = xstep<XSum, 16>(v);
+    v = xstep<XSum, 8>(v);
+    v = xstep<XSum, 4>(v);
+    v = xstep<XSum, 2>(v);
+    return xstep<XSum, 1>(v);
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    return v;
+    v = xstep<XMax, 32>(v);
+    v = xstep<XMax, 16>(v);
+    v = xstep<XMax, 8>(v);
+    v = xstep<XMax, 4>(v);
+    v = xstep<XMax, 2>(v);
+    return xstep<XMax, 1>(v);
+}
+// the P.V reduction over key groups: xor 8, then 16, then 32
+__device__ __forceinline__ float red_8_16_32(float v) {
+    v = xstep<XSum, 8>(v);
+    v = xstep<XSum, 16>(v);
+    return xstep<XSum, 32>(v);
+}
+// max of 64-bit keys across the wave (order-free)
+__device__ __forceinline__ unsigned long long u64max(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+template <int STEP>
+__device__ __forceinline__ unsigned long long kstep(unsigned long long k) {
+    const uint32_t l = (uint32_t)k, h = (uint32_t)(k >> 32);
+    if constexpr (STEP == 32 || STEP == 16) {
+        uint32_t la, lb, ha, hb;
+        if constexpr (STEP == 32) { swap32(l, la, lb); swap32(h, ha, hb); }
+        else { swap16(l, la, lb); swap16(h, ha, hb); }
+        return u64max(((unsigned long long)ha << 32) | la, ((unsigned long long)hb << 32) | lb);
+    } else {
+        const uint32_t tl = STEP == 8 ? dpp_ror<8>(l) : STEP == 4 ? dpp_ror<4>(l) : STEP == 2 ? dpp_xor2(l) : dpp_xor1(l);
+        const uint32_t th = STEP == 8 ? dpp_ror<8>(h) : STEP == 4 ? dpp_ror<4>(h) : STEP == 2 ? dpp_xor2(h) : dpp_xor1(h);
+        return u64max(k, ((unsigned long long)th << 32) | tl);
+    }
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long k) {
+    k = kstep<32>(k);
+    k = kstep<16>(k);
+    k = kstep<8>(k);
+    k = kstep<4>(k);
+    k = kstep<2>(k);
+    return kstep<1>(k);
+}
+// max over the 4 rows (16-lane quarters) of a wave
+__device__ __forceinline__ unsigned long long rows_max_u64(unsigned long long k) {
+    k = kstep<16>(k);
+    return kstep<32>(k);
 }
 __device__ __forceinline__ float gelu_lookup(const uint16_t *tab, float x) { return h2f_bits(tab[f2h_bits(x)]); }
 

@@ -326,11 +326,14 @@ struct PersistArgs {
     uint64_t *xg;                // exchange block (persist_layout), zeroed before a run
     uint32_t *err;               // bit 3: exchange timeout
     unsigned long long *ptrace;  // WMI_PTRACE: [n_steps][L + 1][16][2] phase-end clocks, or null
+    int nres;                    // vocabulary rows per workgroup resident in LDS
+    float *logits_out;           // [B][V] logits of every step (debug / teacher forcing), or null
 };
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G);
 // the persistent decoder's exp vs the host ggml table, every non-positive f16 input
 hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *mismatch);
 // largest co-resident grid for the model (0: not supported for this n / B / T)
-int persist_grid(int device, int n, int B, int T);
+// and the vocabulary rows per workgroup that fit in LDS beside the phases' data
+int persist_grid(int device, int n, int B, int T, int V, int *nres);
 
 }  // namespace wmi

@@ -1113,12 +1113,7 @@ constexpr int DG_LNV = 5;  // float4 per lane for a LayerNorm row (K <= 1280)
 // previous step's greedy token of one clip: max over its AMAX_SHARDS packed
 // (ordered logit << 32 | ~id) words; called by a whole wave, result uniform
 __device__ __forceinline__ int32_t shard_token(const unsigned long long *sh, int lane) {
-    unsigned long long k = sh[lane];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long t = __shfl_xor(k, o);
-        k = t > k ? t : k;
-    }
+    const unsigned long long k = wave_max_u64(sh[lane]);
     return (int32_t)(0xffffffffu - (uint32_t)(k & 0xffffffffull));
 }
 
@@ -1364,10 +1359,7 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
             for (int bb = 0; bb < DG_MAXB; ++bb)
                 if (bb < B) {
                     float v = acc[g][bb];
-                    v += __shfl_xor(v, 8);
-                    v += __shfl_xor(v, 4);
-                    v += __shfl_xor(v, 2);
-                    v += __shfl_xor(v, 1);
+                    v = red16_sum(v);
                     acc[g][bb] = v;
                 }
         const int pos = (EPI == DEC_QKV) ? a.st->pos : 0;
@@ -1790,9 +1782,7 @@ __device__ __forceinline__ void xattn_pv(const DecAttnArgs &a, int c, int h, int
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-        o[e] += __shfl_xor(o[e], 8);
-        o[e] += __shfl_xor(o[e], 16);
-        o[e] += __shfl_xor(o[e], 32);
+        o[e] = red_8_16_32(o[e]);
     }
     if (lane < 8)
 #pragma unroll
@@ -1913,10 +1903,7 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
         float acc = 0.0f;
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) acc = dot8(wq[i][kc], *(const half8 *)(xs + kc * 128 + l16 * 8), acc);
-        acc += __shfl_xor(acc, 8);
-        acc += __shfl_xor(acc, 4);
-        acc += __shfl_xor(acc, 2);
-        acc += __shfl_xor(acc, 1);
+        acc = red16_sum(acc);
         if (l16 == 0) qh[w * 16 + q * 4 + i] = (f16)((acc + bqr[i]) * a.qscale);
     }
     __syncthreads();
@@ -1924,7 +1911,7 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
     float s = 0.0f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) s = dot8(kf[i], *(const half8 *)(qh + half * 32 + 8 * i), s);
-    s += __shfl_xor(s, 1);
+    s = xstep<XSum, 1>(s);
     float *S = a.S + ((int64_t)b * a.H + h) * a.s_stride;
     if (half == 0 && key < M) st_x<COH>(S + key, s);
     float m = (key < M) ? s : -INFINITY;
@@ -2028,10 +2015,7 @@ __global__ __launch_bounds__(256) void k_dec_xattn_rows(DecAttnArgs a) {
             float acc = 0.0f;
 #pragma unroll
             for (int kc = 0; kc < KC; ++kc) acc = dot8(wq[i][kc], *(const half8 *)(xs[r] + kc * 128 + l16 * 8), acc);
-            acc += __shfl_xor(acc, 8);
-            acc += __shfl_xor(acc, 4);
-            acc += __shfl_xor(acc, 2);
-            acc += __shfl_xor(acc, 1);
+            acc = red16_sum(acc);
             if (l16 == 0) qh[r][w * 16 + q * 4 + i] = (f16)((acc + bqr[i]) * a.qscale);
         }
     }
@@ -2040,7 +2024,7 @@ __global__ __launch_bounds__(256) void k_dec_xattn_rows(DecAttnArgs a) {
         float s = 0.0f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) s = dot8(kf[i], *(const half8 *)(qh[r] + half * 32 + 8 * i), s);
-        s += __shfl_xor(s, 1);
+        s = xstep<XSum, 1>(s);
         float *S = a.S + ((int64_t)r * a.H + h) * a.s_stride;
         if (half == 0 && key < M) S[key] = s;
         float m = (key < M) ? s : -INFINITY;
@@ -2190,9 +2174,7 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     // the wave's 8 key groups by shuffles, then the 4 waves through LDS
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-        o[e] += __shfl_xor(o[e], 8);
-        o[e] += __shfl_xor(o[e], 16);
-        o[e] += __shfl_xor(o[e], 32);
+        o[e] = red_8_16_32(o[e]);
     }
     if (lane < 8)
 #pragma unroll
@@ -2216,7 +2198,7 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
         float acc = 0.0f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc = dot8(wov[0][i], part ? ov[4 + i] : ov[i], acc);
-        const float other = __shfl_xor(acc, 1);
+        const float other = __uint_as_float(dpp_xor1(__float_as_uint(acc)));
         if (part == 0) dst[blockIdx.z * 128 + (tid >> 1)] = acc + other;  // summed by the next kernel's prologue
         trace_phase(a.phase, 7);
         trace_end(a.trace);
@@ -2334,14 +2316,10 @@ __global__ __launch_bounds__(1024) void k_ts_sample(TsArgs a) {
         if (i != a.sot && i != a.solm && i != a.not_) k_all = k > k_all ? k : k_all;
     }
     mx = wave_max(mx);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long x;
-        x = __shfl_xor(k_all, o); k_all = x > k_all ? x : k_all;
-        x = __shfl_xor(k_ts, o); k_ts = x > k_ts ? x : k_ts;
-        x = __shfl_xor(k_ts1, o); k_ts1 = x > k_ts1 ? x : k_ts1;
-        x = __shfl_xor(k_tx, o); k_tx = x > k_tx ? x : k_tx;
-    }
+    k_all = wave_max_u64(k_all);
+    k_ts = wave_max_u64(k_ts);
+    k_ts1 = wave_max_u64(k_ts1);
+    k_tx = wave_max_u64(k_tx);
     __shared__ unsigned long long stx[16];
     if (lane == 0) { smax[w] = mx; sk[0][w] = k_all; sk[1][w] = k_ts; sk[2][w] = k_ts1; stx[w] = k_tx; }
     __syncthreads();
@@ -2417,14 +2395,7 @@ hipError_t launch_dec_embed(hipStream_t s, const DecEmbedArgs &a) {
 __device__ __forceinline__ unsigned long long beam_key(float v, int id) {
     return ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)id);
 }
-__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long k) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long t = __shfl_xor(k, o);
-        k = t > k ? t : k;
-    }
-    return k;
-}
+
 
 // one vocabulary split of one row: split max, sum exp(logit - max) (double)
 // and the split's top-(K+1)

@@ -160,30 +160,27 @@ __device__ __forceinline__ void wset_load(WSet<KCH, NP> &S, const uint16_t *W, c
 
 // epi(row, b, v, bias, valid) is called by EVERY lane (pairing shuffles);
 // lane l16 carries the reduced value of row `row` for decoder row b = l16
-template <int KCH, int NP, typename Epi>
+template <int BT, int KCH, int NP, typename Epi>
 __device__ __forceinline__ void wset_dot(const WSet<KCH, NP> &S, const f16 *xs, int K, int B, int rb, int r1, int slot,
                                          int l16, Epi &&epi) {
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         if (rb + 16 * p >= r1) break;  // workgroup-uniform
         const int row = rb + 16 * p + slot;
-        float acc[PMAXB];
+        float acc[BT];
 #pragma unroll
-        for (int b = 0; b < PMAXB; ++b) acc[b] = 0.0f;
+        for (int b = 0; b < BT; ++b) acc[b] = 0.0f;
 #pragma unroll
         for (int c = 0; c < KCH; ++c)
 #pragma unroll
-            for (int b = 0; b < PMAXB; ++b)
+            for (int b = 0; b < BT; ++b)
                 if (b < B) acc[b] = dot8(S.w[p][c], *(const half8 *)(xs + b * K + c * 128 + l16 * 8), acc[b]);
         float v = 0.0f;
 #pragma unroll
-        for (int b = 0; b < PMAXB; ++b)
+        for (int b = 0; b < BT; ++b)
             if (b < B) {
                 float t = acc[b];
-                t += __shfl_xor(t, 8);
-                t += __shfl_xor(t, 4);
-                t += __shfl_xor(t, 2);
-                t += __shfl_xor(t, 1);
+                t = red16_sum(t);
                 if (l16 == b) v = t;
             }
         epi(row, l16, v, S.bias[p], row < r1 && l16 < B);
@@ -284,22 +281,28 @@ __device__ __forceinline__ float exp_f16_fast(float arg, const uint16_t *tab, in
 // clock at the end of every phase of the first launch (host prints averages)
 #define PSTAMP(ph)                                                                                    \
     if (a.ptrace && threadIdx.x == 0 && (wg == 0 || wg == G / 2))                                     \
-        a.ptrace[(((int64_t)step * (L + 1) + (ph) / 16) * 16 + ((ph) & 15)) * 2 + (wg == 0 ? 0 : 1)] = \
+        a.ptrace[(((int64_t)step * (L + 1) + (ph) / 32) * 32 + ((ph) & 31)) * 2 + (wg == 0 ? 0 : 1)] = \
             __builtin_amdgcn_s_memrealtime();
 
-template <int NS>
+// Weight / operand loads issued ahead of a poll must stay ahead of it: the
+// compiler otherwise sinks them to their first use, after the poll, and the
+// whole load latency lands behind the seam.  Nothing waits here.
+#define PREFETCH_ISSUED asm volatile("" : : : "memory");
+
+template <int NS, int BT>  // BT: rows at compile time (1) or at most (8, runtime B)
 __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     constexpr int KC = NS / 128;        // 128-element chunks of a K = n row
     constexpr int H = NS / 64;
     constexpr int NPL = KC <= 4 ? 2 : 1;  // logits passes per register set
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ PShared sh;
-    const int B = a.B, G = gridDim.x, wg = blockIdx.x;
+    const int B = BT == 1 ? 1 : a.B, G = gridDim.x, wg = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int L = a.L, T = a.T, tctx = a.tctx, nch = a.nch, CL = a.cl;
     float *xf = (float *)smem;                                          // [B][NS] f32
     f16 *xs = (f16 *)(smem + (size_t)B * NS * 4);                       // [B][4 NS] f16
     unsigned char *scr = smem + (size_t)B * NS * 4 + (size_t)B * NS * 8;  // SCR_BYTES
+    f16 *vres = (f16 *)(scr + SCR_BYTES);                                  // [nres][NS] resident vocabulary rows
     // exchange offsets as plain scalars (a struct captured by the lambdas
     // below would be kept in scratch memory)
     int oX1, oX2, oX3, oQ, oK, oV, oO, oXQ, oOC, oH, oS, oM, oP, oA;
@@ -324,6 +327,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     part(4 * NS, true, rh0, rh1);  // W0 rows
     part(a.V, false, rv0, rv1);    // vocabulary rows
     const int rn = rn1 - rn0;
+    // this workgroup's first vocabulary rows stay in LDS for the whole launch
+    const int rs0 = rv0 + a.nres < rv1 ? rv0 + a.nres : rv1;
+    {
+        const uint4 *src = (const uint4 *)((const f16 *)a.te + (int64_t)rv0 * NS);
+        uint4 *dst = (uint4 *)vres;
+        for (int i = tid; i < (rs0 - rv0) * NS / 8; i += PT) dst[i] = src[i];
+    }
     if (tid == 0) sh.abort_ = 0;
     __syncthreads();
     auto check = [&](bool ok) -> bool {  // workgroup-uniform abort after a poll
@@ -342,11 +352,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
         for (int b = 0; b < B; ++b) {
             unsigned long long k = 0ull;
             if (tid < G) k = ((unsigned long long)ga[(b * G + tid) * 2] << 32) | ga[(b * G + tid) * 2 + 1];
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const unsigned long long t = __shfl_xor(k, o);
-                k = t > k ? t : k;
-            }
+            k = wave_max_u64(k);
             if (lane == 0) sh.best[w][b] = k;
         }
         __syncthreads();
@@ -375,6 +381,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 wset_load(S, P.wqkv, P.bqkv, NS, ra0, ra1, slot, l16);
                 LnP<NS> lp;
                 ln_params<NS>(P.ln1_w, P.ln1_b, lp, lane);
+                PREFETCH_ISSUED
                 __syncthreads();
                 if (l == 0) {
                     const bool fed = pos < a.feed_len;
@@ -400,6 +407,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 } else {
                     const bool ok = gpoll(B * NS, ptag(pos, L, l - 1, 9), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
                     if (check(ok)) return;
+                PSTAMP(l * 32 + 16)
                 }
                 __syncthreads();
                 for (int i = tid; i < B * rn; i += PT) {
@@ -409,8 +417,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 ln_rows<NS>(xf, lp, xs, B, w, lane);
                 __syncthreads();
                 if (act)
-                    wset_dot(S, xs, NS, B, ra0, ra1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
-                        const float vn = __shfl_down(v, 16), ebn = __shfl_down(eb, 16);
+                    wset_dot<BT>(S, xs, NS, B, ra0, ra1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                        const float vn = from_next_row(v), ebn = from_next_row(eb);
                         if (!valid || (q & 1)) return;
                         const int which = row / NS, c = row - which * NS;
                         uint32_t pk;
@@ -424,7 +432,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     });
             }
 
-            PSTAMP(l * 16 + 0)
+            PSTAMP(l * 32 + 0)
             // ---- B: self-attention per (row, head) ---------------------
             {
                 PHASE_IDS
@@ -439,24 +447,25 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     const int doct = tid & 7, jg = tid >> 3;
                     // cache rows j < pos (this step's row comes from the granules)
                     half8 kv[2][8];
-                    // (every register array is loaded unconditionally, rows
-                    // clamped: a conditionally-defined array becomes an undef
-                    // value carried around the step loop and stays live across
-                    // every other phase)
-                    const int jmax = pos > 0 ? pos - 1 : 0;
+                    // (every register array is defined on every path — a
+                    // conditionally-defined array becomes an undef value carried
+                    // around the step loop and stays live across every phase)
+                    const half8 z8 = {};
 #pragma unroll
                     for (int r = 0; r < 2; ++r) {
-                        const int j = min(tid + 256 * r, jmax);
+                        const int j = tid + 256 * r;
                         const uint32_t off = (uint32_t)((((int64_t)b * tctx + j) * NS + h * 64) * 2);
 #pragma unroll
-                        for (int i = 0; i < 8; ++i) kv[r][i] = bload_sc1(rk, off + 16 * i);
+                        for (int i = 0; i < 8; ++i) kv[r][i] = j < pos ? bload_sc1(rk, off + 16 * i) : z8;
                     }
+                    PREFETCH_ISSUED
                     __syncthreads();
                     const int64_t hq = b * (NS / 2) + h * 32;  // q, k, v granule blocks lie 4 NS apart
                     const bool ok = gpoll(96, ptag(pos, L, l, 0),
                                           [=](int i) { return xg + oQ + (i >> 5) * (4 * NS) + hq + (i & 31); },
                                           (uint32_t *)qn, abortw, a.err);
                     if (check(ok)) return;
+                PSTAMP(l * 32 + 17)
                     float sc[2];
                     float mx = -INFINITY;
 #pragma unroll
@@ -479,9 +488,10 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     half8 vv[16];
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
-                        const int j = min(jg + 32 * i, jmax);
-                        vv[i] = bload_sc1(rv, (uint32_t)((((int64_t)b * tctx + j) * NS + h * 64 + doct * 8) * 2));
+                        const int j = jg + 32 * i;
+                        vv[i] = j < pos ? bload_sc1(rv, (uint32_t)((((int64_t)b * tctx + j) * NS + h * 64 + doct * 8) * 2)) : z8;
                     }
+                    PREFETCH_ISSUED
                     mx = wave_max(mx);
                     if (lane == 0) sh.redf[w] = mx;
                     __syncthreads();
@@ -517,9 +527,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     }
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
-                        o[e] += __shfl_xor(o[e], 8);
-                        o[e] += __shfl_xor(o[e], 16);
-                        o[e] += __shfl_xor(o[e], 32);
+                        o[e] = red_8_16_32(o[e]);
                     }
                     if (lane < 8)
 #pragma unroll
@@ -534,7 +542,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 }
             }
 
-            PSTAMP(l * 16 + 1)
+            PSTAMP(l * 32 + 1)
             // ---- C: Wo rows + residual -> x' ---------------------------
             {
                 PHASE_IDS
@@ -542,11 +550,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 WSet<KC, 1> S;
                 const bool act = rn0 < rn1;
                 wset_load(S, P.wo, P.bo, NS, rn0, rn1, slot, l16);
+                PREFETCH_ISSUED
                 __syncthreads();
                 const bool ok = gpoll(B * NS / 2, ptag(pos, L, l, 1), ptr_u64(xg + oO), (uint32_t *)xs, abortw, a.err);
                 if (check(ok)) return;
+                PSTAMP(l * 32 + 18)
                 if (act)
-                    wset_dot(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                    wset_dot<BT>(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
                         if (!valid) return;
                         const float x = (v + eb) + sh.xres[b][row - rn0];
                         sh.xres[b][row - rn0] = x;
@@ -554,7 +564,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     });
             }
 
-            PSTAMP(l * 16 + 2)
+            PSTAMP(l * 32 + 2)
             // ---- D: LNc(x') + Wcq rows -> cross q ------------------------
             {
                 PHASE_IDS
@@ -564,20 +574,22 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 wset_load(S, P.wcq, P.bcq, NS, rn0, rn1, slot, l16);
                 LnP<NS> lp;
                 ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
+                PREFETCH_ISSUED
                 __syncthreads();
                 const bool ok = gpoll(B * NS, ptag(pos, L, l, 2), ptr_u64(xg + oX2), (uint32_t *)xf, abortw, a.err);
                 if (check(ok)) return;
+                PSTAMP(l * 32 + 19)
                 ln_rows<NS>(xf, lp, xs, B, w, lane);
                 __syncthreads();
                 if (act)
-                    wset_dot(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
-                        const float vn = __shfl_down(v, 16), ebn = __shfl_down(eb, 16);
+                    wset_dot<BT>(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                        const float vn = from_next_row(v), ebn = from_next_row(eb);
                         if (!valid || (q & 1)) return;
                         gput(xg + oXQ + b * (NS / 2) + row / 2, tag, pack2((v + eb) * qs, (vn + ebn) * qs));
                     });
             }
 
-            PSTAMP(l * 16 + 3)
+            PSTAMP(l * 32 + 3)
             // ---- E: cross scores per (row, head, key chunk) ----------------
             {
                 PHASE_IDS
@@ -589,17 +601,21 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
                     const f16 *Kb = (const f16 *)a.ck + ((int64_t)l * a.Bt + a.b0 + b) * T * NS + h * 64 + (tid & 1) * 32;
                     half8 kf[NKP][4];
+                    const half8 z8 = {};
 #pragma unroll
                     for (int p = 0; p < NKP; ++p) {
                         int key = j0 + 128 * p + (tid >> 1);
                         key = key < j1 ? key : j1 - 1;
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) kf[p][i] = *(const half8 *)(Kb + (int64_t)key * NS + 8 * i);
+                        for (int i = 0; i < 4; ++i)
+                            kf[p][i] = 128 * p < CL ? *(const half8 *)(Kb + (int64_t)key * NS + 8 * i) : z8;
                     }
+                    PREFETCH_ISSUED
                     __syncthreads();
                     const bool ok = gpoll(32, ptag(pos, L, l, 3), [=](int i) { return xg + oXQ + b * (NS / 2) + h * 32 + i; },
                                           (uint32_t *)qh, abortw, a.err);
                     if (check(ok)) return;
+                PSTAMP(l * 32 + 20)
                     float m = -INFINITY;
 #pragma unroll
                     for (int p = 0; p < NKP; ++p)
@@ -608,7 +624,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                             float s = 0.0f;
 #pragma unroll
                             for (int i = 0; i < 4; ++i) s = dot8(kf[p][i], *(const half8 *)(qh + (tid & 1) * 32 + 8 * i), s);
-                            s += __shfl_xor(s, 1);
+                            s = xstep<XSum, 1>(s);
                             if (key < j1) {
                                 if ((tid & 1) == 0) gput(xg + oS + (int64_t)bh * T + key, tag, __float_as_uint(s));
                                 m = fmaxf(m, s);
@@ -623,7 +639,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 }
             }
 
-            PSTAMP(l * 16 + 4)
+            PSTAMP(l * 32 + 4)
             // ---- F: exact softmax + P16.V partial per chunk ----------------
             {
                 PHASE_IDS
@@ -637,14 +653,16 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     const int doct = tid & 7, jg = tid >> 3;
                     const f16 *Vb = (const f16 *)a.cv + ((int64_t)l * a.Bt + a.b0 + b) * T * NS + h * 64 + doct * 8;
                     half8 vf[NKP][4];
+                    const half8 z8 = {};
 #pragma unroll
                     for (int p = 0; p < NKP; ++p)
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
                             int key = j0 + 128 * p + jg * 4 + u;
                             key = key < j1 ? key : j1 - 1;
-                            vf[p][u] = *(const half8 *)(Vb + (int64_t)key * NS);
+                            vf[p][u] = 128 * p < CL ? *(const half8 *)(Vb + (int64_t)key * NS) : z8;
                         }
+                    PREFETCH_ISSUED
                     __syncthreads();
                     const uint32_t tg = ptag(pos, L, l, 4);
                     const bool ok = gpoll(nch + T, tg,
@@ -655,6 +673,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                           (uint32_t *)cm, abortw, a.err);
                     // (cm[0..nch) then the scores: Sv = cm + nch; moved below)
                     if (check(ok)) return;
+                PSTAMP(l * 32 + 21)
                     float *Sx = cm + nch;
                     float m = cm[0];
                     for (int i = 1; i < nch; ++i) m = fmaxf(m, cm[i]);
@@ -687,9 +706,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                             }
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
-                        o[e] += __shfl_xor(o[e], 8);
-                        o[e] += __shfl_xor(o[e], 16);
-                        o[e] += __shfl_xor(o[e], 32);
+                        o[e] = red_8_16_32(o[e]);
                     }
                     if (lane < 8)
 #pragma unroll
@@ -702,7 +719,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 }
             }
 
-            PSTAMP(l * 16 + 5)
+            PSTAMP(l * 32 + 5)
             // ---- G1: chunk partials summed in chunk order -> cross o ---------
             {
                 PHASE_IDS
@@ -714,6 +731,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     const bool ok = gpoll(nch * 64, ptag(pos, L, l, 5), ptr_u64(xg + oP + (int64_t)t * nch * 64),
                                           (uint32_t *)pp, abortw, a.err);
                     if (check(ok)) return;
+                PSTAMP(l * 32 + 22)
                     if (tid < 64) {
                         float s = pp[tid];
                         for (int c = 1; c < nch; ++c) s = s + pp[c * 64 + tid];
@@ -725,7 +743,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 }
             }
 
-            PSTAMP(l * 16 + 6)
+            PSTAMP(l * 32 + 6)
             // ---- G2: Wco rows + residual -> x'' -------------------------
             {
                 PHASE_IDS
@@ -733,11 +751,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 WSet<KC, 1> S;
                 const bool act = rn0 < rn1;
                 wset_load(S, P.wco, P.bco, NS, rn0, rn1, slot, l16);
+                PREFETCH_ISSUED
                 __syncthreads();
                 const bool ok = gpoll(B * NS / 2, ptag(pos, L, l, 6), ptr_u64(xg + oOC), (uint32_t *)xs, abortw, a.err);
                 if (check(ok)) return;
+                PSTAMP(l * 32 + 23)
                 if (act)
-                    wset_dot(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                    wset_dot<BT>(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
                         if (!valid) return;
                         const float x = (v + eb) + sh.xres[b][row - rn0];
                         sh.xres[b][row - rn0] = x;
@@ -745,7 +765,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     });
             }
 
-            PSTAMP(l * 16 + 7)
+            PSTAMP(l * 32 + 7)
             // ---- H: LN2(x'') + W0 rows + GELU -> hidden ---------------------
             {
                 PHASE_IDS
@@ -755,14 +775,16 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 wset_load(S, P.w0, P.b0, NS, rh0, rh1, slot, l16);
                 LnP<NS> lp;
                 ln_params<NS>(P.ln2_w, P.ln2_b, lp, lane);
+                PREFETCH_ISSUED
                 __syncthreads();
                 const bool ok = gpoll(B * NS, ptag(pos, L, l, 7), ptr_u64(xg + oX3), (uint32_t *)xf, abortw, a.err);
                 if (check(ok)) return;
+                PSTAMP(l * 32 + 24)
                 ln_rows<NS>(xf, lp, xs, B, w, lane);
                 __syncthreads();
                 if (act)
-                    wset_dot(S, xs, NS, B, rh0, rh1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
-                        const float vn = __shfl_down(v, 16), ebn = __shfl_down(eb, 16);
+                    wset_dot<BT>(S, xs, NS, B, rh0, rh1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                        const float vn = from_next_row(v), ebn = from_next_row(eb);
                         if (!valid || (q & 1)) return;
                         const uint16_t h0 = f2h_bits(v + eb), h1 = f2h_bits(vn + ebn);
                         const uint16_t g0 = a.gelu_tab[h0], g1 = a.gelu_tab[h1];
@@ -770,7 +792,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     });
             }
 
-            PSTAMP(l * 16 + 8)
+            PSTAMP(l * 32 + 8)
             // ---- I: W1 rows + residual -> next layer's x --------------------
             {
                 PHASE_IDS
@@ -778,59 +800,89 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 WSet<4 * KC, 1> S;
                 const bool act = rn0 < rn1;
                 wset_load(S, P.w1, P.b1, 4 * NS, rn0, rn1, slot, l16);
+                PREFETCH_ISSUED
                 __syncthreads();
                 const bool ok = gpoll(B * 2 * NS, ptag(pos, L, l, 8), ptr_u64(xg + oH), (uint32_t *)xs, abortw, a.err);
                 if (check(ok)) return;
+                PSTAMP(l * 32 + 25)
                 if (act)
-                    wset_dot(S, xs, 4 * NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                    wset_dot<BT>(S, xs, 4 * NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
                         if (!valid) return;
                         const float x = (v + eb) + sh.xres[b][row - rn0];
                         sh.xres[b][row - rn0] = x;
                         gput(xg + oX1 + b * NS + row, tag, __float_as_uint(x));
                     });
             }
-            PSTAMP(l * 16 + 9)
+            PSTAMP(l * 32 + 9)
         }
 
         // ---- logits: LN_final + vocabulary rows + per-WG argmax -------------
+        // rows [rv0, rs0) are resident in LDS (loaded once per launch), the
+        // rest [rs0, rv1) stream through two register sets issued before the poll
         {
                 PHASE_IDS
             WSet<KC, NPL> S0, S1;
-            const bool act = rv0 < rv1;
             constexpr int RS = 16 * NPL;  // rows per register set
-            wset_load(S0, a.te, nullptr, NS, rv0, rv1, slot, l16);
-            wset_load(S1, a.te, nullptr, NS, rv0 + RS, rv1, slot, l16);
+            wset_load(S0, a.te, nullptr, NS, rs0, rv1, slot, l16);
+            wset_load(S1, a.te, nullptr, NS, rs0 + RS, rv1, slot, l16);
             LnP<NS> lp;
             ln_params<NS>(a.dln_w, a.dln_b, lp, lane);
+            PREFETCH_ISSUED
             __syncthreads();
             const bool ok = gpoll(B * NS, ptag(pos, L, L - 1, 9), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
             if (check(ok)) return;
+                PSTAMP(L * 32 + 16)
             ln_rows<NS>(xf, lp, xs, B, w, lane);
             __syncthreads();
+            PSTAMP(L * 32 + 1)
             unsigned long long best = 0ull;
             auto epi = [&](int row, int b, float v, float eb, bool valid) {
+                if (a.logits_out && valid) a.logits_out[(int64_t)b * a.V + row] = v;
                 if (!valid || row == a.suppress_id) return;
                 const unsigned long long k =
                     ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)row);
                 best = k > best ? k : best;
             };
-            if (act)
-                for (int rb = rv0;;) {
-                    wset_dot(S0, xs, NS, B, rb, rv1, slot, l16, epi);
+            for (int rb = rv0; rb < rs0; rb += 16) {  // resident rows
+                const int row = rb + slot;
+                const bool okr = row < rs0;
+                const f16 *wr = vres + (okr ? row - rv0 : 0) * NS + l16 * 8;
+                float acc[BT];
+#pragma unroll
+                for (int b = 0; b < BT; ++b) acc[b] = 0.0f;
+#pragma unroll
+                for (int c = 0; c < KC; ++c) {
+                    const half8 wv = *(const half8 *)(wr + c * 128);
+#pragma unroll
+                    for (int b = 0; b < BT; ++b)
+                        if (b < B) acc[b] = dot8(wv, *(const half8 *)(xs + b * NS + c * 128 + l16 * 8), acc[b]);
+                }
+                float v = 0.0f;
+#pragma unroll
+                for (int b = 0; b < BT; ++b)
+                    if (b < B) {
+                        float t = acc[b];
+                        t = red16_sum(t);
+                        if (l16 == b) v = t;
+                    }
+                epi(row, l16, v, 0.0f, okr && l16 < B);
+            }
+            PSTAMP(L * 32 + 2)
+            if (rs0 < rv1)
+                for (int rb = rs0;;) {
+                    wset_dot<BT>(S0, xs, NS, B, rb, rv1, slot, l16, epi);
                     wset_load(S0, a.te, nullptr, NS, rb + 2 * RS, rv1, slot, l16);
+                    PREFETCH_ISSUED
                     if (rb + RS >= rv1) break;
-                    wset_dot(S1, xs, NS, B, rb + RS, rv1, slot, l16, epi);
+                    wset_dot<BT>(S1, xs, NS, B, rb + RS, rv1, slot, l16, epi);
                     wset_load(S1, a.te, nullptr, NS, rb + 3 * RS, rv1, slot, l16);
+                    PREFETCH_ISSUED
                     rb += 2 * RS;
                     if (rb >= rv1) break;
                 }
+            PSTAMP(L * 32 + 3)
             // lane l16 = b holds its quarter's best: reduce the 4 quarters, then the waves
-            {
-                unsigned long long t = __shfl_xor(best, 16);
-                best = t > best ? t : best;
-                t = __shfl_xor(best, 32);
-                best = t > best ? t : best;
-            }
+            best = rows_max_u64(best);
             if (lane < PMAXB) sh.best[w][lane] = best;
             __syncthreads();
             if (tid < B) {
@@ -841,7 +893,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 gput(xg + oA + ((int64_t)tid * G + wg) * 2 + 1, tg, (uint32_t)k);
             }
         }
-        PSTAMP(L * 16 + 0)
+        PSTAMP(L * 32 + 0)
+        if (a.ptrace && threadIdx.x == 0 && (wg == 0 || wg == G / 2))  // shader clock (s_memtime) at the same point
+            a.ptrace[(((int64_t)step * (L + 1) + L) * 32 + 4) * 2 + (wg == 0 ? 0 : 1)] = __builtin_amdgcn_s_memtime();
     }
     // the last step's token: recorded by workgroup 0 and carried to the next launch
     if (wg != 0 || a.n_steps < 1) return;
@@ -858,24 +912,38 @@ template <int NS>
 size_t persist_lds(int B) {
     return (size_t)B * NS * 4 + (size_t)B * NS * 8 + SCR_BYTES;
 }
+constexpr size_t LDS_CU = 160 * 1024;
 
-template <int NS>
-hipError_t launch_ns(hipStream_t s, const PersistArgs &a, int G) {
-    const size_t lds = persist_lds<NS>(a.B);
-    hipError_t e = hipFuncSetAttribute((const void *)k_dec_persist<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+template <int NS, int BT>
+hipError_t launch_nsb(hipStream_t s, const PersistArgs &a, int G) {
+    const size_t lds = persist_lds<NS>(a.B) + (size_t)a.nres * NS * 2;
+    hipError_t e = hipFuncSetAttribute((const void *)k_dec_persist<NS, BT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_dec_persist<NS>, dim3(G), dim3(PT), lds, s, a);
+    hipLaunchKernelGGL((k_dec_persist<NS, BT>), dim3(G), dim3(PT), lds, s, a);
     return hipGetLastError();
 }
-
 template <int NS>
-int grid_ns(int device, int B) {
-    const size_t lds = persist_lds<NS>(B);
-    if (hipFuncSetAttribute((const void *)k_dec_persist<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+hipError_t launch_ns(hipStream_t s, const PersistArgs &a, int G) {
+    return a.B == 1 ? launch_nsb<NS, 1>(s, a, G) : launch_nsb<NS, PMAXB>(s, a, G);
+}
+
+template <int NS, int BT>
+int grid_nsb(int device, int B, int V, int *nres) {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, (const void *)k_dec_persist<NS, BT>) != hipSuccess) return 0;
+    const size_t base = persist_lds<NS>(B), avail = LDS_CU - fa.sharedSizeBytes - 1024;
+    if (base > avail) return 0;
+    // resident vocabulary rows: as many of a workgroup's rows as the LDS holds
+    const int G0 = PX_GMAX, rpw = (V + G0 - 1) / G0;
+    int nr = (int)((avail - base) / (NS * 2));
+    *nres = nr < rpw ? nr : rpw;
+    const size_t lds = base + (size_t)*nres * NS * 2;
+    if (hipFuncSetAttribute((const void *)k_dec_persist<NS, BT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
         hipSuccess)
         return 0;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dec_persist<NS>, PT, lds) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dec_persist<NS, BT>, PT, lds) != hipSuccess || per_cu < 1)
         return 0;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
@@ -895,6 +963,11 @@ __global__ void k_persist_selftest(const uint16_t *tab, int n_exp, uint32_t *mis
     if (got != want) atomicAdd(mismatch, 1u);
 }
 
+template <int NS>
+int grid_ns(int device, int B, int V, int *nres) {
+    return B == 1 ? grid_nsb<NS, 1>(device, B, V, nres) : grid_nsb<NS, PMAXB>(device, B, V, nres);
+}
+
 }  // namespace
 
 hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *mismatch) {
@@ -902,15 +975,16 @@ hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n
     return hipGetLastError();
 }
 
-int persist_grid(int device, int n, int B, int T) {
+int persist_grid(int device, int n, int B, int T, int V, int *nres) {
+    *nres = 0;
     if (B < 1 || B > PMAXB || T < 1 || T > 2048) return 0;
     switch (n) {
-        case 128: return grid_ns<128>(device, B);
-        case 384: return grid_ns<384>(device, B);
-        case 512: return grid_ns<512>(device, B);
-        case 768: return grid_ns<768>(device, B);
-        case 1024: return grid_ns<1024>(device, B);
-        case 1280: return grid_ns<1280>(device, B);
+        case 128: return grid_ns<128>(device, B, V, nres);
+        case 384: return grid_ns<384>(device, B, V, nres);
+        case 512: return grid_ns<512>(device, B, V, nres);
+        case 768: return grid_ns<768>(device, B, V, nres);
+        case 1024: return grid_ns<1024>(device, B, V, nres);
+        case 1280: return grid_ns<1280>(device, B, V, nres);
         default: return 0;
     }
 }
