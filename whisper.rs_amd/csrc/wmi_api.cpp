@@ -1416,6 +1416,23 @@ int ptrace_dump(wmi_context *ctx, int steps) {
             const double d = k < 10 ? (double)ns * L : (double)ns;
             fprintf(stderr, "[wmi ptrace]   %-9s %6.2f / %6.2f\n", nm[k], ph[k] / d, pw[k] / d);
         }
+        // sub-phase stamps (slots 26..31, when a build sets them): time after
+        // the latest poll-done stamp of the same layer
+        for (int k = 26; k < 32; ++k) {
+            double s = 0;
+            int c = 0;
+            for (int st = 1; st < steps; ++st)
+                for (int l = 0; l < L; ++l) {
+                    const unsigned long long v = at(st, l, k, w);
+                    unsigned long long pd = 0;
+                    for (int j = 16; j < 26; ++j) {
+                        const unsigned long long p = at(st, l, j, w);
+                        if (p && p <= v && p > pd) pd = p;
+                    }
+                    if (v && pd) { s += (double)(v - pd) * 0.01; ++c; }
+                }
+            if (c) fprintf(stderr, "[wmi ptrace]   sub %d: %6.2f us after poll\n", k, s / c);
+        }
     }
     return WMI_OK;
 }

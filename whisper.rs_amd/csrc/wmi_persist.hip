@@ -17,6 +17,7 @@
 //   B  self-attention per (b, head)              -> o (f16 pairs)
 //   C  Wo rows + residual                        -> x'
 //   D  LNc(x') -> Wcq rows                       -> cross q (f16 pairs)
+//      (n <= 768: no D phase — every E task computes its head's q itself)
 //   E  cross scores per (b, head, key chunk)     -> scores, chunk max
 //   F  exact softmax (global max, double sum) + P16.V per chunk -> partials
 //   G1 chunk partials summed in order per (b, head) -> cross o (f16 pairs)
@@ -80,6 +81,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *p, uint32_
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
 }
 
+// Address-space casts.  Pointers read from memory (the layer table) are
+// generic: their loads would be flat loads, which count against lgkmcnt too,
+// so every LDS wait or barrier would also wait for the weight prefetch.  The
+// layer table is read through the constant address space (scalar loads; the
+// host writes it before the launch) and weight pointers are marked global.
+// (the host pass only type-checks kernel bodies: no address spaces there)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define WMI_AS(n) __attribute__((address_space(n)))
+#else
+#define WMI_AS(n)
+#endif
+template <typename T>
+__device__ __forceinline__ const WMI_AS(1) T *glb(const T *p) {
+    return (const WMI_AS(1) T *)p;
+}
+typedef const WMI_AS(4) PersistLayer ConstLayer;
+
 struct PShared {
     float xres[PMAXB][RNMAX];   // this workgroup's rows of the residual stream
     int32_t tok[PMAXB];
@@ -93,12 +111,11 @@ struct PShared {
 // Poll cnt granules (granule i at addr(i)) until every tag equals `tag`,
 // storing the values to dst[i] (LDS).  Bounded: a dead seam sets the abort
 // word (every poller checks it) and err bit 3, so the grid always drains.
-template <typename F>
+template <int PU = 4, typename F>  // PU: granules in flight per thread
 __device__ __forceinline__ bool gpoll(int cnt, uint32_t tag, F addr, uint32_t *dst, uint32_t *abortw, uint32_t *err) {
     bool ok = true;
     int tid = (int)threadIdx.x;
     asm volatile("" : "+v"(tid));
-    constexpr int PU = 4;  // granules in flight per thread
     for (int base = tid; base < cnt && ok; base += PT * PU) {
         uint64_t v[PU];
 #pragma unroll
@@ -153,8 +170,8 @@ __device__ __forceinline__ void wset_load(WSet<KCH, NP> &S, const uint16_t *W, c
         row = row > 0 ? row : 0;
         const f16 *wr = (const f16 *)W + (int64_t)row * K + l16 * 8;
 #pragma unroll
-        for (int c = 0; c < KCH; ++c) S.w[p][c] = *(const half8 *)(wr + c * 128);
-        S.bias[p] = bias ? bias[row] : 0.0f;
+        for (int c = 0; c < KCH; ++c) S.w[p][c] = *glb((const half8 *)(wr + c * 128));
+        S.bias[p] = bias ? *glb(bias + row) : 0.0f;
     }
 }
 
@@ -163,6 +180,29 @@ __device__ __forceinline__ void wset_load(WSet<KCH, NP> &S, const uint16_t *W, c
 template <int BT, int KCH, int NP, typename Epi>
 __device__ __forceinline__ void wset_dot(const WSet<KCH, NP> &S, const f16 *xs, int K, int B, int rb, int r1, int slot,
                                          int l16, Epi &&epi) {
+    if constexpr (BT == 1 && NP > 1) {
+        // one decoder row: the passes' dot chains and reductions interleaved
+        // (every pass computed — the loads behind them are clamped rows —
+        // and only valid passes reach the epilogue); each sum keeps its order
+        float acc[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) acc[p] = 0.0f;
+#pragma unroll
+        for (int c = 0; c < KCH; ++c) {
+            const half8 xv = *(const half8 *)(xs + c * 128 + l16 * 8);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) acc[p] = dot8(S.w[p][c], xv, acc[p]);
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) acc[p] = red16_sum(acc[p]);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            if (rb + 16 * p >= r1) break;  // workgroup-uniform
+            const int row = rb + 16 * p + slot;
+            epi(row, l16, l16 == 0 ? acc[p] : 0.0f, S.bias[p], row < r1 && l16 < 1);
+        }
+        return;
+    }
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         if (rb + 16 * p >= r1) break;  // workgroup-uniform
@@ -199,8 +239,8 @@ __device__ __forceinline__ void ln_params(const float *lw, const float *lb, LnP<
 #pragma unroll
     for (int i = 0; i < LnP<NS>::V; ++i) {
         const int e = (lane + 64 * i) * 4, ec = e < NS ? e : 0;
-        P.w[i] = *(const float4 *)(lw + ec);
-        P.b[i] = *(const float4 *)(lb + ec);
+        P.w[i] = *glb((const float4 *)(lw + ec));
+        P.b[i] = *glb((const float4 *)(lb + ec));
     }
 }
 template <int NS>
@@ -294,6 +334,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     constexpr int KC = NS / 128;        // 128-element chunks of a K = n row
     constexpr int H = NS / 64;
     constexpr int NPL = KC <= 4 ? 2 : 1;  // logits passes per register set
+    constexpr bool XQF = KC <= 6;         // cross q computed inside the score tasks (registers allow)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ PShared sh;
     const int B = BT == 1 ? 1 : a.B, G = gridDim.x, wg = blockIdx.x;
@@ -368,7 +409,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     int pos = a.st->pos;
     for (int step = 0; step < a.n_steps; ++step, ++pos) {
         for (int l = 0; l < L; ++l) {
-            const PersistLayer &P = a.layers[l];
+            ConstLayer &P = ((ConstLayer *)a.layers)[l];
             uint16_t *kc = a.kcache + (size_t)l * DEC_ROWS * tctx * NS;
             uint16_t *vc = a.vcache + (size_t)l * DEC_ROWS * tctx * NS;
 
@@ -416,6 +457,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 }
                 ln_rows<NS>(xf, lp, xs, B, w, lane);
                 __syncthreads();
+                PSTAMP(l * 32 + 26)
                 if (act)
                     wset_dot<BT>(S, xs, NS, B, ra0, ra1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
                         const float vn = from_next_row(v), ebn = from_next_row(eb);
@@ -458,6 +500,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #pragma unroll
                         for (int i = 0; i < 8; ++i) kv[r][i] = j < pos ? bload_sc1(rk, off + 16 * i) : z8;
                     }
+                    // value rows j < pos, in flight across the poll as well
+                    half8 vv[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int j = jg + 32 * i;
+                        vv[i] = j < pos ? bload_sc1(rv, (uint32_t)((((int64_t)b * tctx + j) * NS + h * 64 + doct * 8) * 2)) : z8;
+                    }
                     PREFETCH_ISSUED
                     __syncthreads();
                     const int64_t hq = b * (NS / 2) + h * 32;  // q, k, v granule blocks lie 4 NS apart
@@ -466,32 +515,27 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                           (uint32_t *)qn, abortw, a.err);
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 17)
+                    // scores: cache rows from registers, this step's row (same
+                    // value in every lane) from the granules; no lane guards
+                    half8 q8[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) q8[i] = *(const half8 *)(qn + 8 * i);
+                    float snew = 0.0f;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) snew = dot8(*(const half8 *)(kn + 8 * i), q8[i], snew);
                     float sc[2];
                     float mx = -INFINITY;
 #pragma unroll
                     for (int r = 0; r < 2; ++r) {
                         const int j = tid + 256 * r;
                         float s = 0.0f;
-                        if (j < pos) {
+                        if (256 * r < pos)  // workgroup-uniform: skip all-zero rows
 #pragma unroll
-                            for (int i = 0; i < 8; ++i) s = dot8(kv[r][i], *(const half8 *)(qn + 8 * i), s);
-                        } else if (j == pos) {
-#pragma unroll
-                            for (int i = 0; i < 8; ++i) s = dot8(*(const half8 *)(kn + 8 * i), *(const half8 *)(qn + 8 * i), s);
-                        }
+                            for (int i = 0; i < 8; ++i) s = dot8(kv[r][i], q8[i], s);
+                        s = j < pos ? s : j == pos ? snew : 0.0f;
                         sc[r] = s;
                         if (j < M) mx = fmaxf(mx, s);
                     }
-                    // value rows (the key registers are dead now): in flight
-                    // while the softmax runs
-                    asm volatile("" : "+v"(sc[0]), "+v"(sc[1]), "+v"(mx) : : "memory");
-                    half8 vv[16];
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int j = jg + 32 * i;
-                        vv[i] = j < pos ? bload_sc1(rv, (uint32_t)((((int64_t)b * tctx + j) * NS + h * 64 + doct * 8) * 2)) : z8;
-                    }
-                    PREFETCH_ISSUED
                     mx = wave_max(mx);
                     if (lane == 0) sh.redf[w] = mx;
                     __syncthreads();
@@ -514,16 +558,30 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     for (int r = 0; r < 2; ++r)
                         if (tid + 256 * r < M) P16[tid + 256 * r] = f2h_bits(p[r] * inv);
                     __syncthreads();
+                PSTAMP(l * 32 + 31)
+                    // P.V in key order: rows past pos are zero registers and
+                    // add exact zeros (o is never -0), so this step's row —
+                    // the last key — is added after the loop
                     float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                    float pv[16];
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
                         const int j = jg + 32 * i;
-                        if (j < M) {
-                            const float pj = h2f_bits(P16[j]);
-                            const half8 vr = j < pos ? vv[i] : *(const half8 *)(vn + doct * 8);
+                        pv[i] = h2f_bits(P16[j]);  // j < 512: inside the buffer
+                    }
 #pragma unroll
-                            for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vr[e];
-                        }
+                    for (int i = 0; i < 16; ++i) {
+                        if (32 * i >= pos) break;  // workgroup-uniform: the rest add zeros
+                        const int j = jg + 32 * i;
+                        const float pj = j < pos ? pv[i] : 0.0f;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vv[i][e];
+                    }
+                    if (jg == (pos & 31)) {
+                        const float pj = h2f_bits(P16[pos]);
+                        const half8 vr = *(const half8 *)(vn + doct * 8);
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vr[e];
                     }
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
@@ -566,7 +624,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 
             PSTAMP(l * 32 + 2)
             // ---- D: LNc(x') + Wcq rows -> cross q ------------------------
-            {
+            // (n <= 768: folded into E, whose tasks compute their head's q)
+            if constexpr (!XQF) {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 3);
                 WSet<KC, 1> S;
@@ -610,12 +669,36 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         for (int i = 0; i < 4; ++i)
                             kf[p][i] = 128 * p < CL ? *(const half8 *)(Kb + (int64_t)key * NS + 8 * i) : z8;
                     }
-                    PREFETCH_ISSUED
-                    __syncthreads();
-                    const bool ok = gpoll(32, ptag(pos, L, l, 3), [=](int i) { return xg + oXQ + b * (NS / 2) + h * 32 + i; },
-                                          (uint32_t *)qh, abortw, a.err);
-                    if (check(ok)) return;
+                    if constexpr (XQF) {
+                        // this head's cross q from x' directly: LNc(x'_b) and
+                        // Wcq rows h*64 .. h*64+63, the D phase's arithmetic
+                        WSet<KC, 4> S;
+                        wset_load(S, P.wcq, P.bcq, NS, h * 64, h * 64 + 64, slot, l16);
+                        LnP<NS> lp;
+                        ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
+                        PREFETCH_ISSUED
+                        __syncthreads();
+                        const bool ok = gpoll(NS, ptag(pos, L, l, 2), ptr_u64(xg + oX2 + b * NS), (uint32_t *)xf, abortw, a.err);
+                        if (check(ok)) return;
                 PSTAMP(l * 32 + 20)
+                        ln_rows<NS>(xf, lp, xs, 1, w, lane);
+                        __syncthreads();
+                PSTAMP(l * 32 + 29)
+                        wset_dot<1>(S, xs, NS, 1, h * 64, h * 64 + 64, slot, l16,
+                                    [&](int row, int, float v, float eb, bool valid) {
+                                        if (valid) qh[row - h * 64] = (f16)((v + eb) * qs);
+                                    });
+                        __syncthreads();
+                PSTAMP(l * 32 + 30)
+                    } else {
+                        PREFETCH_ISSUED
+                        __syncthreads();
+                        const bool ok = gpoll(32, ptag(pos, L, l, 3),
+                                              [=](int i) { return xg + oXQ + b * (NS / 2) + h * 32 + i; }, (uint32_t *)qh,
+                                              abortw, a.err);
+                        if (check(ok)) return;
+                PSTAMP(l * 32 + 20)
+                    }
                     float m = -INFINITY;
 #pragma unroll
                     for (int p = 0; p < NKP; ++p)
@@ -665,7 +748,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     PREFETCH_ISSUED
                     __syncthreads();
                     const uint32_t tg = ptag(pos, L, l, 4);
-                    const bool ok = gpoll(nch + T, tg,
+                    const bool ok = gpoll<8>(nch + T, tg,  // T <= 2048: one round
                                           [=](int i) {
                                               return i < nch ? xg + oM + (int64_t)bh * nch + i
                                                              : xg + oS + (int64_t)bh * T + (i - nch);
@@ -675,14 +758,24 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 21)
                     float *Sx = cm + nch;
-                    float m = cm[0];
-                    for (int i = 1; i < nch; ++i) m = fmaxf(m, cm[i]);
+                    // (LDS reads are issued unconditionally from clamped
+                    // addresses and selected afterwards: a read under a lane
+                    // guard is waited for on its own, one LDS latency each)
+                    const float m = wave_max(lane < nch ? cm[lane] : -INFINITY);
+                    // exp of every score against the global max; the double
+                    // sum of <= 2048 f16 values in [0, 1] is exact in any order
+                    float sv[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int j = tid + 256 * u;
+                        sv[u] = Sx[j < T ? j : T - 1];
+                    }
                     double sum = 0.0;
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
                         const int j = tid + 256 * u;
+                        const float pj = exp_f16_fast(sv[u] - m, a.exp_tab, a.n_exp);
                         if (j < T) {
-                            const float pj = exp_f16_fast(Sx[j] - m, a.exp_tab, a.n_exp);
                             sum += (double)pj;
                             Sx[j] = pj;
                         }
@@ -694,16 +787,22 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                     for (int p = 0; p < NKP; ++p)
-                        if (j0 + 128 * p < j1)
+                        if (j0 + 128 * p < j1) {  // workgroup-uniform
+                            float sp[4];
 #pragma unroll
                             for (int u = 0; u < 4; ++u) {
                                 const int key = j0 + 128 * p + jg * 4 + u;
-                                if (key < j1) {
-                                    const float pj = h2f_bits(f2h_bits(Sx[key] * inv));
-#pragma unroll
-                                    for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vf[p][u][e];
-                                }
+                                sp[u] = Sx[key < j1 ? key : j1 - 1];
                             }
+                            // keys past the chunk add pj = 0 (o + 0 == o: o is never -0)
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const int key = j0 + 128 * p + jg * 4 + u;
+                                const float pj = key < j1 ? h2f_bits(f2h_bits(sp[u] * inv)) : 0.0f;
+#pragma unroll
+                                for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vf[p][u][e];
+                            }
+                        }
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         o[e] = red_8_16_32(o[e]);
@@ -732,9 +831,16 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                           (uint32_t *)pp, abortw, a.err);
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 22)
-                    if (tid < 64) {
-                        float s = pp[tid];
-                        for (int c = 1; c < nch; ++c) s = s + pp[c * 64 + tid];
+                    if (tid < 64) {  // in chunk order, 8 LDS reads in flight
+                        float s = 0.0f;
+                        for (int c0 = 0; c0 < nch; c0 += 8) {
+                            float v[8];
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) v[u] = pp[(c0 + u < nch ? c0 + u : nch - 1) * 64 + tid];
+#pragma unroll
+                            for (int u = 0; u < 8; ++u)
+                                if (c0 + u < nch) s = c0 + u == 0 ? v[u] : s + v[u];
+                        }
                         sh.ored[0][tid] = s;
                     }
                     __syncthreads();
@@ -755,7 +861,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 __syncthreads();
                 const bool ok = gpoll(B * NS / 2, ptag(pos, L, l, 6), ptr_u64(xg + oOC), (uint32_t *)xs, abortw, a.err);
                 if (check(ok)) return;
-                PSTAMP(l * 32 + 23)
+            PSTAMP(l * 32 + 23)
                 if (act)
                     wset_dot<BT>(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
                         if (!valid) return;
@@ -782,6 +888,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PSTAMP(l * 32 + 24)
                 ln_rows<NS>(xf, lp, xs, B, w, lane);
                 __syncthreads();
+                PSTAMP(l * 32 + 28)
                 if (act)
                     wset_dot<BT>(S, xs, NS, B, rh0, rh1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
                         const float vn = from_next_row(v), ebn = from_next_row(eb);
@@ -843,29 +950,37 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)row);
                 best = k > best ? k : best;
             };
-            for (int rb = rv0; rb < rs0; rb += 16) {  // resident rows
-                const int row = rb + slot;
-                const bool okr = row < rs0;
-                const f16 *wr = vres + (okr ? row - rv0 : 0) * NS + l16 * 8;
-                float acc[BT];
+            constexpr int RU = BT == 1 ? 4 : 1;  // row groups interleaved per iteration (one decoder row)
+            for (int rb = rv0; rb < rs0; rb += 16 * RU) {  // resident rows
+                float acc[RU][BT];
 #pragma unroll
-                for (int b = 0; b < BT; ++b) acc[b] = 0.0f;
+                for (int u = 0; u < RU; ++u)
+#pragma unroll
+                    for (int b = 0; b < BT; ++b) acc[u][b] = 0.0f;
 #pragma unroll
                 for (int c = 0; c < KC; ++c) {
-                    const half8 wv = *(const half8 *)(wr + c * 128);
+#pragma unroll
+                    for (int u = 0; u < RU; ++u) {
+                        const int row = rb + 16 * u + slot;
+                        const f16 *wr = vres + (row < rs0 ? row - rv0 : 0) * NS + l16 * 8;
+                        const half8 wv = *(const half8 *)(wr + c * 128);
+#pragma unroll
+                        for (int b = 0; b < BT; ++b)
+                            if (b < B) acc[u][b] = dot8(wv, *(const half8 *)(xs + b * NS + c * 128 + l16 * 8), acc[u][b]);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < RU; ++u) {
+                    const int row = rb + 16 * u + slot;
+                    float v = 0.0f;
 #pragma unroll
                     for (int b = 0; b < BT; ++b)
-                        if (b < B) acc[b] = dot8(wv, *(const half8 *)(xs + b * NS + c * 128 + l16 * 8), acc[b]);
+                        if (b < B) {
+                            const float t = red16_sum(acc[u][b]);
+                            if (l16 == b) v = t;
+                        }
+                    epi(row, l16, v, 0.0f, row < rs0 && l16 < B);
                 }
-                float v = 0.0f;
-#pragma unroll
-                for (int b = 0; b < BT; ++b)
-                    if (b < B) {
-                        float t = acc[b];
-                        t = red16_sum(t);
-                        if (l16 == b) v = t;
-                    }
-                epi(row, l16, v, 0.0f, okr && l16 < B);
             }
             PSTAMP(L * 32 + 2)
             if (rs0 < rv1)
