@@ -2349,6 +2349,14 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
         } else if (which >= 9 && which <= 13) {
             HIPCHK(ctx, launch_probe_barrier_h(s, hb_mode, hb_wg, bar_rounds, hb_cnt, hb_base, ctx->derr));
             hb_base += (uint32_t)bar_rounds;
+        } else if (which == 14) {
+            // the persistent greedy decoder over the staged clips, exactly as
+            // the last run_staged launched it (per 8-row block: state and
+            // exchange memsets + one launch of all steps)
+            if (ctx->staged_n_decode < 1 || persist_grid_for(ctx, B < 8 ? B : 8) <= 0)
+                return set_err(ctx, WMI_E_INVALID_ARG, "persistent decoder not in use for this run");
+            const int r = run_greedy(ctx, ctx->staged_n_decode, 1, false, nullptr, nullptr);
+            if (r) return r;
         } else {
             return set_err(ctx, WMI_E_INVALID_ARG, "unknown kernel %d", which);
         }
@@ -2391,6 +2399,28 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
         snprintf(out->name, sizeof out->name, "k_probe_barrier (%d WG x %d barriers)", bar_wg, bar_rounds);
     } else if (which >= 9 && which <= 13) {
         snprintf(out->name, sizeof out->name, "k_probe_barrier_h mode %d (%d WG x %d barriers)", hb_mode, hb_wg, bar_rounds);
+    } else if (which == 14) {
+        // algorithmic bytes of one decode: every step reads each decoder
+        // weight, bias and LayerNorm vector once (shared by the block's rows),
+        // the vocabulary matrix once, each row's cross K/V and self K/V rows
+        // [0, pos] once, and writes its new self K/V row
+        const double L = hp.n_text_layer, Tx = T;
+        int32_t prompt[8];
+        const int np = prompt_tokens(ctx, prompt), steps = np + ctx->staged_n_decode - 1;
+        const double w_step = L * (28.0 * nt * nt + 68.0 * nt) + V * nt * 2 + 2 * nt * 4;
+        double bytes = 0, flops = 0;
+        for (int b0 = 0; b0 < B; b0 += 8) {
+            const double rows = B - b0 < 8 ? B - b0 : 8;
+            for (int pos = 0; pos < steps; ++pos) {
+                bytes += w_step + rows * (nt * 2 + nt * 4);                 // weights, token + position rows
+                bytes += rows * L * Tx * nt * 2 * 2;                         // cross K, V
+                bytes += rows * L * ((double)pos * nt * 2 * 2 + nt * 2 * 2);  // self K, V read + new row
+                flops += rows * (2.0 * L * (14.0 * nt * nt + 2.0 * Tx * nt + 2.0 * (pos + 1) * nt) + 2.0 * V * nt);
+            }
+        }
+        out->alg_bytes = bytes;
+        out->alg_flops = flops;
+        snprintf(out->name, sizeof out->name, "k_dec_persist<%d,%d> (%d steps)", (int)nt, B == 1 ? 1 : 8, steps);
     } else {
         const double N = hp.n_text_layer * 2.0 * nt;
         out->alg_flops = 2.0 * M * N * n;
