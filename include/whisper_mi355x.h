@@ -223,7 +223,9 @@ int wmi_selftest(wmi_context *ctx, int32_t *n_mismatch);
  * and bytes).  which: 0 / 1 = the kernel chain's residual-stream buffers
  * [8][n_text_state] f32, 2 = logits [8][n_vocab] f32 (the persistent
  * decoder fills them only with WMI_PERSIST_LOGITS=1), 3 = the persistent
- * decoder's exchange block (8-byte {tag, value} granules). */
+ * decoder's exchange block (8-byte {tag, value} granules), 4-9 = decoder
+ * chain scratch, 10 = this context's tuning knobs (10 int32, host copy; the
+ * WMI_* environment is read once per context at wmi_init_from_file). */
 int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes);
 
 /* ---- parity getters (copy device results into caller-owned buffers) --- */
@@ -243,10 +245,15 @@ size_t wmi_dist_id_size(void);
 /* Rank 0 creates the id; every rank passes the same bytes to init. */
 int wmi_dist_make_id(void *id_out);
 int wmi_dist_init(wmi_context *ctx, int rank, int world, const void *id);
-/* Gather every rank's token block ([n_clips][n_decode] int32 + counts) to
- * root 0 over RCCL; out (root only) is [world][n_clips][n_decode]. */
+/* Gather every rank's token block to root 0 over RCCL (ncclGather).  A block
+ * is [n_clips][1 + n_decode] int32: per clip its token count, then its tokens
+ * (-1 padded) — greedy or beam, whichever the last staged run was.  Every
+ * rank must have staged the same n_clips and n_decode (checked with an
+ * all-reduce first: WMI_E_INVALID_ARG on every rank otherwise).  out (root
+ * only; others may pass NULL) is [world][n_clips][1 + n_decode]. */
 int wmi_dist_gather_tokens(wmi_context *ctx, int32_t *out, size_t cap);
-/* Device-side barrier over the communicator (an RCCL all-reduce of one int). */
+/* Device-side barrier over the communicator (an RCCL all-reduce of a
+ * dedicated int; gathered tokens are never touched). */
 int wmi_dist_barrier(wmi_context *ctx);
 
 #ifdef __cplusplus

@@ -47,3 +47,49 @@ def test_two_rank_shard_and_gather(micro_model):
     import dist_worker
     full = np.concatenate([dist_worker.decode_shard(micro_model, r, cpg, n_tok) for r in range(world)])
     np.testing.assert_array_equal(tcp.reshape(world * cpg, n_tok), full)
+
+
+def test_rendezvous_messages_are_data_only():
+    """The TCP star carries JSON (bytes hex-tagged), never pickles."""
+    import dist
+    obj = [b"\x00\x01uid", 1.5, None, [1, 2, 3], "s"]
+    assert dist._dec(dist._enc(obj)) == obj
+    import pytest
+    with pytest.raises(TypeError):
+        dist._enc(object())
+    with pytest.raises(ValueError):
+        dist._dec(b'{"b": "00", "x": 1}')
+
+
+def test_rendezvous_rejects_bad_ranks():
+    """Rank 0 drops peers announcing an out-of-range or duplicate rank."""
+    import struct
+    import threading
+
+    import dist
+    port = _free_port()
+    res = {}
+
+    def hub():
+        g = dist.Group(0, 2, "127.0.0.1", port, timeout=30)
+        res["gather"] = g.all_gather("hub")
+        g.close()
+
+    t = threading.Thread(target=hub)
+    t.start()
+    import time
+    for _ in range(100):  # the hub is listening once a connection succeeds
+        try:
+            rogue = socket.create_connection(("127.0.0.1", port), timeout=5)
+            break
+        except OSError:
+            time.sleep(0.05)
+    dist._send(rogue, struct.pack("<i", 7))  # world is 2: rank 7 is refused
+    rogue.settimeout(5)
+    assert rogue.recv(1) == b""  # closed by the hub
+    rogue.close()
+    peer = dist.Group(1, 2, "127.0.0.1", port, timeout=30)
+    assert peer.all_gather("peer") == ["hub", "peer"]
+    peer.close()
+    t.join(30)
+    assert res["gather"] == ["hub", "peer"]

@@ -273,6 +273,7 @@ struct wmi_context {
     std::vector<std::string> trace_names;
     std::vector<std::string> phase_names = std::vector<std::string>(32);  // phase slots 32.. (layer 0 GEMVs, logits)
     // persistent decoder (wmi_persist.hip): greedy steps in one launch
+    Tune tune;                        // WMI_* knobs of this context (wmi_internal.h)
     bool use_persist = true;          // WMI_PERSIST=0: kernel chain instead
     bool persist_logits = false;      // WMI_PERSIST_LOGITS=1: also store every step's logits (dlogits)
     int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
@@ -286,7 +287,10 @@ struct wmi_context {
     // dist
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
-    int32_t *d_gather = nullptr;
+    int32_t *d_gather = nullptr;       // root: [world][clips][1 + n_decode]
+    int32_t *d_dsend = nullptr;        // this rank's [clips][1 + n_decode] block
+    int32_t *d_dctl = nullptr;         // [0]: barrier word, [4..8): shape check
+    int32_t *d_dbar = nullptr, *d_dshape = nullptr;
     size_t gather_cap = 0;
 };
 
@@ -1057,7 +1061,7 @@ int run_encode(wmi_context *ctx, int mel_offset) {
         g.A = ctx->xln; g.lda = n; g.B = e.wqkv; g.bias = e.bqkv; g.M = M; g.N = 3 * n; g.K = n;
         g.q = ctx->q; g.k = ctx->k; g.vt = ctx->vt; g.T = T; g.Tp = Tp; g.n_state = n;
         HIPCHK(ctx, launch_gemm(s, EPI_QKV, g));
-        AttnArgs at{};
+        AttnArgs at{}; at.tune = &ctx->tune;
         at.q = ctx->q; at.k = ctx->k; at.vt = ctx->vt; at.out = ctx->att; at.exp_tab = ctx->exp_tab;
         at.n_exp = ctx->n_exp; at.T = T; at.Tp = Tp; at.H = H; at.n_state = n; at.n_clips = B;
         at.scale = (float)(1.0 / sqrt(64.0));
@@ -1171,7 +1175,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         const DecLayerDev &d = ctx->dec[l];
         uint16_t *kc = ctx->kcache + (size_t)l * DEC_ROWS * hp.n_text_ctx * n;
         uint16_t *vc = ctx->vcache + (size_t)l * DEC_ROWS * hp.n_text_ctx * n;
-        DecGemvArgs g{};
+        DecGemvArgs g{}; g.tune = &ctx->tune;
         const bool q5 = ctx->use_q5;
         g.x = X[cur]; g.ln_w = d.ln1_w; g.ln_b = d.ln1_b; g.W = d.wqkv; g.bias = d.bqkv; g.N = 3 * n; g.K = n; g.B = B;
         g.Wq5 = q5 ? d.wqkv5 : nullptr;
@@ -1192,7 +1196,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         g.trace = tslot(ctx, "qkv", l);
         if (l == 0) g.phase = pslot(ctx, 0, "qkv[0]");
         HIPCHK(ctx, launch_dec_gemv(s, DEC_QKV, g));
-        DecAttnArgs at{};
+        DecAttnArgs at{}; at.tune = &ctx->tune;
         at.q = ctx->dq16; at.K = kc; at.V = vc; at.clip_stride = (int64_t)hp.n_text_ctx * n; at.M_fixed = 0;
         at.mk = ctx->self_mk; at.err = ctx->derr;
         at.st = ctx->dstate; at.S = ctx->dS; at.s_stride = ctx->s_stride; at.cmax = ctx->dcmax;
@@ -1258,7 +1262,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         if (l == 0) g.phase = pslot(ctx, 4, "mlp1[0]");
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
     }
-    DecGemvArgs g{};
+    DecGemvArgs g{}; g.tune = &ctx->tune;
     g.x = X[cur]; g.ln_w = ctx->dln_w; g.ln_b = ctx->dln_b; g.W = ctx->te; g.N = hp.n_vocab; g.K = n; g.B = B;
     g.Wq5 = ctx->use_q5 ? ctx->te5 : nullptr;
     g.out32 = ctx->dlogits; g.amax = ctx->damax; g.suppress_id = suppress_eot ? ctx->sp.eot : -1;
@@ -1311,7 +1315,6 @@ int dec_err(wmi_context *ctx, uint32_t err) {
     return set_err(ctx, WMI_E_HIP, "internal: self-attention key capacity below pos + 1 (err word %u)", err);
 }
 
-int g_graph_steps = 8;  // decoder steps per captured graph (WMI_GRAPH_STEPS; base: 1 -> 8 steps 31.4 -> 30.9 ms)
 
 // self-attention key capacity for M = pos + 1 keys
 int self_mk_for(int M) { return M <= 64 ? 64 : M <= 128 ? 128 : M <= 256 ? 256 : 512; }
@@ -1337,7 +1340,7 @@ int run_dec_steps(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride
         }
         // graphs of `reps` consecutive steps (WMI_GRAPH_STEPS) cut the
         // replays per token; the remainder runs through the one-step graph
-        for (int reps : {g_graph_steps, 1}) {
+        for (int reps : {ctx->tune.graph_steps, 1}) {  // (base: 1 -> 8 steps 31.4 -> 30.9 ms)
             if (reps < 1 || (reps > 1 && n < reps)) continue;
             char key[192];
             snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%p/%p/%d/%d/%d/%d/%d", b0, B, feed_len, feed_stride,
@@ -1877,16 +1880,23 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_ptrace, nb));
         HIPCHK(ctx.get(), hipMemset(ctx->d_ptrace, 0, nb));
     }
-    if (const char *c = getenv("WMI_ATTN_V1")) g_attn_v1 = atoi(c) == 2 ? 2 : 1;
-    if (const char *c = getenv("WMI_LOGITS_CAP")) g_logits_cap = atoi(c) > 0 ? atoi(c) : g_logits_cap;
-    if (const char *c = getenv("WMI_LOGITS_G")) g_logits_g = atoi(c);
-    if (const char *c = getenv("WMI_GRAPH_STEPS")) g_graph_steps = atoi(c) > 0 ? atoi(c) : 1;
-    if (const char *c = getenv("WMI_DOWN_NW1_B")) g_down_nw1_b = atoi(c);
-    if (const char *c = getenv("WMI_LOGITS_CAP2")) g_logits_cap2 = atoi(c) > 0 ? atoi(c) : g_logits_cap2;
-    if (const char *c = getenv("WMI_GEMV_NW")) g_gemv_nw = atoi(c) == 1 ? 1 : atoi(c) == 0 ? 0 : 4;
-    if (const char *c = getenv("WMI_COOP_MAX")) g_coop_max = atoi(c) > 0 ? atoi(c) : g_coop_max;
-    if (const char *c = getenv("WMI_XATTN_ROWS")) g_xattn_rows = atoi(c);
-    if (const char *c = getenv("WMI_SELF_SPLIT")) g_self_split = atoi(c) >= 0 ? atoi(c) : g_self_split;
+    Tune &tn = ctx->tune;  // per context: two contexts never see each other's knobs
+    auto knob = [](const char *name, int &v, int lo) {
+        if (const char *c = getenv(name)) {
+            const int x = atoi(c);
+            if (x >= lo) v = x;
+        }
+    };
+    if (const char *c = getenv("WMI_ATTN_V1")) tn.attn_v1 = atoi(c) == 2 ? 2 : atoi(c) == 1 ? 1 : 0;
+    knob("WMI_LOGITS_CAP", tn.logits_cap, 1);
+    knob("WMI_LOGITS_G", tn.logits_g, 0);
+    knob("WMI_GRAPH_STEPS", tn.graph_steps, 1);
+    knob("WMI_DOWN_NW1_B", tn.down_nw1_b, 0);
+    knob("WMI_LOGITS_CAP2", tn.logits_cap2, 1);
+    if (const char *c = getenv("WMI_GEMV_NW")) tn.gemv_nw = atoi(c) == 1 ? 1 : atoi(c) == 0 ? 0 : 4;
+    knob("WMI_COOP_MAX", tn.coop_max, 1);
+    knob("WMI_XATTN_ROWS", tn.xattn_rows, 0);
+    knob("WMI_SELF_SPLIT", tn.self_split, 0);
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_trace, TRACE_SLOTS * 16 + 64 * 16 * 8));
@@ -1907,6 +1917,8 @@ void wmi_free(wmi_context *ctx) {
     if (ctx->dfeed) (void)hipFree(ctx->dfeed);
     if (ctx->dtokens) (void)hipFree(ctx->dtokens);
     if (ctx->d_gather) (void)hipFree(ctx->d_gather);
+    if (ctx->d_dsend) (void)hipFree(ctx->d_dsend);
+    if (ctx->d_dctl) (void)hipFree(ctx->d_dctl);
     if (ctx->d_ws) (void)hipFree(ctx->d_ws);
     if (ctx->d_trace) (void)hipFree(ctx->d_trace);
     if (ctx->d_model) (void)hipFree(ctx->d_model);
@@ -2316,7 +2328,7 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
     }
     auto launch = [&]() -> int {
         if (which == 0) {
-            DecGemvArgs g{};
+            DecGemvArgs g{}; g.tune = &ctx->tune;
             g.x = ctx->dx; g.ln_w = ctx->dln_w; g.ln_b = ctx->dln_b; g.W = ctx->te; g.N = hp.n_vocab;
             g.Wq5 = ctx->use_q5 ? ctx->te5 : nullptr;
             g.K = hp.n_text_state; g.B = B < 8 ? B : 8;
@@ -2329,7 +2341,7 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
             g.out16 = ctx->hid; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
             HIPCHK(ctx, launch_gemm(s, EPI_GELU16, g));
         } else if (which == 2) {
-            AttnArgs at{};
+            AttnArgs at{}; at.tune = &ctx->tune;
             at.q = ctx->q; at.k = ctx->k; at.vt = ctx->vt; at.out = ctx->att; at.exp_tab = ctx->exp_tab;
             at.n_exp = ctx->n_exp; at.T = T; at.Tp = (int)up(T, 64); at.H = hp.n_audio_head; at.n_state = n;
             at.n_clips = B; at.scale = 0.125f;
@@ -2446,6 +2458,13 @@ int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes) {
         case 7: src = ctx->vcache; have = (size_t)ctx->hp.n_text_layer * R * ctx->hp.n_text_ctx * n * 2; break;
         case 8: src = ctx->dS; have = R * (size_t)ctx->hp.n_text_head * ctx->s_stride * 4; break;
         case 9: src = ctx->dopart; have = R * (size_t)ctx->n_chunks_max * n * 4; break;
+        case 10: {  // host: this context's tuning knobs (struct Tune, int32 fields in order)
+            const Tune &t = ctx->tune;
+            const int32_t v[10] = {t.attn_v1, t.logits_cap, t.logits_g, t.logits_cap2, t.down_nw1_b,
+                                   t.gemv_nw, t.coop_max, t.xattn_rows, t.self_split, t.graph_steps};
+            memcpy(out, v, std::min(sizeof v, bytes));
+            return WMI_OK;
+        }
         default: return WMI_E_INVALID_ARG;
     }
     if (hipMemcpy(out, src, std::min(have, bytes), hipMemcpyDeviceToHost) != hipSuccess) return WMI_E_HIP;
@@ -2465,6 +2484,31 @@ int wmi_selftest(wmi_context *ctx, int32_t *n_mismatch) {
     *n_mismatch = (int32_t)mm;
     return WMI_OK;
 }
+
+}  // extern "C"
+
+// gather buffers (total int32 on the root side; 0: control words only)
+static int ensure_dist_buffers(wmi_context *ctx, size_t total) {
+    if (!ctx->d_dctl) {
+        HIPCHK(ctx, hipMalloc(&ctx->d_dctl, 64));
+        HIPCHK(ctx, hipMemset(ctx->d_dctl, 0, 64));
+        ctx->d_dbar = ctx->d_dctl;
+        ctx->d_dshape = ctx->d_dctl + 4;
+    }
+    if (total > ctx->gather_cap) {
+        if (ctx->d_gather) HIPCHK(ctx, hipFree(ctx->d_gather));
+        if (ctx->d_dsend) HIPCHK(ctx, hipFree(ctx->d_dsend));
+        ctx->d_gather = nullptr;
+        ctx->d_dsend = nullptr;
+        ctx->gather_cap = 0;
+        HIPCHK(ctx, hipMalloc(&ctx->d_gather, total * 4));
+        HIPCHK(ctx, hipMalloc(&ctx->d_dsend, total * 4));  // >= one rank's block
+        ctx->gather_cap = total;
+    }
+    return WMI_OK;
+}
+
+extern "C" {
 
 size_t wmi_dist_id_size(void) { return sizeof(ncclUniqueId); }
 
@@ -2490,15 +2534,42 @@ int wmi_dist_init(wmi_context *ctx, int rank, int world, const void *id) {
 
 int wmi_dist_gather_tokens(wmi_context *ctx, int32_t *out, size_t cap) {
     if (!valid(ctx) || !ctx->comm) return WMI_E_INVALID_ARG;
+    if (ctx->enc_clips < 1 || ctx->staged_n_decode < 1) return set_err(ctx, WMI_E_INVALID_ARG, "gather before a staged run");
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    const size_t count = (size_t)ctx->enc_clips * ctx->staged_n_decode;
-    const size_t total = count * ctx->world;
-    if (total > ctx->gather_cap) {
-        if (ctx->d_gather) HIPCHK(ctx, hipFree(ctx->d_gather));
-        HIPCHK(ctx, hipMalloc(&ctx->d_gather, total * 4));
-        ctx->gather_cap = total;
+    const int nd = ctx->staged_n_decode, rec = nd + 1;
+    // every rank must send the same block shape (ncclGather counts are equal):
+    // all-reduce {clips, n_decode, -clips, -n_decode} with MAX
+    int rc = ensure_dist_buffers(ctx, 0);
+    if (rc) return rc;
+    const int32_t shp[4] = {ctx->enc_clips, nd, -ctx->enc_clips, -nd};
+    int32_t got[4];
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_dshape, shp, sizeof shp, hipMemcpyHostToDevice, ctx->stream));
+    RCCLCHK(ctx, ncclAllReduce(ctx->d_dshape, ctx->d_dshape, 4, ncclInt32, ncclMax, ctx->comm, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(got, ctx->d_dshape, sizeof got, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (got[0] != -got[2] || got[1] != -got[3])
+        return set_err(ctx, WMI_E_INVALID_ARG, "token blocks differ across ranks (clips %d..%d, n_decode %d..%d)",
+                       -got[2], got[0], -got[3], got[1]);
+    // this rank's block [clips][1 + n_decode]: token count, then the tokens (-1 padded)
+    const size_t count = (size_t)ctx->enc_clips * rec, total = count * ctx->world;
+    rc = ensure_dist_buffers(ctx, total);
+    if (rc) return rc;
+    std::vector<int32_t> blk(count, -1);
+    if (!ctx->staged_beam.empty()) {  // beam results live on the host
+        for (int c = 0; c < ctx->enc_clips; ++c) {
+            const std::vector<int32_t> &sq = ctx->staged_beam[c];
+            const int k = (int)sq.size() < nd ? (int)sq.size() : nd;
+            blk[(size_t)c * rec] = k;
+            for (int i = 0; i < k; ++i) blk[(size_t)c * rec + 1 + i] = sq[i];
+        }
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_dsend, blk.data(), count * 4, hipMemcpyHostToDevice, ctx->stream));
+    } else {  // greedy tokens stay on the device: [clips][nd] -> rows of rec
+        for (int c = 0; c < ctx->enc_clips; ++c) blk[(size_t)c * rec] = nd;
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_dsend, blk.data(), count * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(ctx, hipMemcpy2DAsync(ctx->d_dsend + 1, (size_t)rec * 4, ctx->dtokens, (size_t)nd * 4, (size_t)nd * 4,
+                                     ctx->enc_clips, hipMemcpyDeviceToDevice, ctx->stream));
     }
-    RCCLCHK(ctx, ncclGather(ctx->dtokens, ctx->d_gather, count, ncclInt32, 0, ctx->comm, ctx->stream));
+    RCCLCHK(ctx, ncclGather(ctx->d_dsend, ctx->d_gather, count, ncclInt32, 0, ctx->comm, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->rank == 0 && out) {
         if (cap < total) return WMI_E_NO_SPACE;
@@ -2510,12 +2581,10 @@ int wmi_dist_gather_tokens(wmi_context *ctx, int32_t *out, size_t cap) {
 int wmi_dist_barrier(wmi_context *ctx) {
     if (!valid(ctx) || !ctx->comm) return WMI_E_INVALID_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    if (ctx->gather_cap < 1) {
-        if (ctx->d_gather) HIPCHK(ctx, hipFree(ctx->d_gather));
-        HIPCHK(ctx, hipMalloc(&ctx->d_gather, 4 * 4));
-        ctx->gather_cap = 4;
-    }
-    RCCLCHK(ctx, ncclAllReduce(ctx->d_gather, ctx->d_gather, 1, ncclInt32, ncclSum, ctx->comm, ctx->stream));
+    int rc = ensure_dist_buffers(ctx, 0);
+    if (rc) return rc;
+    // a word of its own: the all-reduce never touches gathered tokens
+    RCCLCHK(ctx, ncclAllReduce(ctx->d_dbar, ctx->d_dbar, 1, ncclInt32, ncclSum, ctx->comm, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return WMI_OK;
 }

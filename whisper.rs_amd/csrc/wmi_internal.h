@@ -55,6 +55,24 @@ enum GemmEpi {
     EPI_CROSSKV = 6,    // K: f16(acc * kscale), V: f16(acc + bias) -> [l][b][T][ns]
 };
 
+// Tuning knobs of one context (WMI_* environment variables read at
+// wmi_init_from_file).  Kernel-argument structs carry a pointer to their
+// context's copy; a null pointer means the defaults below.
+struct Tune {
+    int attn_v1 = 0;        // WMI_ATTN_V1: encoder attention version (1: v1, 2: v2, 0: v3)
+    int logits_cap = 512;   // WMI_LOGITS_CAP: chain logits grid cap
+    int logits_g = 2;       // WMI_LOGITS_G: logits rows per lane group
+    int logits_cap2 = 1024; // WMI_LOGITS_CAP2
+    int down_nw1_b = 0;     // WMI_DOWN_NW1_B: MLP-down GEMV with one wave per WG up to this many rows
+    int gemv_nw = 4;        // WMI_GEMV_NW: waves per decoder GEMV workgroup (1, 4; 0 auto)
+    int coop_max = 512;     // WMI_COOP_MAX: cooperative cross-attention up to this many workgroups
+    int xattn_rows = 1;     // WMI_XATTN_ROWS: beam rows share cross-attention phase A (1 auto, 2 always, 0 never)
+    int self_split = 1;     // WMI_SELF_SPLIT: self-attention output projection over n / 128 WGs per head
+    int graph_steps = 8;    // WMI_GRAPH_STEPS: chain decoder steps per captured graph
+};
+extern const Tune kTuneDefault;
+inline const Tune &tune_of(const Tune *t) { return t ? *t : kTuneDefault; }
+
 struct GemmArgs {
     const uint16_t *A;  // plain: [M][lda]; conv: X[b][Tin + 2][Cp]
     const uint16_t *B;  // [N][K]
@@ -80,6 +98,7 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a);
 
 // ---- encoder self-attention (ggml flash_attn_f16 semantics, exact softmax) --
 struct AttnArgs {
+    const Tune *tune;  // context knobs (null: defaults)
     const uint16_t *q, *k, *vt;  // [b][h][Tp][64], vt [b][h][64][Tp]
     uint16_t *out;               // [b*T + t][n_state]
     const uint16_t *exp_tab;     // f16 exp table, negative half
@@ -88,7 +107,6 @@ struct AttnArgs {
     float scale;
 };
 hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a);
-extern int g_attn_v1;
 
 // ---- decoder step -----------------------------------------
 struct DecState {          // device-resident, advanced by the kernels
@@ -99,6 +117,7 @@ struct DecState {          // device-resident, advanced by the kernels
 enum DecEpi { DEC_QKV = 0, DEC_Q = 1, DEC_GELU = 2, DEC_RESID = 3, DEC_LOGITS = 4 };
 
 struct DecGemvArgs {
+    const Tune *tune;  // context knobs (null: defaults)
     const float *x;          // LN input [B][K] f32 (ln != null)
     const float *ln_w, *ln_b;
     const uint16_t *xin16;   // non-LN input [B][K] f16
@@ -136,16 +155,9 @@ struct DecGemvArgs {
 constexpr int AMAX_SHARDS = 64;
 constexpr int DEC_ROWS = 8;  // decoder rows per step: clips (greedy) or beam hypotheses
 hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a);
-extern int g_logits_cap;
-extern int g_logits_g;
-extern int g_down_nw1_b;
-extern int g_logits_cap2;
-extern int g_gemv_nw;
-extern int g_self_split;
-extern int g_xattn_rows;
-extern int g_coop_max;
 
 struct DecAttnArgs {
+    const Tune *tune;  // context knobs (null: defaults)
     const uint16_t *q;       // [B][n]
     const uint16_t *K, *V;   // per clip: rows of n (clip_stride elements apart)
     int64_t clip_stride;     // elements between clips in K/V

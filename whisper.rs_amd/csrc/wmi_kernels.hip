@@ -1051,7 +1051,6 @@ __global__ __launch_bounds__(512) void k_attn_enc3(AttnArgs a) {
     }
 }
 
-int g_attn_v1 = 0;  // WMI_ATTN_V1=1: the original three-QK-pass kernel; 2: version 2; 0: version 3
 
 hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a) {
     dim3 grid(cdiv(a.T, ATT_QB), a.H, a.n_clips);
@@ -1059,13 +1058,14 @@ hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a) {
     const size_t ebytes = (size_t)cdiv(a.T, 32) * 64 * 16 * 2, obytes = (size_t)(ATT2_W - 1) * 32 * 64 * 4;
     const size_t lds2 = tabb + ATT2_W * 32 * 4 + ATT2_W * 32 * 8 + (ebytes > obytes ? ebytes : obytes);
     const size_t lds3 = tabb + ATT2_W * 32 * 4 + ATT2_W * 32 * 8 + obytes;
-    if (g_attn_v1 == 0 && lds3 <= 160 * 1024 && cdiv(a.T, 32) <= ATT2_W * ATT2_TPW) {
+    const Tune &tn = tune_of(a.tune);
+    if (tn.attn_v1 == 0 && lds3 <= 160 * 1024 && cdiv(a.T, 32) <= ATT2_W * ATT2_TPW) {
         hipError_t e = allow_lds(k_attn_enc3, lds3);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_attn_enc3, grid, dim3(64 * ATT2_W), lds3, s, a);
         return hipGetLastError();
     }
-    if (g_attn_v1 != 1 && lds2 <= 160 * 1024 && cdiv(a.T, 32) <= ATT2_W * ATT2_TPW) {
+    if (tn.attn_v1 != 1 && lds2 <= 160 * 1024 && cdiv(a.T, 32) <= ATT2_W * ATT2_TPW) {
         hipError_t e = allow_lds(k_attn_enc2, lds2);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_attn_enc2, grid, dim3(64 * ATT2_W), lds2, s, a);
@@ -1528,20 +1528,12 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
     trace_end(a.trace);
 }
 
-int g_logits_cap = 512;  // persistent logits grid (WMI_LOGITS_CAP overrides; 2 workgroups per CU at ~210 VGPRs)
 // waves per workgroup of the per-layer GEMVs (WMI_GEMV_NW=1 / 0 = one wave /
 // one wave at B <= 2): 4 measured fastest at base, B = 1 (one wave per
 // workgroup: mlp0 4.6 -> 10 us, every workgroup repeating the LayerNorm)
-int g_gemv_nw = 4;
 // row groups per register set of the vocabulary GEMV at K <= 512 (WMI_LOGITS_G
 // = 1 / 2 / 4) and its persistent grid cap (WMI_LOGITS_CAP2): base 13.9 us at
 // G = 1 -> 12.1 us at G = 2 over 1024 workgroups
-int g_logits_g = 2;
-int g_logits_cap2 = 1024;
-int g_down_nw1_b = 0;    // MLP-down GEMV with one wave per workgroup up to this many rows (WMI_DOWN_NW1_B)
-int g_coop_max = 512;    // cooperative cross-attention up to this many workgroups (WMI_COOP_MAX)
-int g_xattn_rows = 1;    // beam rows share cross-attention phase A: 1 auto (n > 768), 2 always, 0 never (WMI_XATTN_ROWS)
-int g_self_split = 1;    // self-attention output projection over n / 128 workgroups per head (WMI_SELF_SPLIT=0: one)
 
 template <int EPI, int IN, int WQ, int NW>
 static hipError_t dec_gemv_nw(hipStream_t s, const DecGemvArgs &a) {
@@ -1549,7 +1541,8 @@ static hipError_t dec_gemv_nw(hipStream_t s, const DecGemvArgs &a) {
     dim3 block(64 * NW);
     // the vocabulary GEMV runs persistent and pipelined (its K = n_state <=
     // 1280 fits one sweep of either chunk size); the others one group per WG
-    const int cap = EPI == DEC_LOGITS ? g_logits_cap : 1 << 30;
+    const Tune &tn = tune_of(a.tune);
+    const int cap = EPI == DEC_LOGITS ? tn.logits_cap : 1 << 30;
     const int nrg = cdiv(a.N, 4 * NW);
     const dim3 grid(nrg < cap ? nrg : cap);
     if constexpr (WQ == 1) {  // q5_1: 4 chunks of 512 weights (K <= 2048 per sweep)
@@ -1562,13 +1555,13 @@ static hipError_t dec_gemv_nw(hipStream_t s, const DecGemvArgs &a) {
         hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 1, 16, 0, NW>, lds);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((k_dec_gemv<EPI, IN, 1, 16, 0, NW>), grid, block, lds, s, a);
-    } else if (EPI == DEC_LOGITS && a.K <= 512 && g_logits_g > 1) {
+    } else if (EPI == DEC_LOGITS && a.K <= 512 && tn.logits_g > 1) {
         // K <= 512: 4 chunks cover a row, so each register set can hold G = 2
         // or 4 row groups (more bytes in flight per wave at the same VGPRs)
         // (128 VGPRs at G = 2: four workgroups per CU, hence the larger cap;
         // a balanced grid of equal row-group counts measured slower)
-        const int G = g_logits_g == 2 ? 2 : 4, ng = cdiv(a.N, 4 * NW * G);
-        const dim3 grid2(ng < g_logits_cap2 ? ng : g_logits_cap2);
+        const int G = tn.logits_g == 2 ? 2 : 4, ng = cdiv(a.N, 4 * NW * G);
+        const dim3 grid2(ng < tn.logits_cap2 ? ng : tn.logits_cap2);
         if (G == 2) {
             hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 2, 4, 0, NW>, lds);
             if (e != hipSuccess) return e;
@@ -1595,8 +1588,9 @@ static hipError_t dec_gemv_g(hipStream_t s, const DecGemvArgs &a) {
     } else {
         // the MLP down projection (K = 4n, no LayerNorm) streams 4x the bytes
         // per row: one wave per workgroup spreads them over 4x the CUs
-        const bool down = EPI == DEC_RESID && IN == 1 && a.K > 1024 && a.B <= g_down_nw1_b;
-        const bool one = down || g_gemv_nw == 1 || (g_gemv_nw == 0 && a.B <= 2);
+        const Tune &tn = tune_of(a.tune);
+        const bool down = EPI == DEC_RESID && IN == 1 && a.K > 1024 && a.B <= tn.down_nw1_b;
+        const bool one = down || tn.gemv_nw == 1 || (tn.gemv_nw == 0 && a.B <= 2);
         return one ? dec_gemv_nw<EPI, IN, WQ, 1>(s, a) : dec_gemv_nw<EPI, IN, WQ, 4>(s, a);
     }
 }
@@ -2224,11 +2218,14 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
 }
 
 
+const Tune kTuneDefault{};
+
 hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
+    const Tune &tn = tune_of(a.tune);
     if (a.M_fixed == 0) {  // self-attention: M = pos + 1 <= 512
         if (a.n_chunks != 1 || (a.Wo && !a.wo_parts)) return hipErrorInvalidValue;
         // fused output projection split over n / 128 workgroups per head
-        const int S = (g_self_split && a.Wo && a.n % 128 == 0) ? a.n / 128 : 1;
+        const int S = (tn.self_split && a.Wo && a.n % 128 == 0) ? a.n / 128 : 1;
         const dim3 grid(a.H, a.B, S);
         switch (a.mk) {
             case 64: hipLaunchKernelGGL(k_dec_self_attn<64>, grid, dim3(256), 0, s, a); break;
@@ -2246,12 +2243,12 @@ hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
     // cooperative single kernel while the grid stays far inside residency
     // (<= 2 workgroups per CU) and the Wq rows fit the register budget;
     // otherwise the two-kernel form
-    const bool coop = a.sync && a.n_chunks * a.H * a.B <= g_coop_max && a.n <= 768;
+    const bool coop = a.sync && a.n_chunks * a.H * a.B <= tn.coop_max && a.n <= 768;
     // beam rows sharing one clip: phase A once per (chunk, head) for all rows
     // (auto: n > 768, where the head's Wq rows dominate a workgroup's reads —
     // large-v3 x 5 beams 498 -> 448 ms decode; small x 5 beams is faster per
     // row, 122 vs 132 ms, as 144 workgroups serialising 5 rows under-fill)
-    if (!coop && (g_xattn_rows == 2 || (g_xattn_rows == 1 && a.n > 768)) && a.B > 1 && a.B <= 8 &&
+    if (!coop && (tn.xattn_rows == 2 || (tn.xattn_rows == 1 && a.n > 768)) && a.B > 1 && a.B <= 8 &&
         a.clip_div == a.B) {
         const dim3 g1(a.n_chunks, a.H, 1);
 #define XR(KC)                                                                   \

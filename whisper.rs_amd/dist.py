@@ -9,13 +9,41 @@ import: the benchmark process must load exactly one HIP runtime (ours).
 """
 from __future__ import annotations
 
+import json
 import os
-import pickle
 import socket
 import struct
 import time
 
 _PORT_OFFSET = 23  # torchrun's own TCPStore holds MASTER_PORT itself
+_MAX_MSG = 1 << 24  # messages are ids, timings and small token lists
+
+
+def _enc(obj) -> bytes:
+    """JSON with bytes as {"b": hex}: the payloads are plain data (an RCCL
+    unique id, floats, None, small int lists), so nothing a peer sends is ever
+    executed (no pickle)."""
+    def conv(o):
+        if isinstance(o, (bytes, bytearray)):
+            return {"b": bytes(o).hex()}
+        if isinstance(o, (list, tuple)):
+            return [conv(x) for x in o]
+        if o is None or isinstance(o, (bool, int, float, str)):
+            return o
+        raise TypeError(f"dist: cannot send {type(o).__name__}")
+    return json.dumps(conv(obj)).encode()
+
+
+def _dec(data: bytes):
+    def conv(o):
+        if isinstance(o, dict):
+            if set(o) != {"b"} or not isinstance(o["b"], str):
+                raise ValueError("dist: malformed message")
+            return bytes.fromhex(o["b"])
+        if isinstance(o, list):
+            return [conv(x) for x in o]
+        return o
+    return conv(json.loads(data.decode()))
 
 
 def env_rank_world():
@@ -35,6 +63,8 @@ def _recv(sock) -> bytes:
             raise ConnectionError("peer closed")
         hdr += chunk
     (n,) = struct.unpack("<Q", hdr)
+    if n > _MAX_MSG:
+        raise ConnectionError(f"dist: message of {n} bytes refused")
     buf = bytearray()
     while len(buf) < n:
         chunk = sock.recv(min(1 << 20, n - len(buf)))
@@ -45,7 +75,7 @@ def _recv(sock) -> bytes:
 
 
 class Group:
-    """All-gather of small picklable objects over a TCP star (rank 0 hub)."""
+    """All-gather of small plain-data objects over a TCP star (rank 0 hub)."""
 
     def __init__(self, rank: int, world: int, addr: str | None = None, port: int | None = None,
                  timeout: float = 300.0):
@@ -66,7 +96,15 @@ class Group:
             while len(peers) < world - 1:
                 c, _ = srv.accept()
                 c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                r = struct.unpack("<i", _recv(c))[0]
+                c.settimeout(timeout)
+                try:
+                    hello = _recv(c)
+                    r = struct.unpack("<i", hello)[0] if len(hello) == 4 else -1
+                except (ConnectionError, OSError):
+                    r = -1
+                if not 1 <= r < world or r in peers:  # out of range or duplicate: not a peer
+                    c.close()
+                    continue
                 peers[r] = c
             srv.close()
             self.peers = [peers[r] for r in range(1, world)]
@@ -89,13 +127,13 @@ class Group:
         if self.world == 1:
             return [obj]
         if self.rank == 0:
-            objs = [obj] + [pickle.loads(_recv(p)) for p in self.peers]
-            blob = pickle.dumps(objs)
+            objs = [obj] + [_dec(_recv(p)) for p in self.peers]
+            blob = _enc(objs)
             for p in self.peers:
                 _send(p, blob)
-            return objs
-        _send(self.sock, pickle.dumps(obj))
-        return pickle.loads(_recv(self.sock))
+            return _dec(blob)
+        _send(self.sock, _enc(obj))
+        return _dec(_recv(self.sock))
 
     def broadcast(self, obj, root: int = 0):
         return self.all_gather(obj if self.rank == root else None)[root]

@@ -407,10 +407,16 @@ class WhisperContext:
         self.rank, self.world = rank, world
 
     def dist_gather_tokens(self):
-        total = self.world * self.n_clips * self._n_decode
+        """Root: (tokens [world][clips][n_decode] with -1 padding, counts
+        [world][clips]); other ranks: None."""
+        rec = self._n_decode + 1
+        total = self.world * self.n_clips * rec
         out = np.zeros(total, np.int32) if self.rank == 0 else None
         _raise(lib().wmi_dist_gather_tokens(self._h, _ptr(out) if out is not None else None, total), self._h)
-        return None if out is None else out.reshape(self.world, self.n_clips, self._n_decode)
+        if out is None:
+            return None
+        blk = out.reshape(self.world, self.n_clips, rec)
+        return blk[:, :, 1:].copy(), blk[:, :, 0].copy()
 
     def dist_barrier(self) -> None:
         _raise(lib().wmi_dist_barrier(self._h), self._h)
