@@ -1460,15 +1460,15 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     a.kcache = ctx->kcache; a.vcache = ctx->vcache; a.ck = ctx->ck; a.cv = ctx->cv;
     a.L = ctx->dec_layers; a.n = n; a.V = hp.n_vocab; a.B = B; a.T = T; a.tctx = hp.n_text_ctx;
     a.Bt = ctx->enc_clips; a.b0 = b0;
-    // key chunks of 128 keys per (row, head), the chain's chunking (so the
-    // cross-attention sums group exactly as k_dec_xattn's, and the result
-    // does not depend on the row count); wider only where the task table
-    // would overflow (large-v3 x 8 rows)
+    // key chunks per (row, head): 128 keys, or — when the (row, head, chunk)
+    // tasks would need more than one round of the grid (several rows) —
+    // the smallest multiple of 128 (<= 512) that fits them in one round;
+    // always within the exchange block's task table
     int cl = 128;
-    while ((int64_t)B * H * ((T + cl - 1) / cl) > PX_TASKS && cl < 512) cl *= 2;
+    while (cl < 512 && ((int64_t)B * H * ((T + cl - 1) / cl) > G || (int64_t)B * H * ((T + cl - 1) / cl) > PX_TASKS))
+        cl += 128;
     a.cl = cl;
     a.nch = (T + cl - 1) / cl;
-    (void)G;
     a.qscale = powf((float)n / (float)H, -0.25f);
     a.st = ctx->dstate; a.feed = ctx->dfeed; a.feed_len = feed_len; a.feed_stride = feed_stride;
     a.tokens_out = ctx->dtokens + (size_t)b0 * out_stride; a.out_stride = out_stride;

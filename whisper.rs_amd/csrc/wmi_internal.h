@@ -307,7 +307,7 @@ __host__ __device__ inline XLayout persist_layout(int n, int H, int T) {
     L.h = o; o += R * 2 * n;
     L.s = o; o += R * H * T;
     L.m = o; o += PX_TASKS;
-    L.p = o; o += PX_TASKS * 64;
+    L.p = o; o += R * H * ((T + 127) / 128) * 64;  // 128-key P.V partials
     L.a = o; o += R * PX_GMAX * 2;
     L.ctl = o; o += 16;             // ctl[0] low word: abort flag
     L.total = (o + 15) / 16 * 16;   // whole 128-byte lines (memset size a multiple of 16 B)

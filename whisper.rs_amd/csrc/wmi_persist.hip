@@ -29,8 +29,9 @@
 //
 // Numerics are the decoder chain's (wmi_kernels.hip k_dec_*): the same f16
 // rounding points, double LayerNorm statistics, ggml exp/GELU tables, exact
-// softmax; only the grouping of f32 partial sums of the cross-attention
-// differs (key chunks of cl keys instead of 128).
+// softmax, P.V partials over 128-key chunks summed in chunk order (a task may
+// cover several chunks when many rows share the launch; it still publishes
+// one partial per 128 keys, so a row's result never depends on the batch).
 #include <hip/hip_runtime.h>
 
 #include "wmi_device.h"
@@ -104,7 +105,7 @@ struct PShared {
     float redf[4];
     double redd[4];
     unsigned long long best[4][PMAXB];
-    float ored[4][64];
+    float ored[4][64 * 4];  // per wave: up to NKP 64-float partials
     int abort_;
 };
 
@@ -340,6 +341,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     const int B = BT == 1 ? 1 : a.B, G = gridDim.x, wg = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int L = a.L, T = a.T, tctx = a.tctx, nch = a.nch, CL = a.cl;
+    const int nsub = (T + 127) >> 7;  // 128-key P.V partials per (row, head)
     float *xf = (float *)smem;                                          // [B][NS] f32
     f16 *xs = (f16 *)(smem + (size_t)B * NS * 4);                       // [B][4 NS] f16
     unsigned char *scr = smem + (size_t)B * NS * 4 + (size_t)B * NS * 8;  // SCR_BYTES
@@ -784,7 +786,14 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     if (lane == 0) sh.redd[w] = sum;
                     __syncthreads();
                     const float inv = (float)(1.0 / (((sh.redd[0] + sh.redd[1]) + sh.redd[2]) + sh.redd[3]));
-                    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                    // one partial per 128-key sub-chunk: the grouping of a
+                    // one-row run whatever the task's chunk (CL), so results
+                    // do not depend on how many rows share the launch
+                    float o[NKP][8];
+#pragma unroll
+                    for (int p = 0; p < NKP; ++p)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) o[p][e] = 0.0f;
 #pragma unroll
                     for (int p = 0; p < NKP; ++p)
                         if (j0 + 128 * p < j1) {  // workgroup-uniform
@@ -800,19 +809,24 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                 const int key = j0 + 128 * p + jg * 4 + u;
                                 const float pj = key < j1 ? h2f_bits(f2h_bits(sp[u] * inv)) : 0.0f;
 #pragma unroll
-                                for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vf[p][u][e];
+                                for (int e = 0; e < 8; ++e) o[p][e] = o[p][e] + pj * (float)vf[p][u][e];
                             }
                         }
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        o[e] = red_8_16_32(o[e]);
-                    }
+                    for (int p = 0; p < NKP; ++p)
+                        if (j0 + 128 * p < j1)
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) o[p][e] = red_8_16_32(o[p][e]);
                     if (lane < 8)
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) sh.ored[w][lane * 8 + e] = o[e];
+                        for (int p = 0; p < NKP; ++p)
+                            if (j0 + 128 * p < j1)
+#pragma unroll
+                                for (int e = 0; e < 8; ++e) sh.ored[w][p * 64 + lane * 8 + e] = o[p][e];
                     __syncthreads();
-                    if (tid < 64)
-                        gput(xg + oP + (int64_t)t * 64 + tid, tag,
+                    const int nsp = (j1 - j0 + 127) >> 7;  // sub-chunks of this task
+                    if (tid < 64 * nsp)
+                        gput(xg + oP + ((int64_t)bh * nsub + (j0 >> 7)) * 64 + tid, tag,
                              __float_as_uint(((sh.ored[0][tid] + sh.ored[1][tid]) + sh.ored[2][tid]) + sh.ored[3][tid]));
                     (void)Sv;
                 }
@@ -823,23 +837,23 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 6);
-                float *pp = (float *)scr;  // [nch][64]
+                float *pp = (float *)scr;  // [nsub][64]
                 for (int t = wg; t < B * H; t += G) {
                     const int b = t / H, h = t - b * H;
                     __syncthreads();
-                    const bool ok = gpoll(nch * 64, ptag(pos, L, l, 5), ptr_u64(xg + oP + (int64_t)t * nch * 64),
+                    const bool ok = gpoll(nsub * 64, ptag(pos, L, l, 5), ptr_u64(xg + oP + (int64_t)t * nsub * 64),
                                           (uint32_t *)pp, abortw, a.err);
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 22)
                     if (tid < 64) {  // in chunk order, 8 LDS reads in flight
                         float s = 0.0f;
-                        for (int c0 = 0; c0 < nch; c0 += 8) {
+                        for (int c0 = 0; c0 < nsub; c0 += 8) {
                             float v[8];
 #pragma unroll
-                            for (int u = 0; u < 8; ++u) v[u] = pp[(c0 + u < nch ? c0 + u : nch - 1) * 64 + tid];
+                            for (int u = 0; u < 8; ++u) v[u] = pp[(c0 + u < nsub ? c0 + u : nsub - 1) * 64 + tid];
 #pragma unroll
                             for (int u = 0; u < 8; ++u)
-                                if (c0 + u < nch) s = c0 + u == 0 ? v[u] : s + v[u];
+                                if (c0 + u < nsub) s = c0 + u == 0 ? v[u] : s + v[u];
                         }
                         sh.ored[0][tid] = s;
                     }
@@ -1107,7 +1121,7 @@ int persist_grid(int device, int n, int B, int T, int V, int *nres) {
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G) {
     if (G < 1 || G > PX_GMAX || a.B < 1 || a.B > PMAXB || a.T > 2048 || a.nch < 1 || a.nch > 64 ||
         a.cl > 128 * NKP || (int64_t)a.nch * a.cl < a.T || (int64_t)a.B * (a.n / 64) * a.nch > PX_TASKS ||
-        a.tctx > 512)
+        a.tctx > 512 || a.cl % 128)
         return hipErrorInvalidValue;
     switch (a.n) {
         case 128: return launch_ns<128>(s, a, G);
