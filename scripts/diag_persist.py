@@ -34,8 +34,11 @@ def toks(path, env, seeds, n=60):
 
 mode = sys.argv[1] if len(sys.argv) > 1 else "all"
 if mode in ("all", "trace"):
-    path = synth.model_path("base")
-    toks(path, {"WMI_PTRACE": "1"}, [40], 130)
+    # trace [model] [rows]: phase clocks of a greedy run (rows clips at once)
+    model = sys.argv[2] if len(sys.argv) > 2 else "base"
+    rows = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    path = synth.model_path(model)
+    toks(path, {"WMI_PTRACE": "1"}, list(range(40, 40 + rows)), 130 if model != "large-v3" else 40)
 if mode in ("all", "rows"):
     path = synth.model_path("base")
     P, C = {"WMI_PERSIST": "1"}, {"WMI_PERSIST": "0", "WMI_NO_FUSE": "1"}

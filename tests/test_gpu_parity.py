@@ -484,14 +484,14 @@ def test_beam_rows_cross_attention(wmi, micro_model, oracle_micro, K):
     tokens and scores bit-identical to one workgroup per row
     (WMI_XATTN_ROWS=0).  The fused output projection's residual update runs
     inside the row loop at these sizes."""
-    rows = _ctx_with_env(wmi, micro_model, {"WMI_NO_COOP": "1", "WMI_XATTN_ROWS": "2"})
+    rows = _ctx_with_env(wmi, micro_model, {"WMI_PERSIST": "0", "WMI_NO_COOP": "1", "WMI_XATTN_ROWS": "2"})
     try:
         ref, score, got, got_score = _beam_case(rows, oracle_micro, range(100, 130), K, 20, True)
         np.testing.assert_array_equal(got, ref)
         assert abs(got_score - score) < 1e-2
     finally:
         rows.close()
-    per = _ctx_with_env(wmi, micro_model, {"WMI_NO_COOP": "1", "WMI_XATTN_ROWS": "0"})
+    per = _ctx_with_env(wmi, micro_model, {"WMI_PERSIST": "0", "WMI_NO_COOP": "1", "WMI_XATTN_ROWS": "0"})
     try:
         ref2, score2, got2, got_score2 = _beam_case(per, oracle_micro, range(100, 130), K, 20, True)
         np.testing.assert_array_equal(got2, got)
@@ -507,7 +507,7 @@ def test_beam_rows_tiny_en_beam5_identical(wmi, model_cache):
     pcm = synth.synth_pcm_f32(30.0, 1234)
     out = []
     for rows in ("2", "0", "1"):
-        ctx = _ctx_with_env(wmi, path, {"WMI_NO_COOP": "1", "WMI_XATTN_ROWS": rows})
+        ctx = _ctx_with_env(wmi, path, {"WMI_PERSIST": "0", "WMI_NO_COOP": "1", "WMI_XATTN_ROWS": rows})
         try:
             ctx.set_audio_ctx(1500)
             ctx.pcm_to_mel_batch([pcm])
@@ -517,3 +517,24 @@ def test_beam_rows_tiny_en_beam5_identical(wmi, model_cache):
             ctx.close()
     np.testing.assert_array_equal(out[0][0], out[1][0])
     assert out[0][1] == out[1][1]
+
+
+def test_persistent_beam_matches_chain(wmi, model_cache):
+    """Beam search on the persistent decoder (one launch per step with the
+    beam slots as rows, the history table for self-attention keys, the beam
+    kernels between launches) against the kernel chain's beam search: the
+    same 5-beam hypothesis at C5's width over the full audio context."""
+    path = synth.model_path("tiny.en", model_cache)
+    pcm = synth.synth_pcm_f32(30.0, 1234)
+    out = []
+    for env in ({"WMI_PERSIST": "1"}, {"WMI_PERSIST": "0"}):
+        ctx = _ctx_with_env(wmi, path, env)
+        try:
+            ctx.set_audio_ctx(1500)
+            ctx.pcm_to_mel_batch([pcm])
+            ctx.encode(1, 0)
+            out.append(ctx.decode_beam(5, 24, suppress_eot=True)[0])
+        finally:
+            ctx.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert abs(out[0][1] - out[1][1]) < 1e-2, (out[0][1], out[1][1])  # the oracle tests' bound

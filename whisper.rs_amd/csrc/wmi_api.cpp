@@ -1151,6 +1151,17 @@ int trace_dump(wmi_context *ctx) {
 }
 
 // one decoder step for clips [b0, b0 + B) of the encoded batch
+// beam-step kernel arguments of the current beam search
+BeamArgs beam_args(wmi_context *ctx, int feed_len, int suppress_eot) {
+    const wmi_hparams &hp = ctx->hp;
+    BeamArgs ba{};
+    ba.logits = ctx->dlogits; ba.V = hp.n_vocab; ba.K = ctx->beam_k; ba.suppress_id = suppress_eot ? ctx->sp.eot : -1;
+    ba.eot = ctx->sp.eot; ba.feed_len = feed_len; ba.max_tokens = ctx->beam_max_tokens; ba.tctx = hp.n_text_ctx;
+    ba.st = ctx->dstate; ba.parts = ctx->dbparts; ba.bs = ctx->dbstate; ba.kv_src = ctx->dkvsrc;
+    ba.hist_parent = ctx->dhist_par; ba.hist_tok = ctx->dhist_tok;
+    return ba;
+}
+
 int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride, int suppress_eot, int out_stride) {
     const wmi_hparams &hp = ctx->hp;
     const int n = hp.n_text_state, H = hp.n_text_head, T = ctx->enc_T, Bt = ctx->enc_clips;
@@ -1279,11 +1290,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         HIPCHK(ctx, launch_ts_sample(s, ta));
     }
     if (beam) {
-        BeamArgs ba{};
-        ba.logits = ctx->dlogits; ba.V = hp.n_vocab; ba.K = ctx->beam_k; ba.suppress_id = suppress_eot ? ctx->sp.eot : -1;
-        ba.eot = ctx->sp.eot; ba.feed_len = feed_len; ba.max_tokens = ctx->beam_max_tokens; ba.tctx = hp.n_text_ctx;
-        ba.st = ctx->dstate; ba.parts = ctx->dbparts; ba.bs = ctx->dbstate; ba.kv_src = ctx->dkvsrc;
-        ba.hist_parent = ctx->dhist_par; ba.hist_tok = ctx->dhist_tok;
+        BeamArgs ba = beam_args(ctx, feed_len, suppress_eot);
         ba.trace = tslot(ctx, "beam", 0);
         HIPCHK(ctx, launch_beam_step(s, ba));
     }
@@ -1738,12 +1745,31 @@ int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_st
         HIPCHK(ctx, hipMemcpyAsync(ctx->dkvsrc, ctx->kvsrc_init.data(), ctx->kvsrc_init.size() * 4,
                                    hipMemcpyHostToDevice, ctx->stream));
         const int total_steps = np + n_gen - 1;
+        const int G = persist_grid_for(ctx, K);
+        if (G > 0) HIPCHK(ctx, hipMemsetAsync(ctx->d_xg, 0, ctx->xg_bytes, ctx->stream));
         int done_steps = 0;
         while (done_steps < total_steps) {
             int chunk = total_steps - done_steps;
             if (early_stop && chunk > 32) chunk = 32;
-            rc = run_dec_steps(ctx, clip, K, np, np, suppress_eot, 1, done_steps, chunk);
-            if (rc) return rc;
+            if (G > 0) {
+                // persistent decoder, one step per launch (K rows = the beam
+                // slots of this clip), then the beam kernels select
+                for (int i = 0; i < chunk; ++i) {
+                    PersistArgs pa = persist_args(ctx, clip, K, G, np, np, suppress_eot, 1);
+                    pa.n_steps = 1;
+                    pa.beam = 1;
+                    pa.cur_tok = ctx->dbstate->tok;
+                    pa.kv_src = ctx->dkvsrc;
+                    pa.kv_src_stride = hp.n_text_ctx;
+                    pa.logits_out = ctx->dlogits;
+                    pa.tokens_out = ctx->dtokens;  // (unused: no argmax in beam mode)
+                    HIPCHK(ctx, launch_dec_persist(ctx->stream, pa, G));
+                    HIPCHK(ctx, launch_beam_step(ctx->stream, beam_args(ctx, np, suppress_eot)));
+                }
+            } else {
+                rc = run_dec_steps(ctx, clip, K, np, np, suppress_eot, 1, done_steps, chunk);
+                if (rc) return rc;
+            }
             done_steps += chunk;
             if (early_stop && done_steps < total_steps) {
                 int32_t done = 0;

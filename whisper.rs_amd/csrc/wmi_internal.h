@@ -340,6 +340,13 @@ struct PersistArgs {
     unsigned long long *ptrace;  // WMI_PTRACE: [n_steps][L + 1][16][2] phase-end clocks, or null
     int nres;                    // vocabulary rows per workgroup resident in LDS
     float *logits_out;           // [B][V] logits of every step (debug / teacher forcing), or null
+    // beam search (one step per launch; the beam kernels select between launches):
+    // rows are the beam slots of clip b0, step 0 feeds cur_tok (the beam state's
+    // tokens), self-attention keys j < pos come from cache row kv_src[b][j], and
+    // the launch records no argmax
+    int beam;
+    const int32_t *kv_src;       // [B][kv_src_stride] or null
+    int kv_src_stride;
 };
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G);
 // the persistent decoder's exp vs the host ggml table, every non-positive f16 input

@@ -167,12 +167,18 @@ __device__ __forceinline__ void wset_load(WSet<KCH, NP> &S, const uint16_t *W, c
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         int row = rb + 16 * p + slot;
-        row = row < r1 ? row : r1 - 1;  // clamped: every load unconditional
-        row = row > 0 ? row : 0;
+        const bool ok = row < r1;  // slots past the rows load nothing (zeros)
+        row = ok ? row : 0;
         const f16 *wr = (const f16 *)W + (int64_t)row * K + l16 * 8;
+        const half8 z8 = {};
 #pragma unroll
-        for (int c = 0; c < KCH; ++c) S.w[p][c] = *glb((const half8 *)(wr + c * 128));
-        S.bias[p] = bias ? *glb(bias + row) : 0.0f;
+        for (int c = 0; c < KCH; ++c) S.w[p][c] = z8;
+        S.bias[p] = 0.0f;
+        if (ok) {  // exec-masked loads straight into the zeroed registers
+#pragma unroll
+            for (int c = 0; c < KCH; ++c) S.w[p][c] = *glb((const half8 *)(wr + c * 128));
+            if (bias) S.bias[p] = *glb(bias + row);
+        }
     }
 }
 
@@ -330,7 +336,10 @@ __device__ __forceinline__ float exp_f16_fast(float arg, const uint16_t *tab, in
 // whole load latency lands behind the seam.  Nothing waits here.
 #define PREFETCH_ISSUED asm volatile("" : : : "memory");
 
-template <int NS, int BT>  // BT: rows at compile time (1) or at most (8, runtime B)
+// BT: rows at compile time (1) or at most (8, runtime B); BEAM: beam-search
+// launches (self-attention history through kv_src; its index registers stay
+// out of the greedy instances)
+template <int NS, int BT, bool BEAM>
 __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     constexpr int KC = NS / 128;        // 128-element chunks of a K = n row
     constexpr int H = NS / 64;
@@ -342,6 +351,11 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int L = a.L, T = a.T, tctx = a.tctx, nch = a.nch, CL = a.cl;
     const int nsub = (T + 127) >> 7;  // 128-key P.V partials per (row, head)
+    // granules in flight per thread for the all-to-all polls (8-byte sc1
+    // loads; one round of loads per L2/MALL round trip): the whole vector
+    // in one round where registers allow
+    constexpr int PUX = BT == 1 ? (NS <= 1024 ? 4 : 8) : 16;   // B x n f32
+    constexpr int PUH = BT == 1 ? (NS <= 512 ? 4 : NS <= 1024 ? 8 : 16) : 16;  // B x 2n f16 pairs
     float *xf = (float *)smem;                                          // [B][NS] f32
     f16 *xs = (f16 *)(smem + (size_t)B * NS * 4);                       // [B][4 NS] f16
     unsigned char *scr = smem + (size_t)B * NS * 4 + (size_t)B * NS * 8;  // SCR_BYTES
@@ -390,7 +404,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     // logits at position pp: sh.tok[b]
     auto argmax_gather = [&](int pp) -> bool {
         uint32_t *ga = (uint32_t *)scr;  // [B][G][2]
-        const bool ok = gpoll(B * G * 2, atag(pp, L), ptr_u64(xg + oA), ga, abortw, a.err);
+        const bool ok = gpoll<BT == 1 ? 4 : 16>(B * G * 2, atag(pp, L), ptr_u64(xg + oA), ga, abortw, a.err);
         if (check(ok)) return false;
         for (int b = 0; b < B; ++b) {
             unsigned long long k = 0ull;
@@ -448,7 +462,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                                                    (float)tv[2] + pv.z, (float)tv[3] + pv.w);
                     }
                 } else {
-                    const bool ok = gpoll(B * NS, ptag(pos, L, l - 1, 9), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
+                    const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l - 1, 9), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 16)
                 }
@@ -495,10 +509,30 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     // conditionally-defined array becomes an undef value carried
                     // around the step loop and stays live across every phase)
                     const half8 z8 = {};
+                    // cache row of key j: the row's own, or (beam search) the
+                    // slot holding the hypothesis' history of position j
+                    int srk[2], srv[16];
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) srk[r] = b;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) srv[i] = b;
+                    if (BEAM && a.kv_src) {  // every table load first, then every cache load
+                        const int32_t *src = a.kv_src + (int64_t)b * a.kv_src_stride;
+#pragma unroll
+                        for (int r = 0; r < 2; ++r) {
+                            const int j = tid + 256 * r;
+                            srk[r] = src[j < pos ? j : 0];
+                        }
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const int j = jg + 32 * i;
+                            srv[i] = src[j < pos ? j : 0];
+                        }
+                    }
 #pragma unroll
                     for (int r = 0; r < 2; ++r) {
                         const int j = tid + 256 * r;
-                        const uint32_t off = (uint32_t)((((int64_t)b * tctx + j) * NS + h * 64) * 2);
+                        const uint32_t off = (uint32_t)((((int64_t)srk[r] * tctx + j) * NS + h * 64) * 2);
 #pragma unroll
                         for (int i = 0; i < 8; ++i) kv[r][i] = j < pos ? bload_sc1(rk, off + 16 * i) : z8;
                     }
@@ -507,7 +541,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
                         const int j = jg + 32 * i;
-                        vv[i] = j < pos ? bload_sc1(rv, (uint32_t)((((int64_t)b * tctx + j) * NS + h * 64 + doct * 8) * 2)) : z8;
+                        vv[i] = j < pos ? bload_sc1(rv, (uint32_t)((((int64_t)srv[i] * tctx + j) * NS + h * 64 + doct * 8) * 2)) : z8;
                     }
                     PREFETCH_ISSUED
                     __syncthreads();
@@ -612,7 +646,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 wset_load(S, P.wo, P.bo, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll(B * NS / 2, ptag(pos, L, l, 1), ptr_u64(xg + oO), (uint32_t *)xs, abortw, a.err);
+                const bool ok = gpoll<PUX>(B * NS / 2, ptag(pos, L, l, 1), ptr_u64(xg + oO), (uint32_t *)xs, abortw, a.err);
                 if (check(ok)) return;
                 PSTAMP(l * 32 + 18)
                 if (act)
@@ -637,7 +671,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll(B * NS, ptag(pos, L, l, 2), ptr_u64(xg + oX2), (uint32_t *)xf, abortw, a.err);
+                const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l, 2), ptr_u64(xg + oX2), (uint32_t *)xf, abortw, a.err);
                 if (check(ok)) return;
                 PSTAMP(l * 32 + 19)
                 ln_rows<NS>(xf, lp, xs, B, w, lane);
@@ -660,7 +694,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 for (int t = wg; t < ntask; t += G) {
                     const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
-                    const f16 *Kb = (const f16 *)a.ck + ((int64_t)l * a.Bt + a.b0 + b) * T * NS + h * 64 + (tid & 1) * 32;
+                    const f16 *Kb = (const f16 *)a.ck + ((int64_t)l * a.Bt + a.b0 + (a.beam ? 0 : b)) * T * NS + h * 64 + (tid & 1) * 32;
                     half8 kf[NKP][4];
                     const half8 z8 = {};
 #pragma unroll
@@ -680,7 +714,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
                         PREFETCH_ISSUED
                         __syncthreads();
-                        const bool ok = gpoll(NS, ptag(pos, L, l, 2), ptr_u64(xg + oX2 + b * NS), (uint32_t *)xf, abortw, a.err);
+                        const bool ok = gpoll<PUX>(NS, ptag(pos, L, l, 2), ptr_u64(xg + oX2 + b * NS), (uint32_t *)xf, abortw, a.err);
                         if (check(ok)) return;
                 PSTAMP(l * 32 + 20)
                         ln_rows<NS>(xf, lp, xs, 1, w, lane);
@@ -736,7 +770,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
                     const int doct = tid & 7, jg = tid >> 3;
-                    const f16 *Vb = (const f16 *)a.cv + ((int64_t)l * a.Bt + a.b0 + b) * T * NS + h * 64 + doct * 8;
+                    const f16 *Vb = (const f16 *)a.cv + ((int64_t)l * a.Bt + a.b0 + (a.beam ? 0 : b)) * T * NS + h * 64 + doct * 8;
                     half8 vf[NKP][4];
                     const half8 z8 = {};
 #pragma unroll
@@ -873,7 +907,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 wset_load(S, P.wco, P.bco, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll(B * NS / 2, ptag(pos, L, l, 6), ptr_u64(xg + oOC), (uint32_t *)xs, abortw, a.err);
+                const bool ok = gpoll<PUX>(B * NS / 2, ptag(pos, L, l, 6), ptr_u64(xg + oOC), (uint32_t *)xs, abortw, a.err);
                 if (check(ok)) return;
             PSTAMP(l * 32 + 23)
                 if (act)
@@ -897,7 +931,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 ln_params<NS>(P.ln2_w, P.ln2_b, lp, lane);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll(B * NS, ptag(pos, L, l, 7), ptr_u64(xg + oX3), (uint32_t *)xf, abortw, a.err);
+                const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l, 7), ptr_u64(xg + oX3), (uint32_t *)xf, abortw, a.err);
                 if (check(ok)) return;
                 PSTAMP(l * 32 + 24)
                 ln_rows<NS>(xf, lp, xs, B, w, lane);
@@ -923,7 +957,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 wset_load(S, P.w1, P.b1, 4 * NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll(B * 2 * NS, ptag(pos, L, l, 8), ptr_u64(xg + oH), (uint32_t *)xs, abortw, a.err);
+                const bool ok = gpoll<PUH>(B * 2 * NS, ptag(pos, L, l, 8), ptr_u64(xg + oH), (uint32_t *)xs, abortw, a.err);
                 if (check(ok)) return;
                 PSTAMP(l * 32 + 25)
                 if (act)
@@ -950,7 +984,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             ln_params<NS>(a.dln_w, a.dln_b, lp, lane);
             PREFETCH_ISSUED
             __syncthreads();
-            const bool ok = gpoll(B * NS, ptag(pos, L, L - 1, 9), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
+            const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, L - 1, 9), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
             if (check(ok)) return;
                 PSTAMP(L * 32 + 16)
             ln_rows<NS>(xf, lp, xs, B, w, lane);
@@ -1028,6 +1062,10 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     }
     // the last step's token: recorded by workgroup 0 and carried to the next launch
     if (wg != 0 || a.n_steps < 1) return;
+    if (a.beam) {  // the beam kernels select the next tokens
+        if (tid == 0) a.st->pos = pos;
+        return;
+    }
     __syncthreads();
     if (!argmax_gather(pos - 1)) return;
     if (tid < B) {
@@ -1043,24 +1081,25 @@ size_t persist_lds(int B) {
 }
 constexpr size_t LDS_CU = 160 * 1024;
 
-template <int NS, int BT>
+template <int NS, int BT, bool BEAM>
 hipError_t launch_nsb(hipStream_t s, const PersistArgs &a, int G) {
     const size_t lds = persist_lds<NS>(a.B) + (size_t)a.nres * NS * 2;
-    hipError_t e = hipFuncSetAttribute((const void *)k_dec_persist<NS, BT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
+    hipError_t e = hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_dec_persist<NS, BT>), dim3(G), dim3(PT), lds, s, a);
+    hipLaunchKernelGGL((k_dec_persist<NS, BT, BEAM>), dim3(G), dim3(PT), lds, s, a);
     return hipGetLastError();
 }
 template <int NS>
 hipError_t launch_ns(hipStream_t s, const PersistArgs &a, int G) {
-    return a.B == 1 ? launch_nsb<NS, 1>(s, a, G) : launch_nsb<NS, PMAXB>(s, a, G);
+    if (a.beam) return launch_nsb<NS, PMAXB, true>(s, a, G);
+    return a.B == 1 ? launch_nsb<NS, 1, false>(s, a, G) : launch_nsb<NS, PMAXB, false>(s, a, G);
 }
 
-template <int NS, int BT>
+template <int NS, int BT, bool BEAM>
 int grid_nsb(int device, int B, int V, int *nres) {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void *)k_dec_persist<NS, BT>) != hipSuccess) return 0;
+    if (hipFuncGetAttributes(&fa, (const void *)k_dec_persist<NS, BT, BEAM>) != hipSuccess) return 0;
     const size_t base = persist_lds<NS>(B), avail = LDS_CU - fa.sharedSizeBytes - 1024;
     if (base > avail) return 0;
     // resident vocabulary rows: as many of a workgroup's rows as the LDS holds
@@ -1068,11 +1107,12 @@ int grid_nsb(int device, int B, int V, int *nres) {
     int nr = (int)((avail - base) / (NS * 2));
     *nres = nr < rpw ? nr : rpw;
     const size_t lds = base + (size_t)*nres * NS * 2;
-    if (hipFuncSetAttribute((const void *)k_dec_persist<NS, BT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-        hipSuccess)
+    if (hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
         return 0;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dec_persist<NS, BT>, PT, lds) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dec_persist<NS, BT, BEAM>, PT, lds) != hipSuccess ||
+        per_cu < 1)
         return 0;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
@@ -1094,7 +1134,13 @@ __global__ void k_persist_selftest(const uint16_t *tab, int n_exp, uint32_t *mis
 
 template <int NS>
 int grid_ns(int device, int B, int V, int *nres) {
-    return B == 1 ? grid_nsb<NS, 1>(device, B, V, nres) : grid_nsb<NS, PMAXB>(device, B, V, nres);
+    if (B == 1) return grid_nsb<NS, 1, false>(device, B, V, nres);
+    // several rows: the beam instance must fit wherever the greedy one does
+    int nb = 0;
+    const int g = grid_nsb<NS, PMAXB, false>(device, B, V, nres);
+    const int gb = grid_nsb<NS, PMAXB, true>(device, B, V, &nb);
+    if (nb < *nres) *nres = nb;
+    return g < gb ? g : gb;
 }
 
 }  // namespace
@@ -1121,7 +1167,7 @@ int persist_grid(int device, int n, int B, int T, int V, int *nres) {
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G) {
     if (G < 1 || G > PX_GMAX || a.B < 1 || a.B > PMAXB || a.T > 2048 || a.nch < 1 || a.nch > 64 ||
         a.cl > 128 * NKP || (int64_t)a.nch * a.cl < a.T || (int64_t)a.B * (a.n / 64) * a.nch > PX_TASKS ||
-        a.tctx > 512 || a.cl % 128)
+        a.tctx > 512 || a.cl % 128 || (a.beam && a.n_steps != 1) || (a.kv_src && a.kv_src_stride < a.tctx))
         return hipErrorInvalidValue;
     switch (a.n) {
         case 128: return launch_ns<128>(s, a, G);
