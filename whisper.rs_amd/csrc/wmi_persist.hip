@@ -106,6 +106,7 @@ struct PShared {
     double redd[4];
     unsigned long long best[4][PMAXB];
     float ored[4][64 * 4];  // per wave: up to NKP 64-float partials
+    float kpart[16 * PMAXB];  // split-K GEMV: per (row, k-slice) partials of every decoder row
     int abort_;
 };
 
@@ -234,6 +235,105 @@ __device__ __forceinline__ void wset_dot(const WSet<KCH, NP> &S, const f16 *xs, 
     }
 }
 
+// ---- split-K GEMV for phases whose workgroup owns few rows: KS quarter-
+// waves per row, quarter ks summing chunks [ks * CQ, ks * CQ + CQ) of the
+// row (lane l16 holds c * 128 + l16 * 8 of each, as wset_*), the KS partials
+// added in ks order through LDS.  KS depends on n only (rows per workgroup
+// at the full grid), so a row's sum never depends on the row count B.
+template <int KCH, int KS>
+struct WSplit {
+    static constexpr int CQ = (KCH + KS - 1) / KS;
+    half8 w[CQ];
+};
+// rows per workgroup of an N-row GEMV at the full grid (PX_GMAX), even
+__host__ __device__ constexpr int rows_full(int N) { return (((N + PX_GMAX - 1) / PX_GMAX) + 1) & ~1; }
+// the largest divisor of kch with rows * ks <= 16 (one pass of 16 quarters)
+__host__ __device__ constexpr int split_of(int kch, int rows) {
+    int best = 1;
+    for (int k = 1; k <= kch; ++k)
+        if (kch % k == 0 && rows * k <= 16) best = k;
+    return best;
+}
+
+template <int KCH, int KS>
+__device__ __forceinline__ void wsplit_load(WSplit<KCH, KS> &S, const uint16_t *W, int K, int rb, int r1, int slot,
+                                            int l16) {
+    constexpr int CQ = WSplit<KCH, KS>::CQ;
+    const int rl = slot / KS, ks = slot - rl * KS, row = rb + rl;
+    const bool ok = rl < 16 / KS && row < r1;
+    const f16 *wr = (const f16 *)W + (int64_t)(ok ? row : 0) * K + ks * CQ * 128 + l16 * 8;
+    const half8 z8 = {};
+#pragma unroll
+    for (int c = 0; c < CQ; ++c) S.w[c] = z8;
+    if (ok) {
+#pragma unroll
+        for (int c = 0; c < CQ; ++c) S.w[c] = *glb((const half8 *)(wr + c * 128));
+    }
+}
+
+// epi(row, b, v, bias, valid) as wset_dot's: called by every lane of the
+// first 16 / KS quarters, quarter q carrying row rb + q (lane l16: decoder row l16)
+template <int BT, int KCH, int KS, typename Epi>
+__device__ __forceinline__ void wsplit_dot(const WSplit<KCH, KS> &S, const f16 *xs, int K, int B, int rb, int r1,
+                                           int slot, int l16, float bias, float *kpart, Epi &&epi) {
+    constexpr int CQ = WSplit<KCH, KS>::CQ;
+    const int rl = slot / KS, ks = slot - rl * KS;
+    float acc[BT];
+#pragma unroll
+    for (int b = 0; b < BT; ++b) acc[b] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < CQ; ++c)
+#pragma unroll
+        for (int b = 0; b < BT; ++b)
+            if (b < B) acc[b] = dot8(S.w[c], *(const half8 *)(xs + b * K + (ks * CQ + c) * 128 + l16 * 8), acc[b]);
+    float v = 0.0f;
+#pragma unroll
+    for (int b = 0; b < BT; ++b)
+        if (b < B) {
+            const float t = red16_sum(acc[b]);
+            if (l16 == b) v = t;
+        }
+    if (l16 < PMAXB && rl < 16 / KS) kpart[(rl * KS + ks) * PMAXB + l16] = v;
+    __syncthreads();
+    const int row = rb + slot;
+    float sum = 0.0f;
+    if (slot < 16 / KS && l16 < PMAXB) {
+        sum = kpart[(slot * KS) * PMAXB + l16];
+#pragma unroll
+        for (int k = 1; k < KS; ++k) sum = sum + kpart[(slot * KS + k) * PMAXB + l16];
+    }
+    epi(row, l16, sum, bias, slot < 16 / KS && row < r1 && l16 < B);
+}
+
+// a phase's weight set: split-K (KS > 1) or one quarter-wave per row
+template <int KCH, int NP, int KS>
+struct GSet {
+    WSplit<KCH, KS> s;
+    float bias;
+    __device__ __forceinline__ void load(const uint16_t *W, const float *b, int K, int rb, int r1, int slot, int l16) {
+        wsplit_load(s, W, K, rb, r1, slot, l16);
+        bias = 0.0f;
+        if (b && slot < 16 / KS && rb + slot < r1) bias = *glb(b + rb + slot);
+    }
+    template <int BT, typename Epi>
+    __device__ __forceinline__ void dot(const f16 *xs, int K, int B, int rb, int r1, int slot, int l16, float *kpart,
+                                        Epi &&epi) const {
+        wsplit_dot<BT>(s, xs, K, B, rb, r1, slot, l16, bias, kpart, epi);
+    }
+};
+template <int KCH, int NP>
+struct GSet<KCH, NP, 1> {
+    WSet<KCH, NP> s;
+    __device__ __forceinline__ void load(const uint16_t *W, const float *b, int K, int rb, int r1, int slot, int l16) {
+        wset_load(s, W, b, K, rb, r1, slot, l16);
+    }
+    template <int BT, typename Epi>
+    __device__ __forceinline__ void dot(const f16 *xs, int K, int B, int rb, int r1, int slot, int l16, float *,
+                                        Epi &&epi) const {
+        wset_dot<BT>(s, xs, K, B, rb, r1, slot, l16, epi);
+    }
+};
+
 // LayerNorm (ggml norm: double mean / variance, eps 1e-5; then * w + b) of
 // rows b < B of xf [B][NS] into xs [B][NS] f16 — wave w takes rows w, w + 4
 template <int NS>
@@ -345,6 +445,10 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     constexpr int H = NS / 64;
     constexpr int NPL = KC <= 4 ? 2 : 1;  // logits passes per register set
     constexpr bool XQF = KC <= 6;         // cross q computed inside the score tasks (registers allow)
+    // split-K factors of the GEMV phases (quarter-waves per row), from the
+    // rows a workgroup owns at the full grid
+    constexpr int KS_N = split_of(KC, rows_full(NS)), KS_I = split_of(4 * KC, rows_full(NS));
+    constexpr int KS_A = split_of(KC, rows_full(3 * NS)), KS_H = split_of(KC, rows_full(4 * NS));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ PShared sh;
     const int B = BT == 1 ? 1 : a.B, G = gridDim.x, wg = blockIdx.x;
@@ -433,9 +537,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 0);
-                WSet<KC, 2> S;
+                GSet<KC, 2, KS_A> S;
                 const bool act = ra0 < ra1;
-                wset_load(S, P.wqkv, P.bqkv, NS, ra0, ra1, slot, l16);
+                S.load(P.wqkv, P.bqkv, NS, ra0, ra1, slot, l16);
                 LnP<NS> lp;
                 ln_params<NS>(P.ln1_w, P.ln1_b, lp, lane);
                 PREFETCH_ISSUED
@@ -475,7 +579,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 __syncthreads();
                 PSTAMP(l * 32 + 26)
                 if (act)
-                    wset_dot<BT>(S, xs, NS, B, ra0, ra1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                    S.template dot<BT>(xs, NS, B, ra0, ra1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
                         const float vn = from_next_row(v), ebn = from_next_row(eb);
                         if (!valid || (q & 1)) return;
                         const int which = row / NS, c = row - which * NS;
@@ -641,16 +745,16 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 2);
-                WSet<KC, 1> S;
+                GSet<KC, 1, KS_N> S;
                 const bool act = rn0 < rn1;
-                wset_load(S, P.wo, P.bo, NS, rn0, rn1, slot, l16);
+                S.load(P.wo, P.bo, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
                 const bool ok = gpoll<PUX>(B * NS / 2, ptag(pos, L, l, 1), ptr_u64(xg + oO), (uint32_t *)xs, abortw, a.err);
                 if (check(ok)) return;
                 PSTAMP(l * 32 + 18)
                 if (act)
-                    wset_dot<BT>(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                    S.template dot<BT>(xs, NS, B, rn0, rn1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
                         if (!valid) return;
                         const float x = (v + eb) + sh.xres[b][row - rn0];
                         sh.xres[b][row - rn0] = x;
@@ -664,9 +768,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             if constexpr (!XQF) {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 3);
-                WSet<KC, 1> S;
+                GSet<KC, 1, KS_N> S;
                 const bool act = rn0 < rn1;
-                wset_load(S, P.wcq, P.bcq, NS, rn0, rn1, slot, l16);
+                S.load(P.wcq, P.bcq, NS, rn0, rn1, slot, l16);
                 LnP<NS> lp;
                 ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
                 PREFETCH_ISSUED
@@ -677,7 +781,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 ln_rows<NS>(xf, lp, xs, B, w, lane);
                 __syncthreads();
                 if (act)
-                    wset_dot<BT>(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                    S.template dot<BT>(xs, NS, B, rn0, rn1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
                         const float vn = from_next_row(v), ebn = from_next_row(eb);
                         if (!valid || (q & 1)) return;
                         gput(xg + oXQ + b * (NS / 2) + row / 2, tag, pack2((v + eb) * qs, (vn + ebn) * qs));
@@ -902,16 +1006,16 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 7);
-                WSet<KC, 1> S;
+                GSet<KC, 1, KS_N> S;
                 const bool act = rn0 < rn1;
-                wset_load(S, P.wco, P.bco, NS, rn0, rn1, slot, l16);
+                S.load(P.wco, P.bco, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
                 const bool ok = gpoll<PUX>(B * NS / 2, ptag(pos, L, l, 6), ptr_u64(xg + oOC), (uint32_t *)xs, abortw, a.err);
                 if (check(ok)) return;
             PSTAMP(l * 32 + 23)
                 if (act)
-                    wset_dot<BT>(S, xs, NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                    S.template dot<BT>(xs, NS, B, rn0, rn1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
                         if (!valid) return;
                         const float x = (v + eb) + sh.xres[b][row - rn0];
                         sh.xres[b][row - rn0] = x;
@@ -924,9 +1028,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 8);
-                WSet<KC, 2> S;
+                GSet<KC, 2, KS_H> S;
                 const bool act = rh0 < rh1;
-                wset_load(S, P.w0, P.b0, NS, rh0, rh1, slot, l16);
+                S.load(P.w0, P.b0, NS, rh0, rh1, slot, l16);
                 LnP<NS> lp;
                 ln_params<NS>(P.ln2_w, P.ln2_b, lp, lane);
                 PREFETCH_ISSUED
@@ -938,7 +1042,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 __syncthreads();
                 PSTAMP(l * 32 + 28)
                 if (act)
-                    wset_dot<BT>(S, xs, NS, B, rh0, rh1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                    S.template dot<BT>(xs, NS, B, rh0, rh1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
                         const float vn = from_next_row(v), ebn = from_next_row(eb);
                         if (!valid || (q & 1)) return;
                         const uint16_t h0 = f2h_bits(v + eb), h1 = f2h_bits(vn + ebn);
@@ -952,16 +1056,16 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 9);
-                WSet<4 * KC, 1> S;
+                GSet<4 * KC, 1, KS_I> S;
                 const bool act = rn0 < rn1;
-                wset_load(S, P.w1, P.b1, 4 * NS, rn0, rn1, slot, l16);
+                S.load(P.w1, P.b1, 4 * NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
                 const bool ok = gpoll<PUH>(B * 2 * NS, ptag(pos, L, l, 8), ptr_u64(xg + oH), (uint32_t *)xs, abortw, a.err);
                 if (check(ok)) return;
                 PSTAMP(l * 32 + 25)
                 if (act)
-                    wset_dot<BT>(S, xs, 4 * NS, B, rn0, rn1, slot, l16, [&](int row, int b, float v, float eb, bool valid) {
+                    S.template dot<BT>(xs, 4 * NS, B, rn0, rn1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
                         if (!valid) return;
                         const float x = (v + eb) + sh.xres[b][row - rn0];
                         sh.xres[b][row - rn0] = x;
@@ -1117,8 +1221,11 @@ int grid_nsb(int device, int B, int V, int *nres) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
     const int G = prop.multiProcessorCount < PX_GMAX ? prop.multiProcessorCount : PX_GMAX;
-    // row-partition limits of the register sets (see wset_dot users)
+    // row-partition limits of the register sets (see wset_dot users); the
+    // split-K phases need the full grid's rows per workgroup
     if ((3 * NS + G - 1) / G > 31 || (4 * NS + G - 1) / G > 31 || (NS + G - 1) / G > RNMAX - 1) return 0;
+    auto rows_g = [G](int N) { return (((N + G - 1) / G) + 1) & ~1; };
+    if (rows_g(NS) > rows_full(NS) || rows_g(3 * NS) > rows_full(3 * NS) || rows_g(4 * NS) > rows_full(4 * NS)) return 0;
     return G;
 }
 
