@@ -219,6 +219,14 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
  * f16 inputs) where the computed value differs from the host-built table. */
 int wmi_selftest(wmi_context *ctx, int32_t *n_mismatch);
 
+/* The reference's stage checksums (its debug println!s, each a sequential
+ * f32 sum): out5 = {_hann (main.rs:1571-1572), the samples (:1682-1686), the
+ * filters (:1688-1690), clip 0's mel before clamp_and_normalize
+ * (:1645-1647), clip 0's encoder mel window (:1819-1832)}.  Computed (and
+ * printed in the reference's order) only when the context was created with
+ * WMI_CHECKSUMS=1; the model-only sums (_hann, filters) always. */
+int wmi_get_checksums(const wmi_context *ctx, float *out5);
+
 /* Debug: copy a device buffer of the last decode into out (min of its size
  * and bytes).  which: 0 / 1 = the kernel chain's residual-stream buffers
  * [8][n_text_state] f32, 2 = logits [8][n_vocab] f32 (the persistent

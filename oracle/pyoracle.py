@@ -40,6 +40,7 @@ def lib():
         L.or_tables.argtypes = [hp_, hp_]
         L.or_set_dot_mode.argtypes = [C.c_int]
         L.or_mel.argtypes = [vp, fp, sz, C.c_int, C.c_void_p, C.POINTER(i32)]
+        L.or_checksums.argtypes = [vp, fp, sz, C.c_int, C.c_int, C.c_int, C.c_void_p]
         L.or_encode.argtypes = [vp, fp, i32, C.c_int, C.c_int, C.c_int, fp, hp_, hp_, C.c_void_p]
         L.or_decode_logits.argtypes = [vp, hp_, hp_, C.c_int, ip, C.c_int, C.c_int, fp]
         L.or_decode_greedy.argtypes = [vp, hp_, hp_, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.POINTER(i32), fp]
@@ -121,6 +122,16 @@ class OracleModel:
         if rc:
             raise OracleError(rc, "mel")
         return out
+
+    def checksums(self, pcm: np.ndarray, mel_offset: int = 0, n_ctx: int = 0, n_threads: int = 4) -> dict:
+        """The reference's debug sums (main.rs:1571, 1686, 1690, 1647, 1832)."""
+        pcm = np.ascontiguousarray(pcm, np.float32)
+        out = np.zeros(5, np.float32)
+        rc = lib().or_checksums(self.h, pcm, pcm.size, mel_offset, n_ctx or self.hp["n_audio_ctx"], n_threads,
+                                out.ctypes.data)
+        if rc:
+            raise OracleError(rc, "checksums")
+        return dict(zip(("hann", "samples", "filters", "mel_raw", "mel_window"), out.tolist()))
 
     def encode(self, mel: np.ndarray, n_ctx: int = 0, mel_offset: int = 0, n_threads: int = 8, probe: bool = False):
         hp = self.hp

@@ -623,13 +623,12 @@ static void fft(const float *in, int n, float *out) {
     }
 }
 
-int or_mel(const or_model *m, const float *pcm, size_t n_samples, int n_threads, float *mel, int32_t *n_len_out) {
+/* log_mel_spectrogram's frames (main.rs:1575-1644): log10 mel before
+ * clamp_and_normalize, [n_mels][n_len] */
+static int mel_raw(const or_model *m, const float *pcm, size_t n_samples, int n_threads, float *mel, int64_t n_len) {
     pthread_once(&tw_once, init_tw);
     const int n_mel = m->hp[HP_N_MELS];
     const int n_ff = 1 + NFFT / 2; /* main.rs:1580, speed_up = false */
-    const int64_t n_len = (int64_t)(n_samples / HOP);
-    *n_len_out = (int32_t)n_len;
-    if (!mel) return WMI_OK;
     if (m->n_filt_mel < n_mel || m->n_filt_mel * m->n_filt_ff < n_mel * n_ff) return WMI_E_UNEXPECTED;
     float hann[NFFT];
     for (int i = 0; i < NFFT; ++i) hann[i] = 0.5f * (1.0f - cosf((2.0f * PI_F * (float)i) / (float)NFFT));
@@ -649,8 +648,11 @@ int or_mel(const or_model *m, const float *pcm, size_t n_samples, int n_threads,
             mel[(int64_t)j * n_len + i] = log10f(sum);
         }
     }
-    /* clamp_and_normalize (main.rs:1654-1671) */
-    const int64_t tot = (int64_t)n_mel * n_len;
+    return WMI_OK;
+}
+
+/* clamp_and_normalize (main.rs:1654-1671) */
+static void mel_norm(float *mel, int64_t tot) {
     double mmax = -1e20;
     for (int64_t i = 0; i < tot; ++i)
         if ((double)mel[i] > mmax) mmax = (double)mel[i];
@@ -659,6 +661,50 @@ int or_mel(const or_model *m, const float *pcm, size_t n_samples, int n_threads,
         if ((double)mel[i] < mmax) mel[i] = (float)mmax;
         mel[i] = (mel[i] + 4.0f) / 4.0f;
     }
+}
+
+int or_mel(const or_model *m, const float *pcm, size_t n_samples, int n_threads, float *mel, int32_t *n_len_out) {
+    const int64_t n_len = (int64_t)(n_samples / HOP);
+    *n_len_out = (int32_t)n_len;
+    if (!mel) return WMI_OK;
+    const int rc = mel_raw(m, pcm, n_samples, n_threads, mel, n_len);
+    if (rc) return rc;
+    mel_norm(mel, (int64_t)m->hp[HP_N_MELS] * n_len);
+    return WMI_OK;
+}
+
+/* The reference's debug prints, each a sequential f32 sum (Rust
+ * iter().sum() / a += loop): "_hann" main.rs:1571-1572, "y" of the samples
+ * :1682-1686, "filters" :1688-1690, "x1" of the mel before
+ * clamp_and_normalize :1645-1647, "y" of the encoder's mel window
+ * :1819-1832 (for mel_offset, n_ctx). */
+int or_checksums(const or_model *m, const float *pcm, size_t n_samples, int mel_offset, int n_ctx, int n_threads,
+                 float out[5]) {
+    const int n_mel = m->hp[HP_N_MELS];
+    const int64_t n_len = (int64_t)(n_samples / HOP);
+    float hs = 0.0f;
+    for (int i = 0; i < NFFT; ++i) hs += 0.5f * (1.0f - cosf((2.0f * PI_F * (float)i) / (float)NFFT));
+    float ps = 0.0f;
+    for (size_t i = 0; i < n_samples; ++i) ps += pcm[i];
+    float fs = 0.0f;
+    for (int64_t i = 0; i < (int64_t)m->n_filt_mel * m->n_filt_ff; ++i) fs += m->filters[i];
+    float *mel = (float *)malloc(sizeof(float) * (size_t)(n_mel * n_len + 1));
+    if (!mel) return WMI_E_UNEXPECTED;
+    int rc = mel_raw(m, pcm, n_samples, n_threads, mel, n_len);
+    if (rc) { free(mel); return rc; }
+    float xs = 0.0f;
+    for (int64_t i = 0; i < (int64_t)n_mel * n_len; ++i) xs += mel[i];
+    mel_norm(mel, (int64_t)n_mel * n_len);
+    const int64_t i0 = mel_offset < n_len ? mel_offset : n_len;
+    const int64_t i1 = mel_offset + 2 * (int64_t)n_ctx < n_len ? mel_offset + 2 * (int64_t)n_ctx : n_len;
+    float ys = 0.0f;
+    for (int j = 0; j < n_mel; ++j)
+        for (int64_t c = 0; c < 2 * (int64_t)n_ctx; ++c) {
+            const int64_t i = i0 + c;
+            ys += i < i1 ? mel[(int64_t)j * n_len + i] : 0.0f;
+        }
+    free(mel);
+    out[0] = hs; out[1] = ps; out[2] = fs; out[3] = xs; out[4] = ys;
     return WMI_OK;
 }
 

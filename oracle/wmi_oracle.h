@@ -52,6 +52,13 @@ void or_tables(uint16_t *gelu, uint16_t *expt);
 int or_mel(const or_model *m, const float *pcm, size_t n_samples, int n_threads,
            float *mel, int32_t *n_len);
 
+/* The reference's stage checksums (debug prints): {_hann, samples, filters,
+ * mel before clamp_and_normalize, the encoder's mel window}, each the
+ * sequential f32 sum the reference prints (main.rs:1571, 1686, 1690, 1647,
+ * 1832). */
+int or_checksums(const or_model *m, const float *pcm, size_t n_samples, int mel_offset, int n_ctx, int n_threads,
+                 float out[5]);
+
 /* whisper_encode (main.rs:1799-2063).  enc_out [n_ctx][n_state] f32;
  * cross_k / cross_v [n_text_layer][n_ctx][n_text_state] f16 bits.
  * probe (optional) receives the residual stream after the conv stem + PE and

@@ -538,3 +538,25 @@ def test_persistent_beam_matches_chain(wmi, model_cache):
             ctx.close()
     np.testing.assert_array_equal(out[0][0], out[1][0])
     assert abs(out[0][1] - out[1][1]) < 1e-2, (out[0][1], out[1][1])  # the oracle tests' bound
+
+
+def test_reference_checksums(wmi, micro_model, oracle_micro):
+    """The reference's stage sums from the HIP path (WMI_CHECKSUMS=1) against
+    the oracle's: model-only and host sums exactly, the two mel sums within
+    the mel's own tolerance (<= 2e-6 a value, summed sequentially)."""
+    ctx = _ctx_with_env(wmi, micro_model, {"WMI_CHECKSUMS": "1"})
+    try:
+        pcm = synth.synth_pcm_f32(3.0, 77)
+        ctx.set_audio_ctx(64)
+        ctx.pcm_to_mel_batch([pcm])
+        ctx.encode(1, 17)
+        got = ctx.checksums()
+        ref = oracle_micro.checksums(pcm, mel_offset=17, n_ctx=64)
+        print(f"[checksums] hip {got} oracle {ref}")
+        for k in ("hann", "samples", "filters"):
+            assert got[k] == ref[k], (k, got[k], ref[k])
+        n = 80 * 300
+        for k in ("mel_raw", "mel_window"):
+            assert abs(got[k] - ref[k]) <= 2e-6 * n + 1e-5 * abs(ref[k]), (k, got[k], ref[k])
+    finally:
+        ctx.close()

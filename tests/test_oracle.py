@@ -161,3 +161,25 @@ def test_hf_transformers_crosscheck(oracle_micro, micro_model):
         hf_lg = (dec[0] @ model.decoder.embed_tokens.weight.T).numpy()
     assert np.abs(hf_lg - lg).max() < 2e-2
     np.testing.assert_array_equal(hf_lg.argmax(1), lg.argmax(1))
+
+
+def test_reference_checksums(oracle_micro):
+    """The reference's stage sums (main.rs:1571, 1686, 1690, 1647, 1832):
+    sequential f32 sums, restated by or_checksums; the window sum equals the
+    one taken over or_mel's output the way main.rs:1819-1832 lays it out."""
+    import synth
+    pcm = synth.synth_pcm_f32(3.0, 77)
+    ck = oracle_micro.checksums(pcm, mel_offset=17, n_ctx=64)
+    seq = lambda a: float(np.cumsum(np.asarray(a, np.float32).ravel(), dtype=np.float32)[-1])
+    i = np.arange(400, dtype=np.float32)
+    hann = (np.float32(0.5) * (np.float32(1.0) - np.cos((np.float32(2.0) * np.float32(np.pi) * i) / np.float32(400.0),
+                                                         dtype=np.float32))).astype(np.float32)
+    assert abs(ck["hann"] - seq(hann)) <= 1e-3  # host cosf vs numpy cos may differ in the last bit
+    assert ck["samples"] == seq(pcm)
+    mel = oracle_micro.mel(pcm)
+    n_mel, n_len = mel.shape
+    win = np.zeros((n_mel, 128), np.float32)
+    i0, i1 = min(17, n_len), min(17 + 128, n_len)
+    win[:, :i1 - i0] = mel[:, i0:i1]
+    assert ck["mel_window"] == seq(win)
+    assert np.isfinite(ck["mel_raw"]) and np.isfinite(ck["filters"])

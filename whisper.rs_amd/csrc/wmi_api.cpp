@@ -274,6 +274,8 @@ struct wmi_context {
     std::vector<std::string> phase_names = std::vector<std::string>(32);  // phase slots 32.. (layer 0 GEMVs, logits)
     // persistent decoder (wmi_persist.hip): greedy steps in one launch
     Tune tune;                        // WMI_* knobs of this context (wmi_internal.h)
+    bool checksums = false;           // WMI_CHECKSUMS=1: the reference's stage sums (debug prints)
+    float cks[5] = {0, 0, 0, 0, 0};   // _hann, samples, filters, mel before normalisation, mel window
     bool use_persist = true;          // WMI_PERSIST=0: kernel chain instead
     bool persist_logits = false;      // WMI_PERSIST_LOGITS=1: also store every step's logits (dlogits)
     int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
@@ -676,6 +678,11 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
     auto T = [&](const std::string &name) -> HostTensor & { return pm.tensors.at(name); };
     MelTables mt;
     build_mel_tables(mt);
+    // the reference's debug sums that depend only on the model (sequential f32)
+    ctx->cks[0] = 0.0f;
+    for (int i = 0; i < 400; ++i) ctx->cks[0] += mt.hann[i];  // main.rs:1571
+    ctx->cks[2] = 0.0f;
+    for (float f : pm.filters) ctx->cks[2] += f;  // main.rs:1689
     const size_t o_mt = add(&mt, sizeof(mt));
     std::vector<float> filt_t((size_t)201 * C, 0.0f);
     if ((int64_t)pm.n_filt_mel * pm.n_filt_ff < (int64_t)C * 201)
@@ -980,6 +987,11 @@ int stage_pcm(wmi_context *ctx, int n_clips, const float *const *pcm, const size
             HIPCHK(ctx, hipMalloc(&ctx->pcm_dev[c], ctx->pcm_cap[c] * 4));
         }
         if (ns) HIPCHK(ctx, hipMemcpyAsync(ctx->pcm_dev[c], pcm[c], ns * 4, hipMemcpyHostToDevice, ctx->stream));
+        if (ctx->checksums && c == 0) {  // main.rs:1682-1686, clip 0
+            float x = 0.0f;
+            for (size_t i = 0; i < ns; ++i) x += pcm[0][i];
+            ctx->cks[1] = x;
+        }
         ptrs[c] = ctx->pcm_dev[c];
         ctx->n_samp_host[c] = (int64_t)ns;
         ctx->n_len_host[c] = (int64_t)(ns / 160);  // main.rs:1575
@@ -1010,6 +1022,16 @@ int run_mel(wmi_context *ctx) {
     HIPCHK(ctx, launch_mel_frames(ctx->stream, ctx->meltabs, ctx->filt_t, ctx->hp.n_mels,
                                   (const float *const *)ctx->d_pcm_ptrs, ctx->d_nsamp, ctx->d_mel, ctx->mel_stride,
                                   ctx->d_nlen, ctx->max_len, ctx->d_melmax, B));
+    if (ctx->checksums) {  // clip 0's mel before clamp_and_normalize (main.rs:1645-1647)
+        std::vector<float> m((size_t)ctx->hp.n_mels * ctx->n_len_host[0]);
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (!m.empty()) HIPCHK(ctx, hipMemcpy(m.data(), ctx->d_mel, m.size() * 4, hipMemcpyDeviceToHost));
+        float x = 0.0f;
+        for (float v : m) x += v;
+        ctx->cks[3] = x;
+        printf("y:%.9g\nfilters:%.9g\n_hann:%.9g\nx1:%.9g\n", ctx->cks[1], ctx->cks[2], ctx->cks[0], x);
+        fflush(stdout);
+    }
     HIPCHK(ctx, launch_mel_norm(ctx->stream, ctx->d_mel, ctx->mel_stride, ctx->hp.n_mels, ctx->d_nlen, ctx->max_len,
                                 ctx->d_melmax, B));
     return WMI_OK;
@@ -1034,6 +1056,18 @@ int run_encode(wmi_context *ctx, int mel_offset) {
         HIPCHK(ctx, hipMemsetAsync(ctx->k, 0, qkv_bytes, s));
         HIPCHK(ctx, hipMemsetAsync(ctx->vt, 0, qkv_bytes, s));
         ctx->layout_T = T;
+    }
+    if (ctx->checksums) {  // clip 0's mel window (main.rs:1819-1832)
+        const int64_t nl = ctx->n_len_host[0], nm = hp.n_mels;
+        std::vector<float> m((size_t)nm * nl);
+        if (!m.empty()) HIPCHK(ctx, hipMemcpy(m.data(), ctx->d_mel, m.size() * 4, hipMemcpyDeviceToHost));
+        const int64_t i0 = mel_offset < nl ? mel_offset : nl, i1 = mel_offset + T2 < nl ? mel_offset + T2 : nl;
+        float y = 0.0f;
+        for (int64_t j = 0; j < nm; ++j)
+            for (int64_t c = 0; c < T2; ++c) y += i0 + c < i1 ? m[(size_t)(j * nl + i0 + c)] : 0.0f;
+        ctx->cks[4] = y;
+        printf("y:%.9g\n", y);
+        fflush(stdout);
     }
     // mel window -> conv1 input (main.rs:1816-1833)
     HIPCHK(ctx, launch_mel_window(s, ctx->d_mel, ctx->mel_stride, hp.n_mels, ctx->d_nlen, mel_offset, T2, ctx->Cp1,
@@ -1899,6 +1933,7 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
     if (getenv("WMI_NO_FUSE")) ctx->fuse_wo = false;
     if (const char *c = getenv("WMI_PERSIST")) ctx->use_persist = atoi(c) != 0;
     if (getenv("WMI_PERSIST_LOGITS")) ctx->persist_logits = true;
+    if (const char *c = getenv("WMI_CHECKSUMS")) ctx->checksums = atoi(c) != 0;
     ctx->dec_layers = ctx->hp.n_text_layer;
     if (const char *c = getenv("WMI_DEC_LAYERS")) ctx->dec_layers = std::max(1, std::min(atoi(c), ctx->hp.n_text_layer));
     if (getenv("WMI_PTRACE")) {
@@ -2309,6 +2344,12 @@ int wmi_get_mel(const wmi_context *ctx, int clip, float *out, size_t cap, int32_
     if (cap < need) return WMI_E_NO_SPACE;
     if (need && hipMemcpy(out, ctx->d_mel + (size_t)clip * ctx->mel_stride, need * 4, hipMemcpyDeviceToHost) != hipSuccess)
         return WMI_E_HIP;
+    return WMI_OK;
+}
+
+int wmi_get_checksums(const wmi_context *ctx, float *out5) {
+    if (!ctx || !out5) return WMI_E_INVALID_ARG;
+    for (int i = 0; i < 5; ++i) out5[i] = ctx->cks[i];
     return WMI_OK;
 }
 

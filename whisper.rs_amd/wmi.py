@@ -64,7 +64,7 @@ EXPORTS = (
     "wmi_decode_timestamps", "wmi_transcribe", "wmi_get_segment", "wmi_get_segment_tokens",
     "wmi_pcm_to_mel", "wmi_pcm_to_mel_batch", "wmi_encode", "wmi_decode_greedy", "wmi_decode_logits",
     "wmi_decode_beam", "wmi_full", "wmi_stage_pcm", "wmi_run_staged", "wmi_run_staged_beam", "wmi_get_tokens", "wmi_get_timings", "wmi_sync",
-    "wmi_get_mel", "wmi_get_encoder_out", "wmi_get_cross_kv", "wmi_bench_kernel", "wmi_selftest", "wmi_debug_read",
+    "wmi_get_mel", "wmi_get_checksums", "wmi_get_encoder_out", "wmi_get_cross_kv", "wmi_bench_kernel", "wmi_selftest", "wmi_debug_read",
     "wmi_dist_id_size", "wmi_dist_make_id", "wmi_dist_init", "wmi_dist_gather_tokens", "wmi_dist_barrier",
 )
 
@@ -150,6 +150,7 @@ def lib():
         L.wmi_bench_kernel.argtypes = [vp, C.c_int, C.c_int, C.POINTER(KernelBench)]
         L.wmi_selftest.argtypes = [vp, C.POINTER(i32)]
         L.wmi_debug_read.argtypes = [vp, C.c_int, vp, C.c_size_t]
+        L.wmi_get_checksums.argtypes = [vp, vp]
         L.wmi_dist_id_size.restype = sz
         L.wmi_dist_make_id.argtypes = [vp]
         L.wmi_dist_init.argtypes = [vp, C.c_int, C.c_int, vp]
@@ -366,6 +367,12 @@ class WhisperContext:
         n = C.c_int32()
         _raise(lib().wmi_selftest(self._h, C.byref(n)), self._h)
         return n.value
+
+    def checksums(self) -> dict:
+        """The reference's stage sums (wmi_get_checksums; WMI_CHECKSUMS=1 contexts)."""
+        out = np.zeros(5, np.float32)
+        _raise(lib().wmi_get_checksums(self._h, _ptr(out)), self._h)
+        return dict(zip(("hann", "samples", "filters", "mel_raw", "mel_window"), out.tolist()))
 
     def debug_read(self, which: int, nbytes: int) -> bytes:
         """Raw copy of a device buffer of the last decode (wmi_debug_read)."""
