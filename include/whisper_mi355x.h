@@ -204,8 +204,10 @@ int wmi_sync(wmi_context *ctx);
 
 /* Re-launch one kernel of the last pipeline call `iters` times between HIP
  * events on the context stream (bench.py's live roofline measurement).
- * which: 0 = decoder logits GEMV + argmax (HBM-bound), 1 = encoder MLP-up
- * GEMM of layer 0 (MFMA), 2 = encoder attention of layer 0, 3 = cross-K/V GEMM. */
+ * which: 14 = the persistent greedy decoder over the staged clips (one launch
+ * per 8-row block, as run_staged makes it; algorithmic bytes summed per step),
+ * 0 = the kernel chain's logits GEMV + argmax, 1 = encoder MLP-up GEMM of
+ * layer 0 (MFMA), 2 = encoder attention of layer 0, 3 = cross-K/V GEMM. */
 typedef struct wmi_kernel_bench {
     float avg_us;          /* mean launch duration */
     double alg_bytes;      /* algorithmic HBM bytes per launch */
@@ -232,7 +234,7 @@ int wmi_get_checksums(const wmi_context *ctx, float *out5);
  * [8][n_text_state] f32, 2 = logits [8][n_vocab] f32 (the persistent
  * decoder fills them only with WMI_PERSIST_LOGITS=1), 3 = the persistent
  * decoder's exchange block (8-byte {tag, value} granules), 4-9 = decoder
- * chain scratch, 10 = this context's tuning knobs (10 int32, host copy; the
+ * chain scratch, 10 = this context's tuning knobs (9 int32, host copy; the
  * WMI_* environment is read once per context at wmi_init_from_file). */
 int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes);
 

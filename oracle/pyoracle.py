@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+LIB_PATH = os.environ.get("WMI_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")  # (sanitizer builds)
 _lib = None
 
 

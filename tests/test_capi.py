@@ -144,3 +144,28 @@ def test_pcm_conversion_matches_reference():
     s16 = np.array([-32768, -1, 0, 1, 32767], np.int16)
     np.testing.assert_array_equal(wmi.convert_integer_to_float_audio(s16),
                                   np.array([-1.0, -1 / 32768, 0.0, 1 / 32768, 32767 / 32768], np.float32))
+
+
+def test_hostile_headers_allocate_nothing(tmp_path, micro_model):
+    """Header fields that would size huge host allocations are checked
+    against the file first: out-of-range hparams, a vocabulary
+    count or a WAV data chunk larger than the file — each a status code, not
+    a std::bad_alloc escaping the C ABI."""
+    data = open(micro_model, "rb").read()
+    d = str(tmp_path)
+    big = os.path.join(d, "hp.bin")  # n_vocab = 2^30
+    open(big, "wb").write(data[:4] + struct.pack("<i", 1 << 30) + data[8:])
+    with pytest.raises(wmi.Unexpected):
+        wmi.WhisperContext.new(big)
+    nfilt = struct.unpack("<ii", data[48:56])
+    voc_off = 56 + 4 * nfilt[0] * nfilt[1]
+    nv = os.path.join(d, "nv.bin")  # vocabulary of 2^31 - 1 entries in a small file
+    open(nv, "wb").write(data[:voc_off] + struct.pack("<i", 0x7FFFFFFF) + data[voc_off + 4:])
+    with pytest.raises(wmi.UnexpectIO):
+        wmi.WhisperContext.new(nv)
+    wav = os.path.join(d, "huge.wav")  # data chunk claims 4 GiB - 2
+    body = b"WAVE" + b"fmt " + struct.pack("<IHHIIHH", 16, 1, 1, 16000, 32000, 2, 16)
+    body += b"data" + struct.pack("<I", 0xFFFFFFFE) + b"\x00\x01" * 8
+    open(wav, "wb").write(b"RIFF" + struct.pack("<I", len(body)) + body)
+    with pytest.raises(wmi.UnexpectIO):
+        wmi.read_wav(wav)

@@ -69,10 +69,10 @@ def test_tuning_knobs_are_per_context(wmi, micro_model, monkeypatch):
     under one setting keeps it while another context, created on another
     thread under a different environment, gets its own."""
     import threading
-    monkeypatch.setenv("WMI_ATTN_V1", "1")
+    monkeypatch.setenv("WMI_LOGITS_CAP", "64")
     monkeypatch.setenv("WMI_COOP_MAX", "64")
     a = wmi.WhisperContext.new(micro_model, 0, max_clips=1)
-    monkeypatch.delenv("WMI_ATTN_V1")
+    monkeypatch.delenv("WMI_LOGITS_CAP")
     monkeypatch.delenv("WMI_COOP_MAX")
     box = {}
     t = threading.Thread(target=lambda: box.update(b=wmi.WhisperContext.new(micro_model, 0, max_clips=1)))
@@ -80,11 +80,11 @@ def test_tuning_knobs_are_per_context(wmi, micro_model, monkeypatch):
     t.join(120)
     b = box["b"]
     try:
-        ka = np.frombuffer(a.debug_read(10, 40), np.int32)
-        kb = np.frombuffer(b.debug_read(10, 40), np.int32)
-        assert ka[0] == 1 and ka[6] == 64   # attn_v1, coop_max of the first context
-        assert kb[0] == 0 and kb[6] == 512  # defaults in the second
-        # and each still runs its own encoder variant to the same numbers
+        ka = np.frombuffer(a.debug_read(10, 36), np.int32)
+        kb = np.frombuffer(b.debug_read(10, 36), np.int32)
+        assert ka[0] == 64 and ka[5] == 64    # logits_cap, coop_max of the first context
+        assert kb[0] == 512 and kb[5] == 512  # defaults in the second
+        # and both run to the same numbers
         pcm = synth.synth_pcm_f32(2.0, 5)
         outs = []
         for c in (a, b):

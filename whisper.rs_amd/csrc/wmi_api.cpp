@@ -410,13 +410,23 @@ int parse_file(const char *path, ParsedModel &pm, std::string &err) {
     const wmi_hparams &hp = pm.hp;
     for (int i = 0; i < 10; ++i)
         if (hpv[i] <= 0) { err = "Unexpected: non-positive hparam"; return WMI_E_UNEXPECTED; }
+    // bounds far above every Whisper model, so no element count derived from
+    // them can overflow and nothing is allocated from a corrupt header
+    if (hp.n_vocab > (1 << 20) || hp.n_audio_ctx > (1 << 16) || hp.n_text_ctx > (1 << 16) ||
+        hp.n_audio_state > (1 << 14) || hp.n_text_state > (1 << 14) || hp.n_audio_head > (1 << 10) ||
+        hp.n_text_head > (1 << 10) || hp.n_audio_layer > (1 << 10) || hp.n_text_layer > (1 << 10) ||
+        hp.n_mels > (1 << 12)) {
+        err = "Unexpected: hparam out of range";
+        return WMI_E_UNEXPECTED;
+    }
     if (hp.n_audio_state % hp.n_audio_head || hp.n_text_state % hp.n_text_head) {
         err = "Unexpected: state not divisible by heads";
         return WMI_E_UNEXPECTED;
     }
     // filters (main.rs:513-535)
     if (!rd(&pm.n_filt_mel, 4) || !rd(&pm.n_filt_ff, 4)) { err = "Unexpected IO: short read (filters)"; return WMI_E_IO; }
-    if (pm.n_filt_mel <= 0 || pm.n_filt_ff <= 0 || (int64_t)pm.n_filt_mel * pm.n_filt_ff > (1 << 24)) {
+    if (pm.n_filt_mel <= 0 || pm.n_filt_ff <= 0 || (int64_t)pm.n_filt_mel * pm.n_filt_ff > (1 << 24) ||
+        (int64_t)pm.n_filt_mel * pm.n_filt_ff * 4 > fsize - ftell(f)) {
         err = "Unexpected: bad filter dims";
         return WMI_E_UNEXPECTED;
     }
@@ -424,11 +434,11 @@ int parse_file(const char *path, ParsedModel &pm, std::string &err) {
     if (!rd(pm.filters.data(), pm.filters.size() * 4)) { err = "Unexpected IO: short read (filters)"; return WMI_E_IO; }
     // vocab (main.rs:430, 578-592)
     int32_t nv = 0;
-    if (!rd(&nv, 4) || nv < 0) { err = "Unexpected IO: vocab"; return WMI_E_IO; }
+    if (!rd(&nv, 4) || nv < 0 || (int64_t)nv * 4 > fsize - ftell(f)) { err = "Unexpected IO: vocab"; return WMI_E_IO; }
     pm.vocab.resize(nv);
     for (int32_t i = 0; i < nv; ++i) {
         uint32_t len = 0;
-        if (!rd(&len, 4) || len > (1u << 20)) { err = "Unexpected IO: vocab"; return WMI_E_IO; }
+        if (!rd(&len, 4) || len > (1u << 20) || (int64_t)len > fsize - ftell(f)) { err = "Unexpected IO: vocab"; return WMI_E_IO; }
         pm.vocab[i].resize(len);
         if (len && !rd(&pm.vocab[i][0], len)) { err = "Unexpected IO: vocab"; return WMI_E_IO; }
     }
@@ -484,7 +494,15 @@ int parse_file(const char *path, ParsedModel &pm, std::string &err) {
             snprintf(s, sizeof s, "%s.out.bias", a); E(s, 0, 1, nt, 1);
         }
     }
-    // every expected tensor exists, zero-filled, like the reference arena
+    // every expected tensor exists, zero-filled, like the reference arena —
+    // once the file is large enough to hold them (>= 1 byte per 4 elements:
+    // q4 blocks are the densest form), so a small corrupt file allocates nothing
+    int64_t exp_nel = 0;
+    for (auto &kv : exp) exp_nel += (int64_t)kv.second.ne[0] * kv.second.ne[1] * kv.second.ne[2];
+    if (exp_nel / 4 > (int64_t)fsize) {
+        err = "Unexpected IO: file too short for its hparams";
+        return WMI_E_IO;
+    }
     for (auto &kv : exp) {
         HostTensor t;
         t.dtype = kv.second.dtype;
@@ -1861,6 +1879,21 @@ int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_st
 
 }  // namespace
 
+// An exception (host allocation failure on a hostile file, an internal
+// std:: error) never crosses the C ABI: it becomes a status code.
+template <typename F>
+int guarded(wmi_context *ctx, F &&f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc &) {
+        return set_err(ctx, WMI_E_UNEXPECTED, "host memory exhausted");
+    } catch (const std::exception &e) {
+        return set_err(ctx, WMI_E_UNEXPECTED, "internal error: %s", e.what());
+    } catch (...) {
+        return set_err(ctx, WMI_E_UNEXPECTED, "internal error");
+    }
+}
+
 // ===========================================================================
 // C ABI
 // ===========================================================================
@@ -1890,7 +1923,7 @@ const char *wmi_strerror(int status) {
 const char *wmi_last_error(const wmi_context *ctx) { return ctx ? ctx->last_error.c_str() : g_last_error.c_str(); }
 const char *wmi_last_error_global(void) { return g_last_error.c_str(); }
 
-int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context **out) {
+static int wmi_init_from_file_impl(const char *path, int device, int max_clips, wmi_context **out) {
     if (!out || !path) return set_err(nullptr, WMI_E_INVALID_ARG, "null argument");
     *out = nullptr;
     if (max_clips < 1) return set_err(nullptr, WMI_E_INVALID_ARG, "max_clips must be >= 1");
@@ -1948,7 +1981,6 @@ int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context 
             if (x >= lo) v = x;
         }
     };
-    if (const char *c = getenv("WMI_ATTN_V1")) tn.attn_v1 = atoi(c) == 2 ? 2 : atoi(c) == 1 ? 1 : 0;
     knob("WMI_LOGITS_CAP", tn.logits_cap, 1);
     knob("WMI_LOGITS_G", tn.logits_g, 0);
     knob("WMI_GRAPH_STEPS", tn.graph_steps, 1);
@@ -2015,7 +2047,7 @@ int wmi_set_audio_ctx(wmi_context *ctx, int n_audio_ctx) {
 // Chunks other than "fmt " and "data" are skipped (word-aligned, as RIFF
 // requires); a data chunk longer than the file is an IO error, as is a
 // missing "fmt " before "data".
-int wmi_read_wav(const char *path, int16_t *samples, size_t cap, size_t *n_samples, int32_t *sample_rate,
+static int wmi_read_wav_impl(const char *path, int16_t *samples, size_t cap, size_t *n_samples, int32_t *sample_rate,
                  int32_t *channels) {
     if (!path || !n_samples) return set_err(nullptr, WMI_E_INVALID_ARG, "null argument");
     FILE *f = fopen(path, "rb");
@@ -2055,6 +2087,13 @@ int wmi_read_wav(const char *path, int16_t *samples, size_t cap, size_t *n_sampl
             if (channels) *channels = (int32_t)nch;
             if (!samples) return WMI_OK;
             if (cap < n) return WMI_E_NO_SPACE;
+            {
+                const long here = ftell(f);
+                fseek(f, 0, SEEK_END);
+                const long end = ftell(f);
+                fseek(f, here, SEEK_SET);
+                if ((long)size > end - here) return set_err(nullptr, WMI_E_IO, "%s: data chunk of %u bytes beyond the file", path, size);
+            }
             std::vector<unsigned char> raw(size);
             if (fread(raw.data(), 1, size, f) != size) return set_err(nullptr, WMI_E_IO, "%s: truncated data", path);
             for (size_t i = 0; i < n; ++i) samples[i] = (int16_t)u16(raw.data() + 2 * i);
@@ -2075,7 +2114,7 @@ int wmi_pcm16_to_f32(const int16_t *s16, size_t n, float *out) {
 // Text of a token sequence: the id_to_token bytes (main.rs:578-592) of every
 // text token (id < eot) concatenated, special and timestamp tokens skipped,
 // as whisper.cpp-1.0.3's whisper_full builds a segment's text.
-int wmi_tokens_to_text(const wmi_context *ctx, const int32_t *ids, int n, char *buf, size_t cap, size_t *len) {
+static int wmi_tokens_to_text_impl(const wmi_context *ctx, const int32_t *ids, int n, char *buf, size_t cap, size_t *len) {
     if (!ctx || (!ids && n) || n < 0 || !len) return WMI_E_INVALID_ARG;
     std::string s;
     for (int i = 0; i < n; ++i) {
@@ -2093,7 +2132,7 @@ static void to_token_data(const TsRec &r, wmi_token_data *d) {
     d->t0 = -1; d->t1 = -1; d->vlen = 0.0f;  // token-level timestamps are not computed (as whisper.cpp-1.0.3 by default)
 }
 
-int wmi_decode_timestamps(wmi_context *ctx, const int32_t *prompt, int n_prompt, int max_tokens, wmi_token_data *out,
+static int wmi_decode_timestamps_impl(wmi_context *ctx, const int32_t *prompt, int n_prompt, int max_tokens, wmi_token_data *out,
                           int32_t *n_out) {
     if (!valid(ctx) || !prompt || n_prompt < 1 || !out || !n_out) return WMI_E_INVALID_ARG;
     for (int i = 0; i < n_prompt; ++i)
@@ -2107,7 +2146,7 @@ int wmi_decode_timestamps(wmi_context *ctx, const int32_t *prompt, int n_prompt,
     return WMI_OK;
 }
 
-int wmi_transcribe(wmi_context *ctx, const float *pcm, size_t n_samples, int max_tokens, int32_t *n_segments) {
+static int wmi_transcribe_impl(wmi_context *ctx, const float *pcm, size_t n_samples, int max_tokens, int32_t *n_segments) {
     if (!valid(ctx) || (!pcm && n_samples) || max_tokens < 1 || !n_segments) return WMI_E_INVALID_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     const float *pp[1] = {pcm};
@@ -2150,7 +2189,7 @@ int wmi_token_to_bytes(const wmi_context *ctx, int32_t id, char *buf, size_t cap
     return WMI_OK;
 }
 
-int wmi_pcm_to_mel_batch(wmi_context *ctx, int n_clips, const float *const *pcm, const size_t *n_samples) {
+static int wmi_pcm_to_mel_batch_impl(wmi_context *ctx, int n_clips, const float *const *pcm, const size_t *n_samples) {
     if (!valid(ctx)) return WMI_E_INVALID_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc = stage_pcm(ctx, n_clips, pcm, n_samples);
@@ -2187,7 +2226,7 @@ int wmi_encode(wmi_context *ctx, int n_threads, int mel_offset) {
     return WMI_OK;
 }
 
-int wmi_decode_greedy(wmi_context *ctx, int max_tokens, int suppress_eot, int32_t *tokens, int32_t *n_tokens) {
+static int wmi_decode_greedy_impl(wmi_context *ctx, int max_tokens, int suppress_eot, int32_t *tokens, int32_t *n_tokens) {
     if (!valid(ctx) || !tokens || !n_tokens) return WMI_E_INVALID_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     std::vector<int32_t> tk, cnt;
@@ -2204,7 +2243,7 @@ int wmi_decode_greedy(wmi_context *ctx, int max_tokens, int suppress_eot, int32_
     return WMI_OK;
 }
 
-int wmi_decode_logits(wmi_context *ctx, int clip, const int32_t *tokens, int n_tokens, float *logits) {
+static int wmi_decode_logits_impl(wmi_context *ctx, int clip, const int32_t *tokens, int n_tokens, float *logits) {
     if (!valid(ctx) || !tokens || !logits || n_tokens < 1) return WMI_E_INVALID_ARG;
     if (ctx->enc_T <= 0) return set_err(ctx, WMI_E_INVALID_ARG, "decode before encode");
     if (clip < 0 || clip >= ctx->enc_clips) return set_err(ctx, WMI_E_INVALID_ARG, "clip %d", clip);
@@ -2240,7 +2279,7 @@ int wmi_decode_logits(wmi_context *ctx, int clip, const int32_t *tokens, int n_t
     return WMI_OK;
 }
 
-int wmi_decode_beam(wmi_context *ctx, int beam_size, int max_tokens, int suppress_eot, int32_t *tokens,
+static int wmi_decode_beam_impl(wmi_context *ctx, int beam_size, int max_tokens, int suppress_eot, int32_t *tokens,
                     int32_t *n_tokens, double *scores) {
     if (!valid(ctx) || !tokens || !n_tokens) return WMI_E_INVALID_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -2264,7 +2303,7 @@ int wmi_full(wmi_context *ctx, const float *pcm, size_t n_samples, int max_token
     return wmi_decode_greedy(ctx, max_tokens, 0, tokens, n_tokens);
 }
 
-int wmi_stage_pcm(wmi_context *ctx, int n_clips, const float *const *pcm, const size_t *n_samples) {
+static int wmi_stage_pcm_impl(wmi_context *ctx, int n_clips, const float *const *pcm, const size_t *n_samples) {
     if (!valid(ctx)) return WMI_E_INVALID_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     return stage_pcm(ctx, n_clips, pcm, n_samples);
@@ -2272,7 +2311,7 @@ int wmi_stage_pcm(wmi_context *ctx, int n_clips, const float *const *pcm, const 
 
 int wmi_run_staged(wmi_context *ctx, int mel_offset, int n_decode) { return wmi_run_staged_beam(ctx, mel_offset, n_decode, 0); }
 
-int wmi_run_staged_beam(wmi_context *ctx, int mel_offset, int n_decode, int beam_size) {
+static int wmi_run_staged_beam_impl(wmi_context *ctx, int mel_offset, int n_decode, int beam_size) {
     if (!valid(ctx)) return WMI_E_INVALID_ARG;
     if (ctx->n_clips < 1) return set_err(ctx, WMI_E_INVALID_ARG, "nothing staged");
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -2382,17 +2421,6 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
     const int n = hp.n_audio_state, T = ctx->enc_T, B = ctx->enc_clips, M = B * T;
     memset(out, 0, sizeof(*out));
     hipStream_t s = ctx->stream;
-    const int bar_wg = which == 6 ? 128 : which == 7 ? 256 : 512, bar_rounds = 32;
-    uint32_t *bar_cnt = ctx->derr + 32;  // inside the 256-byte tail of the sync region
-    uint32_t bar_base = 0;
-    if (which >= 6 && which <= 8) HIPCHK(ctx, hipMemsetAsync(bar_cnt, 0, 4, s));
-    // 9-12: hierarchical barrier at 256 WGs, modes 0-3; 13: mode 2 at 512 WGs
-    const int hb_mode = which == 13 ? 2 : which - 9, hb_wg = which == 13 ? 512 : 256;
-    uint32_t *hb_cnt = nullptr, hb_base = 0;
-    if (which >= 9 && which <= 13) {
-        HIPCHK(ctx, hipMalloc(&hb_cnt, 4096));
-        HIPCHK(ctx, hipMemsetAsync(hb_cnt, 0, 4096, s));
-    }
     auto launch = [&]() -> int {
         if (which == 0) {
             DecGemvArgs g{}; g.tune = &ctx->tune;
@@ -2420,14 +2448,6 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
             g.ck = ctx->ck; g.cv = ctx->cv; g.T = T; g.n_state = hp.n_text_state; g.n_clips = B;
             g.kscale = powf((float)n / (float)hp.n_audio_head, -0.25f);
             HIPCHK(ctx, launch_gemm(s, EPI_CROSSKV, g));
-        } else if (which == 4 || which == 5) {
-            HIPCHK(ctx, launch_probe(s, which - 4, ctx->hid, ctx->hid + (1 << 20)));
-        } else if (which >= 6 && which <= 8) {
-            HIPCHK(ctx, launch_probe_barrier(s, bar_wg, bar_rounds, bar_cnt, bar_base, ctx->derr));
-            bar_base += (uint32_t)(bar_wg * bar_rounds);
-        } else if (which >= 9 && which <= 13) {
-            HIPCHK(ctx, launch_probe_barrier_h(s, hb_mode, hb_wg, bar_rounds, hb_cnt, hb_base, ctx->derr));
-            hb_base += (uint32_t)bar_rounds;
         } else if (which == 14) {
             // the persistent greedy decoder over the staged clips, exactly as
             // the last run_staged launched it (per 8-row block: state and
@@ -2453,7 +2473,6 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
     float ms = 0;
     HIPCHK(ctx, hipEventElapsedTime(&ms, ctx->ev[6], ctx->ev[7]));
     out->avg_us = ms * 1000.0f / iters;
-    if (hb_cnt) HIPCHK(ctx, hipFree(hb_cnt));
     const double nt = hp.n_text_state, V = hp.n_vocab;
     if (which == 0) {
         const double b = B < 8 ? B : 8;
@@ -2468,16 +2487,7 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
     } else if (which == 2) {
         out->alg_flops = 4.0 * T * (double)T * n * B;
         out->alg_bytes = 4.0 * (double)M * n * 2;
-        snprintf(out->name, sizeof out->name, "k_attn_enc");
-    } else if (which == 4) {
-        snprintf(out->name, sizeof out->name, "k_probe_empty");
-    } else if (which == 5) {
-        out->alg_bytes = 2.0 * 256 * 256 * 16;
-        snprintf(out->name, sizeof out->name, "k_probe_copy (1 MiB)");
-    } else if (which >= 6 && which <= 8) {
-        snprintf(out->name, sizeof out->name, "k_probe_barrier (%d WG x %d barriers)", bar_wg, bar_rounds);
-    } else if (which >= 9 && which <= 13) {
-        snprintf(out->name, sizeof out->name, "k_probe_barrier_h mode %d (%d WG x %d barriers)", hb_mode, hb_wg, bar_rounds);
+        snprintf(out->name, sizeof out->name, "k_attn_enc3");
     } else if (which == 14) {
         // algorithmic bytes of one decode: every step reads each decoder
         // weight, bias and LayerNorm vector once (shared by the block's rows),
@@ -2527,8 +2537,8 @@ int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes) {
         case 9: src = ctx->dopart; have = R * (size_t)ctx->n_chunks_max * n * 4; break;
         case 10: {  // host: this context's tuning knobs (struct Tune, int32 fields in order)
             const Tune &t = ctx->tune;
-            const int32_t v[10] = {t.attn_v1, t.logits_cap, t.logits_g, t.logits_cap2, t.down_nw1_b,
-                                   t.gemv_nw, t.coop_max, t.xattn_rows, t.self_split, t.graph_steps};
+            const int32_t v[9] = {t.logits_cap, t.logits_g, t.logits_cap2, t.down_nw1_b, t.gemv_nw,
+                                  t.coop_max, t.xattn_rows, t.self_split, t.graph_steps};
             memcpy(out, v, std::min(sizeof v, bytes));
             return WMI_OK;
         }
@@ -2599,7 +2609,7 @@ int wmi_dist_init(wmi_context *ctx, int rank, int world, const void *id) {
     return WMI_OK;
 }
 
-int wmi_dist_gather_tokens(wmi_context *ctx, int32_t *out, size_t cap) {
+static int wmi_dist_gather_tokens_impl(wmi_context *ctx, int32_t *out, size_t cap) {
     if (!valid(ctx) || !ctx->comm) return WMI_E_INVALID_ARG;
     if (ctx->enc_clips < 1 || ctx->staged_n_decode < 1) return set_err(ctx, WMI_E_INVALID_ARG, "gather before a staged run");
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -2654,6 +2664,58 @@ int wmi_dist_barrier(wmi_context *ctx) {
     RCCLCHK(ctx, ncclAllReduce(ctx->d_dbar, ctx->d_dbar, 1, ncclInt32, ncclSum, ctx->comm, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return WMI_OK;
+}
+
+// ---- exception-guarded entry points (bodies above: *_impl) ----
+int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context **out) {
+    return guarded(nullptr, [&] { return wmi_init_from_file_impl(path, device, max_clips, out); });
+}
+
+int wmi_read_wav(const char *path, int16_t *samples, size_t cap, size_t *n_samples, int32_t *sample_rate,
+                 int32_t *channels) {
+    return guarded(nullptr, [&] { return wmi_read_wav_impl(path, samples, cap, n_samples, sample_rate, channels); });
+}
+
+int wmi_tokens_to_text(const wmi_context *ctx, const int32_t *ids, int n, char *buf, size_t cap, size_t *len) {
+    return guarded(const_cast<wmi_context *>(ctx), [&] { return wmi_tokens_to_text_impl(ctx, ids, n, buf, cap, len); });
+}
+
+int wmi_decode_timestamps(wmi_context *ctx, const int32_t *prompt, int n_prompt, int max_tokens, wmi_token_data *out,
+                          int32_t *n_out) {
+    return guarded(ctx, [&] { return wmi_decode_timestamps_impl(ctx, prompt, n_prompt, max_tokens, out, n_out); });
+}
+
+int wmi_transcribe(wmi_context *ctx, const float *pcm, size_t n_samples, int max_tokens, int32_t *n_segments) {
+    return guarded(ctx, [&] { return wmi_transcribe_impl(ctx, pcm, n_samples, max_tokens, n_segments); });
+}
+
+int wmi_pcm_to_mel_batch(wmi_context *ctx, int n_clips, const float *const *pcm, const size_t *n_samples) {
+    return guarded(ctx, [&] { return wmi_pcm_to_mel_batch_impl(ctx, n_clips, pcm, n_samples); });
+}
+
+int wmi_decode_greedy(wmi_context *ctx, int max_tokens, int suppress_eot, int32_t *tokens, int32_t *n_tokens) {
+    return guarded(ctx, [&] { return wmi_decode_greedy_impl(ctx, max_tokens, suppress_eot, tokens, n_tokens); });
+}
+
+int wmi_decode_logits(wmi_context *ctx, int clip, const int32_t *tokens, int n_tokens, float *logits) {
+    return guarded(ctx, [&] { return wmi_decode_logits_impl(ctx, clip, tokens, n_tokens, logits); });
+}
+
+int wmi_decode_beam(wmi_context *ctx, int beam_size, int max_tokens, int suppress_eot, int32_t *tokens,
+                    int32_t *n_tokens, double *scores) {
+    return guarded(ctx, [&] { return wmi_decode_beam_impl(ctx, beam_size, max_tokens, suppress_eot, tokens, n_tokens, scores); });
+}
+
+int wmi_stage_pcm(wmi_context *ctx, int n_clips, const float *const *pcm, const size_t *n_samples) {
+    return guarded(ctx, [&] { return wmi_stage_pcm_impl(ctx, n_clips, pcm, n_samples); });
+}
+
+int wmi_run_staged_beam(wmi_context *ctx, int mel_offset, int n_decode, int beam_size) {
+    return guarded(ctx, [&] { return wmi_run_staged_beam_impl(ctx, mel_offset, n_decode, beam_size); });
+}
+
+int wmi_dist_gather_tokens(wmi_context *ctx, int32_t *out, size_t cap) {
+    return guarded(ctx, [&] { return wmi_dist_gather_tokens_impl(ctx, out, cap); });
 }
 
 }  // extern "C"

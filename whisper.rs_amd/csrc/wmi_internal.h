@@ -11,10 +11,6 @@
 namespace wmi {
 
 // ---- launch-overhead probes: 0 = empty kernel, 1 = 256 x 4 KiB copy ---------
-hipError_t launch_probe(hipStream_t s, int which, const void *src, void *dst);
-hipError_t launch_probe_barrier(hipStream_t s, int n_wg, int rounds, uint32_t *cnt, uint32_t base, uint32_t *err);
-hipError_t launch_probe_barrier_h(hipStream_t s, int mode, int n_wg, int rounds, uint32_t *cnt, uint32_t base,
-                                  uint32_t *err);
 // device exp (decoder attention) vs the host-built ggml exp table, all inputs
 hipError_t launch_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *mismatch);
 
@@ -59,7 +55,6 @@ enum GemmEpi {
 // wmi_init_from_file).  Kernel-argument structs carry a pointer to their
 // context's copy; a null pointer means the defaults below.
 struct Tune {
-    int attn_v1 = 0;        // WMI_ATTN_V1: encoder attention version (1: v1, 2: v2, 0: v3)
     int logits_cap = 512;   // WMI_LOGITS_CAP: chain logits grid cap
     int logits_g = 2;       // WMI_LOGITS_G: logits rows per lane group
     int logits_cap2 = 1024; // WMI_LOGITS_CAP2

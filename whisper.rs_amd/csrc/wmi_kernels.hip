@@ -38,12 +38,6 @@ static hipError_t allow_lds(K *kern, size_t bytes) {
 // ============================================================================
 // launch-overhead probes (wmi_bench_kernel 4 / 5)
 // ============================================================================
-__global__ void k_probe_empty() {}
-__global__ __launch_bounds__(256) void k_probe_copy(const uint4 *src, uint4 *dst) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    dst[i] = src[i];
-}
-// every non-positive f16 argument: computed exp vs the host-built table
 __global__ void k_selftest_exp(const uint16_t *tab, int n_exp, uint32_t *mismatch) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j > 0x7c00) return;
@@ -57,11 +51,6 @@ hipError_t launch_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, ui
     return hipGetLastError();
 }
 
-hipError_t launch_probe(hipStream_t s, int which, const void *src, void *dst) {
-    if (which == 0) hipLaunchKernelGGL(k_probe_empty, dim3(1), dim3(64), 0, s);
-    else hipLaunchKernelGGL(k_probe_copy, dim3(256), dim3(256), 0, s, (const uint4 *)src, (uint4 *)dst);
-    return hipGetLastError();
-}
 
 // ============================================================================
 // mel frontend
@@ -529,357 +518,18 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a) {
 // ============================================================================
 constexpr int ATT_QB = 32;
 
-__global__ __launch_bounds__(256) void k_attn_enc(AttnArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
-    uint16_t *tab = (uint16_t *)smraw;
-    const int tab_bytes = ((a.n_exp * 2 + 15) / 16) * 16;
-    float *red = (float *)(smraw + tab_bytes);          // [4][32] f32
-    double *redd = (double *)(red + 128);               // [4][32] f64
-    float *opart = (float *)(redd + 128);               // [3][32][64] f32
-    const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int lr = lane & 31, lh = lane >> 5;
-    for (int i = tid; i < a.n_exp; i += 256) tab[i] = a.exp_tab[i];
-    const int64_t bh = (int64_t)b * a.H + h;
-    const f16 *Q = (const f16 *)a.q + bh * a.Tp * 64;
-    const f16 *K = (const f16 *)a.k + bh * a.Tp * 64;
-    const f16 *Vt = (const f16 *)a.vt + bh * 64 * a.Tp;
-    const int q0 = qb * ATT_QB;
-    const int T = a.T;
-    const float scale = a.scale;
-    half8 qf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = *(const half8 *)(Q + (int64_t)(q0 + lr) * 64 + 16 * s + 8 * lh);
-    const int ntiles = (T + 31) / 32;
-    __syncthreads();
-
-    auto qk_tile = [&](int key0) {
-        floatx16 sacc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[r] = 0.0f;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const half8 kf = *(const half8 *)(K + (int64_t)(key0 + lr) * 64 + 16 * s + 8 * lh);
-            sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[s], sacc, 0, 0, 0);
-        }
-        return sacc;
-    };
-
-    // pass 1: max
-    float mx = -INFINITY;
-    for (int kt = w; kt < ntiles; kt += 4) {
-        const int key0 = kt * 32;
-        const floatx16 sacc = qk_tile(key0);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            if (key < T) mx = fmaxf(mx, sacc[r] * scale);
-        }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    if (lh == 0) red[w * 32 + lr] = mx;
-    __syncthreads();
-    const float mrow = fmaxf(fmaxf(red[lr], red[32 + lr]), fmaxf(red[64 + lr], red[96 + lr]));
-
-    auto pexp = [&](float sv) -> float {
-        const uint32_t i = f2h_bits(sv - mrow) & 0x7fffu;
-        return (int)i < a.n_exp ? h2f_bits(tab[i]) : 0.0f;
-    };
-    // pass 2: sum
-    double sum = 0.0;
-    for (int kt = w; kt < ntiles; kt += 4) {
-        const int key0 = kt * 32;
-        const floatx16 sacc = qk_tile(key0);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            if (key < T) sum += (double)pexp(sacc[r] * scale);
-        }
-    }
-    sum += __shfl_xor(sum, 32);
-    if (lh == 0) redd[w * 32 + lr] = sum;
-    __syncthreads();
-    const float sumf = (float)(((redd[lr] + redd[32 + lr]) + redd[64 + lr]) + redd[96 + lr]);
-    const float inv = (float)(1.0 / (double)sumf);
-
-    // pass 3: O = P16 V
-    floatx16 o0, o1;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { o0[r] = 0.0f; o1[r] = 0.0f; }
-    for (int kt = w; kt < ntiles; kt += 4) {
-        const int key0 = kt * 32;
-        const floatx16 sacc = qk_tile(key0);
-        half8 pa[2];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            const float p = key < T ? pexp(sacc[r] * scale) * inv : 0.0f;
-            pa[r >> 3][r & 7] = (f16)p;
-        }
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-            const f16 *vrow = Vt + (int64_t)(dt * 32 + lr) * a.Tp + key0;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const half4 v0 = *(const half4 *)(vrow + 16 * s + 4 * lh);
-                const half4 v1 = *(const half4 *)(vrow + 16 * s + 8 + 4 * lh);
-                half8 vb;
-                vb[0] = v0[0]; vb[1] = v0[1]; vb[2] = v0[2]; vb[3] = v0[3];
-                vb[4] = v1[0]; vb[5] = v1[1]; vb[6] = v1[2]; vb[7] = v1[3];
-                if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[s], vb, o0, 0, 0, 0);
-                else o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[s], vb, o1, 0, 0, 0);
-            }
-        }
-    }
-    // combine the 4 waves' partial O: ((w0 + w1) + w2) + w3
-    if (w > 0) {
-        float *op = opart + (w - 1) * 32 * 64;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int q = (r & 3) + 8 * (r >> 2) + 4 * lh;
-            op[q * 64 + lr] = o0[r];
-            op[q * 64 + 32 + lr] = o1[r];
-        }
-    }
-    __syncthreads();
-    if (w == 0) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int q = (r & 3) + 8 * (r >> 2) + 4 * lh;
-            const int t = q0 + q;
-            float v0 = o0[r], v1 = o1[r];
-#pragma unroll
-            for (int ww = 0; ww < 3; ++ww) {
-                v0 = v0 + opart[ww * 2048 + q * 64 + lr];
-                v1 = v1 + opart[ww * 2048 + q * 64 + 32 + lr];
-            }
-            if (t < T) {
-                uint16_t *dst = a.out + ((int64_t)b * T + t) * a.n_state + h * 64;
-                dst[lr] = f2h_bits(v0);
-                dst[32 + lr] = f2h_bits(v1);
-            }
-        }
-    }
-}
-
-// Version 2 (default): the same three passes and the same arithmetic, but
-//  * 8 waves (two per SIMD) split the 32-key tiles;
-//  * K (and V) tiles are software-pipelined: tile i + 1's fragments are in
-//    flight while tile i is multiplied and reduced;
-//  * pass 2 keeps every table value e = exp_tab[f16(s - max)] (an f16) in LDS
-//    in the lane's own accumulator order, so pass 3 reads them back instead of
-//    recomputing Q K^T: two QK^T passes instead of three.  The e buffer
-//    (ntiles x 2 KB) later holds the waves' partial outputs.
+// Version 3: 8 waves (two per SIMD) split the 32-key tiles of one
+// 32-query block; a wave holds at most ATT2_TPW key tiles in registers.
 constexpr int ATT2_W = 8;
 constexpr int ATT2_TPW = 6;  // key tiles per wave held in registers: T <= 8 * 6 * 32 = 1536
 
-__global__ __launch_bounds__(512) void k_attn_enc2(AttnArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
-    uint16_t *tab = (uint16_t *)smraw;
-    const int tab_bytes = ((a.n_exp * 2 + 15) / 16) * 16;
-    float *red = (float *)(smraw + tab_bytes);                 // [8][32] f32
-    double *redd = (double *)(red + ATT2_W * 32);              // [8][32] f64
-    unsigned char *big = (unsigned char *)(redd + ATT2_W * 32);
-    uint16_t *ebuf = (uint16_t *)big;                          // [ntiles][64 lanes][16] f16 bits
-    float *opart = (float *)big;                               // [7][32][64] f32 (after pass 3)
-    const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int lr = lane & 31, lh = lane >> 5;
-    // the table into LDS in 16-byte chunks (the host pads it to whole chunks):
-    // its loads, then the K tile loads, are all in flight before the stores
-    constexpr int TCH = 6;  // chunks per thread: 6 * 512 * 8 >= 19.5k entries
-    const int nch = (a.n_exp + 7) / 8;
-    const uint4 *tsrc = (const uint4 *)a.exp_tab;
-    uint4 tch[TCH];
-#pragma unroll
-    for (int c = 0; c < TCH; ++c) {
-        const int i = tid + c * 64 * ATT2_W;
-        tch[c] = tsrc[i < nch ? i : 0];
-    }
-    const int64_t bh = (int64_t)b * a.H + h;
-    const f16 *Q = (const f16 *)a.q + bh * a.Tp * 64;
-    const f16 *K = (const f16 *)a.k + bh * a.Tp * 64;
-    const f16 *Vt = (const f16 *)a.vt + bh * 64 * a.Tp;
-    const int q0 = qb * ATT_QB;
-    const int T = a.T;
-    const float scale = a.scale;
-    half8 qf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = *(const half8 *)(Q + (int64_t)(q0 + lr) * 64 + 16 * s + 8 * lh);
-    const int ntiles = (T + 31) / 32;
-
-    // key tile fragments (rows past T are the zeroed padding up to Tp)
-    auto kload = [&](int kt, half8 (&kf)[4]) {
-        const int key0 = (kt < ntiles ? kt : ntiles - 1) * 32;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) kf[s] = *(const half8 *)(K + (int64_t)(key0 + lr) * 64 + 16 * s + 8 * lh);
-    };
-    auto qk = [&](const half8 (&kf)[4]) {
-        floatx16 sacc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[r] = 0.0f;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) sacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[s], qf[s], sacc, 0, 0, 0);
-        return sacc;
-    };
-
-    // every K tile of this wave in registers at once (one memory round trip),
-    // kept for passes 1 and 2
-    half8 kr[ATT2_TPW][4];
-#pragma unroll
-    for (int j = 0; j < ATT2_TPW; ++j) kload(w + ATT2_W * j, kr[j]);
-#pragma unroll
-    for (int c = 0; c < TCH; ++c) {
-        const int i = tid + c * 64 * ATT2_W;
-        if (i < nch) ((uint4 *)tab)[i] = tch[c];
-    }
-    for (int i = tid + TCH * 64 * ATT2_W; i < nch; i += 64 * ATT2_W) ((uint4 *)tab)[i] = tsrc[i];
-    __syncthreads();
-
-    // pass 1: max
-    float mx = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < ATT2_TPW; ++j) {
-        const int kt = w + ATT2_W * j;
-        if (kt < ntiles) {
-            const floatx16 sacc = qk(kr[j]);
-            const int key0 = kt * 32;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (key < T) mx = fmaxf(mx, sacc[r] * scale);
-            }
-        }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    if (lh == 0) red[w * 32 + lr] = mx;
-    __syncthreads();
-    float mrow = red[lr];
-#pragma unroll
-    for (int ww = 1; ww < ATT2_W; ++ww) mrow = fmaxf(mrow, red[ww * 32 + lr]);
-
-    // pass 2: e = exp_tab[f16(s - max)] kept in LDS, sum in double
-    double sum = 0.0;
-#pragma unroll
-    for (int j = 0; j < ATT2_TPW; ++j) {
-        const int kt = w + ATT2_W * j;
-        if (kt < ntiles) {
-            const floatx16 sacc = qk(kr[j]);
-            const int key0 = kt * 32;
-            uint16_t eb[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                const uint32_t i = f2h_bits(sacc[r] * scale - mrow) & 0x7fffu;
-                eb[r] = (key < T && (int)i < a.n_exp) ? tab[i] : (uint16_t)0;
-                if (key < T) sum += (double)h2f_bits(eb[r]);
-            }
-            uint4 *dst = (uint4 *)(ebuf + ((int64_t)kt * 64 + lane) * 16);
-            dst[0] = make_uint4(eb[0] | ((uint32_t)eb[1] << 16), eb[2] | ((uint32_t)eb[3] << 16),
-                                eb[4] | ((uint32_t)eb[5] << 16), eb[6] | ((uint32_t)eb[7] << 16));
-            dst[1] = make_uint4(eb[8] | ((uint32_t)eb[9] << 16), eb[10] | ((uint32_t)eb[11] << 16),
-                                eb[12] | ((uint32_t)eb[13] << 16), eb[14] | ((uint32_t)eb[15] << 16));
-        }
-    }
-    sum += __shfl_xor(sum, 32);
-    if (lh == 0) redd[w * 32 + lr] = sum;
-    __syncthreads();
-    double dsum = redd[lr];
-#pragma unroll
-    for (int ww = 1; ww < ATT2_W; ++ww) dsum = dsum + redd[ww * 32 + lr];
-    const float sumf = (float)dsum;
-    const float inv = (float)(1.0 / (double)sumf);
-
-    // pass 3: O = P16 V, P16 = f16(e * inv) from this wave's own LDS tiles
-    floatx16 o0, o1;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { o0[r] = 0.0f; o1[r] = 0.0f; }
-    auto vload = [&](int kt, half4 (&vf)[8]) {
-        const int key0 = (kt < ntiles ? kt : ntiles - 1) * 32;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-            const f16 *vrow = Vt + (int64_t)(dt * 32 + lr) * a.Tp + key0;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                vf[dt * 4 + s * 2] = *(const half4 *)(vrow + 16 * s + 4 * lh);
-                vf[dt * 4 + s * 2 + 1] = *(const half4 *)(vrow + 16 * s + 8 + 4 * lh);
-            }
-        }
-    };
-    // every V tile of this wave at once (the K registers are dead)
-    half4 vr[ATT2_TPW][8];
-#pragma unroll
-    for (int j = 0; j < ATT2_TPW; ++j) vload(w + ATT2_W * j, vr[j]);
-#pragma unroll
-    for (int j = 0; j < ATT2_TPW; ++j) {
-        const int kt = w + ATT2_W * j;
-        if (kt < ntiles) {
-            const half4 (&vc)[8] = vr[j];
-            const uint4 *src = (const uint4 *)(ebuf + ((int64_t)kt * 64 + lane) * 16);
-            const uint4 e0 = src[0], e1 = src[1];
-            const uint32_t ew[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-            const int key0 = kt * 32;
-            half8 pa[2];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                const uint16_t e = (uint16_t)(ew[r >> 1] >> (16 * (r & 1)));
-                const float p = key < T ? h2f_bits(e) * inv : 0.0f;
-                pa[r >> 3][r & 7] = (f16)p;
-            }
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const half4 v0 = vc[dt * 4 + s * 2], v1 = vc[dt * 4 + s * 2 + 1];
-                    half8 vb;
-                    vb[0] = v0[0]; vb[1] = v0[1]; vb[2] = v0[2]; vb[3] = v0[3];
-                    vb[4] = v1[0]; vb[5] = v1[1]; vb[6] = v1[2]; vb[7] = v1[3];
-                    if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[s], vb, o0, 0, 0, 0);
-                    else o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[s], vb, o1, 0, 0, 0);
-                }
-            }
-        }
-    }
-    // combine the waves' partial O in wave order (the e tiles are dead now)
-    __syncthreads();
-    if (w > 0) {
-        float *op = opart + (w - 1) * 32 * 64;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int q = (r & 3) + 8 * (r >> 2) + 4 * lh;
-            op[q * 64 + lr] = o0[r];
-            op[q * 64 + 32 + lr] = o1[r];
-        }
-    }
-    __syncthreads();
-    if (w == 0) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int q = (r & 3) + 8 * (r >> 2) + 4 * lh;
-            const int t = q0 + q;
-            float v0 = o0[r], v1 = o1[r];
-#pragma unroll
-            for (int ww = 0; ww < ATT2_W - 1; ++ww) {
-                v0 = v0 + opart[ww * 2048 + q * 64 + lr];
-                v1 = v1 + opart[ww * 2048 + q * 64 + 32 + lr];
-            }
-            if (t < T) {
-                uint16_t *dst = a.out + ((int64_t)b * T + t) * a.n_state + h * 64;
-                dst[lr] = f2h_bits(v0);
-                dst[32 + lr] = f2h_bits(v1);
-            }
-        }
-    }
-}
-
-// Version 3 (default): one QK^T pass.  Each of the 8 waves holds its (<= 6)
-// key tiles' scores S = scale * K Q^T in registers (issued as 24 back-to-back
-// MFMAs after one round trip for all its K fragments), takes the row max from
-// them (pass 1), turns them into the table values e = exp_tab[f16(S - max)]
-// kept as packed f16 registers (pass 2; V tiles requested meanwhile), and
-// multiplies P16 = f16(e * (1/sum)) with V (pass 3).  Same arithmetic as v1:
-// the scores are the very values v1 recomputes three times.
+// One QK^T pass.  Each of the 8 waves holds its (<= 6) key tiles' scores
+// S = scale * K Q^T in registers (issued as 24 back-to-back MFMAs after one
+// round trip for all its K fragments), takes the row max from them (pass 1),
+// turns them into the table values e = exp_tab[f16(S - max)] kept as packed
+// f16 registers (pass 2; V tiles requested meanwhile), and multiplies
+// P16 = f16(e * (1/sum)) with V (pass 3).  (Earlier versions recomputed Q K^T
+// per pass; they are in the git history.)
 __global__ __launch_bounds__(512) void k_attn_enc3(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
     uint16_t *tab = (uint16_t *)smraw;
@@ -1055,26 +705,12 @@ __global__ __launch_bounds__(512) void k_attn_enc3(AttnArgs a) {
 hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a) {
     dim3 grid(cdiv(a.T, ATT_QB), a.H, a.n_clips);
     const size_t tabb = ((a.n_exp * 2 + 15) / 16) * 16;
-    const size_t ebytes = (size_t)cdiv(a.T, 32) * 64 * 16 * 2, obytes = (size_t)(ATT2_W - 1) * 32 * 64 * 4;
-    const size_t lds2 = tabb + ATT2_W * 32 * 4 + ATT2_W * 32 * 8 + (ebytes > obytes ? ebytes : obytes);
+    const size_t obytes = (size_t)(ATT2_W - 1) * 32 * 64 * 4;
     const size_t lds3 = tabb + ATT2_W * 32 * 4 + ATT2_W * 32 * 8 + obytes;
-    const Tune &tn = tune_of(a.tune);
-    if (tn.attn_v1 == 0 && lds3 <= 160 * 1024 && cdiv(a.T, 32) <= ATT2_W * ATT2_TPW) {
-        hipError_t e = allow_lds(k_attn_enc3, lds3);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_attn_enc3, grid, dim3(64 * ATT2_W), lds3, s, a);
-        return hipGetLastError();
-    }
-    if (tn.attn_v1 != 1 && lds2 <= 160 * 1024 && cdiv(a.T, 32) <= ATT2_W * ATT2_TPW) {
-        hipError_t e = allow_lds(k_attn_enc2, lds2);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_attn_enc2, grid, dim3(64 * ATT2_W), lds2, s, a);
-        return hipGetLastError();
-    }
-    const size_t lds = tabb + 128 * 4 + 128 * 8 + 3 * 32 * 64 * 4;
-    hipError_t e = allow_lds(k_attn_enc, lds);
+    if (lds3 > 160 * 1024 || cdiv(a.T, 32) > ATT2_W * ATT2_TPW) return hipErrorInvalidValue;  // T <= 1536
+    hipError_t e = allow_lds(k_attn_enc3, lds3);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_attn_enc, grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL(k_attn_enc3, grid, dim3(64 * ATT2_W), lds3, s, a);
     return hipGetLastError();
 }
 
@@ -1638,63 +1274,6 @@ __device__ __forceinline__ uint32_t spin_until(uint32_t *p, uint32_t target, uin
     }
     asm volatile("" ::: "memory");
     return v;
-}
-
-// grid-barrier probe (wmi_bench_kernel 6-8): `rounds` device-wide barriers on
-// a monotonic counter (base = value left by earlier launches)
-__global__ __launch_bounds__(256) void k_probe_barrier(uint32_t *cnt, uint32_t base, int rounds, uint32_t *err) {
-    for (int r = 0; r < rounds; ++r) {
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            spin_until(cnt, base + (uint32_t)(r + 1) * gridDim.x, err);
-        }
-        __syncthreads();
-    }
-}
-
-// hierarchical grid barrier probe: workgroup i arrives on group counter i % 8
-// (one group per XCD under round-robin dispatch, so arrivals contend only
-// within an XCD); the last arrival of a group bumps the top counter.  MODE 0:
-// every workgroup polls the top counter; MODE 1: group leaders poll it and
-// release their group through a per-group word.  FENCE adds the agent-scope
-// release / acquire fences a real hand-off of plain-stored data needs.
-// Layout (uint32 index): group counters g * 32, top 256, release words 288 + g * 32.
-template <int MODE, bool FENCE>
-__global__ __launch_bounds__(256) void k_probe_barrier_h(uint32_t *cnt, uint32_t base, int rounds, uint32_t *err) {
-    const int g = blockIdx.x & 7, ng = gridDim.x >> 3;
-    for (int r = 0; r < rounds; ++r) {
-        const uint32_t gen = base + (uint32_t)r + 1;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            if (FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            const uint32_t old = __hip_atomic_fetch_add(cnt + g * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const bool last = old + 1 == gen * (uint32_t)ng;
-            if (last) __hip_atomic_fetch_add(cnt + 256, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (MODE == 0 || last) spin_until(cnt + 256, gen * 8u, err);
-            if (MODE == 1) {
-                if (last) __hip_atomic_store(cnt + 288 + g * 32, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else spin_until(cnt + 288 + g * 32, gen, err);
-            }
-            if (FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-        __syncthreads();
-    }
-}
-
-hipError_t launch_probe_barrier_h(hipStream_t s, int mode, int n_wg, int rounds, uint32_t *cnt, uint32_t base,
-                                  uint32_t *err) {
-    if (n_wg % 8) return hipErrorInvalidValue;
-    if (mode == 0) hipLaunchKernelGGL((k_probe_barrier_h<0, false>), dim3(n_wg), dim3(256), 0, s, cnt, base, rounds, err);
-    else if (mode == 1) hipLaunchKernelGGL((k_probe_barrier_h<1, false>), dim3(n_wg), dim3(256), 0, s, cnt, base, rounds, err);
-    else if (mode == 2) hipLaunchKernelGGL((k_probe_barrier_h<0, true>), dim3(n_wg), dim3(256), 0, s, cnt, base, rounds, err);
-    else hipLaunchKernelGGL((k_probe_barrier_h<1, true>), dim3(n_wg), dim3(256), 0, s, cnt, base, rounds, err);
-    return hipGetLastError();
-}
-
-hipError_t launch_probe_barrier(hipStream_t s, int n_wg, int rounds, uint32_t *cnt, uint32_t base, uint32_t *err) {
-    hipLaunchKernelGGL(k_probe_barrier, dim3(n_wg), dim3(256), 0, s, cnt, base, rounds, err);
-    return hipGetLastError();
 }
 
 // ---- words exchanged between workgroups of one launch ----------------------
