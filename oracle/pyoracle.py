@@ -249,7 +249,8 @@ def transcribe_ref(om, pcm, n_ctx, max_tokens, token_text, n_threads=8):
     past, segs, margin, seek = [], [], np.inf, 0
     while seek < n_len:
         _, ck, cv = om.encode(mel, n_ctx=n_ctx, mel_offset=seek, n_threads=n_threads)
-        prompt = ([sp["prev"]] + past[-(hp["n_text_ctx"] // 2 - 1):] if past else []) + init
+        # whisper_full: n_take = min(n_text_ctx / 2, past size) tokens after <|prev|>
+        prompt = ([sp["prev"]] + past[-(hp["n_text_ctx"] // 2):] if past else []) + init
         toks, m = ts_window_ref(om, ck, cv, prompt, n_max, n_threads)
         margin = min(margin, m)
         seek_delta, result_len, failed, ended = window, 0, False, False

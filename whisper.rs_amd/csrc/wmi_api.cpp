@@ -1689,8 +1689,9 @@ int run_ts_window(wmi_context *ctx, int clip, const std::vector<int32_t> &prompt
 // whisper_full (whisper.cpp-1.0.3, the loop the reference's WhisperSegment /
 // WhisperTokenData / prompt_past fields belong to, main.rs:317-331, 353-362,
 // 599-604): windows of 2 * n_ctx mel frames from `seek`, prompt = [prev] +
-// the last n_text_ctx/2 - 1 tokens of earlier windows + [sot (, lang,
-// transcribe)], timestamp sampling; a window's tokens up to its last
+// the last min(n_text_ctx/2, past) tokens of earlier windows (whisper_full's
+// n_take) + [sot (, lang, transcribe)], at most n_text_ctx/2 - 4 sampled
+// tokens (1 + 224 + 3 + 220 = 448 positions at most), timestamp sampling; a window's tokens up to its last
 // timestamp form segments [t0, t1) in 10 ms units; seek advances to the
 // last timestamp, or past the window; a window without a usable timestamp is
 // skipped by 100 frames.  Restated op for op in oracle/pyoracle.py transcribe_ref.
@@ -1711,7 +1712,7 @@ int run_transcribe(wmi_context *ctx, int max_tokens) {
         std::vector<int32_t> prompt;
         if (!past.empty()) {
             prompt.push_back(ctx->sp.prev);
-            const size_t keep = std::min(past.size(), (size_t)(hp.n_text_ctx / 2 - 1));
+            const size_t keep = std::min(past.size(), (size_t)(hp.n_text_ctx / 2));
             prompt.insert(prompt.end(), past.end() - keep, past.end());
         }
         prompt.insert(prompt.end(), init.begin(), init.end());
