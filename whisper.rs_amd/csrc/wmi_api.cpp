@@ -280,6 +280,8 @@ struct wmi_context {
     bool persist_logits = false;      // WMI_PERSIST_LOGITS=1: also store every step's logits (dlogits)
     int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
     PersistLayer *d_players = nullptr;
+    uint32_t *d_expfb = nullptr;       // exp fallback list of the persistent decoder [64] + count
+    int n_expfb = 0;
     uint64_t *d_xg = nullptr;         // exchange block (persist_layout at n_audio_ctx)
     size_t xg_bytes = 0;
     int32_t *d_curtok = nullptr;      // [8]
@@ -874,6 +876,15 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
     }
     HIPCHK(ctx, hipMalloc(&ctx->d_players, pl.size() * sizeof(PersistLayer)));
     HIPCHK(ctx, hipMemcpy(ctx->d_players, pl.data(), pl.size() * sizeof(PersistLayer), hipMemcpyHostToDevice));
+    // the persistent decoder's exp fallback list (64 entries + a count word)
+    HIPCHK(ctx, hipMalloc(&ctx->d_expfb, 65 * 4));
+    HIPCHK(ctx, hipMemset(ctx->d_expfb, 0xff, 64 * 4));
+    HIPCHK(ctx, hipMemset(ctx->d_expfb + 64, 0, 4));
+    HIPCHK(ctx, launch_exp_fallbacks(nullptr, ctx->exp_tab, ctx->n_exp, ctx->d_expfb, ctx->d_expfb + 64));
+    uint32_t nfb = 0;
+    HIPCHK(ctx, hipMemcpy(&nfb, ctx->d_expfb + 64, 4, hipMemcpyDeviceToHost));
+    ctx->n_expfb = (int)nfb;
+    if (nfb > 64) ctx->use_persist = false;  // (not seen: ~19 inputs) the kernel chain then decodes
     return WMI_OK;
 }
 
@@ -1515,7 +1526,7 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     const int n = hp.n_text_state, H = hp.n_text_head, T = ctx->enc_T;
     PersistArgs a{};
     a.layers = ctx->d_players; a.te = ctx->te; a.pe = ctx->d_pe; a.dln_w = ctx->dln_w; a.dln_b = ctx->dln_b;
-    a.gelu_tab = ctx->gelu_tab; a.exp_tab = ctx->exp_tab; a.n_exp = ctx->n_exp;
+    a.gelu_tab = ctx->gelu_tab; a.exp_tab = ctx->exp_tab; a.n_exp = ctx->n_exp; a.exp_fb = ctx->d_expfb;
     a.kcache = ctx->kcache; a.vcache = ctx->vcache; a.ck = ctx->ck; a.cv = ctx->cv;
     a.L = ctx->dec_layers; a.n = n; a.V = hp.n_vocab; a.B = B; a.T = T; a.tctx = hp.n_text_ctx;
     a.Bt = ctx->enc_clips; a.b0 = b0;
@@ -1965,7 +1976,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (getenv("WMI_NO_COOP")) ctx->use_coop = false;
     if (getenv("WMI_NO_Q5")) ctx->use_q5 = false;
     if (getenv("WMI_NO_FUSE")) ctx->fuse_wo = false;
-    if (const char *c = getenv("WMI_PERSIST")) ctx->use_persist = atoi(c) != 0;
+    if (const char *c = getenv("WMI_PERSIST")) ctx->use_persist = ctx->use_persist && atoi(c) != 0;
     if (getenv("WMI_PERSIST_LOGITS")) ctx->persist_logits = true;
     if (const char *c = getenv("WMI_CHECKSUMS")) ctx->checksums = atoi(c) != 0;
     ctx->dec_layers = ctx->hp.n_text_layer;
@@ -2017,6 +2028,7 @@ void wmi_free(wmi_context *ctx) {
     if (ctx->d_trace) (void)hipFree(ctx->d_trace);
     if (ctx->d_model) (void)hipFree(ctx->d_model);
     if (ctx->d_players) (void)hipFree(ctx->d_players);
+    if (ctx->d_expfb) (void)hipFree(ctx->d_expfb);
     if (ctx->d_ptrace) (void)hipFree(ctx->d_ptrace);
     for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -2554,7 +2566,7 @@ int wmi_selftest(wmi_context *ctx, int32_t *n_mismatch) {
     HIPCHK(ctx, hipSetDevice(ctx->device));
     HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));
     HIPCHK(ctx, launch_selftest(ctx->stream, ctx->exp_tab, ctx->n_exp, ctx->derr));
-    HIPCHK(ctx, launch_persist_selftest(ctx->stream, ctx->exp_tab, ctx->n_exp, ctx->derr));
+    HIPCHK(ctx, launch_persist_selftest(ctx->stream, ctx->exp_tab, ctx->n_exp, ctx->d_expfb, ctx->derr));
     uint32_t mm = 0;
     HIPCHK(ctx, hipMemcpyAsync(&mm, ctx->derr, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));

@@ -317,6 +317,7 @@ struct PersistArgs {
     const uint16_t *gelu_tab;    // ggml GELU table [65536]
     const uint16_t *exp_tab;     // ggml exp table, non-positive half [n_exp]
     int n_exp;
+    const uint32_t *exp_fb;      // [64] exp fallback list (launch_exp_fallbacks), 0xffffffff-padded
     uint16_t *kcache, *vcache;   // [L][DEC_ROWS][tctx][n]
     const uint16_t *ck, *cv;     // cross K/V [L][Bt][T][n]; row b uses clip b0 + b
     int L, n, V, B, T, tctx, Bt, b0;
@@ -344,8 +345,12 @@ struct PersistArgs {
     int kv_src_stride;
 };
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G);
+// the inputs whose f32 exp is too close to an f16 midpoint, with their table
+// values, into list[64] (count in *n; > 64 means the list is unusable)
+hipError_t launch_exp_fallbacks(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *list, uint32_t *n);
 // the persistent decoder's exp vs the host ggml table, every non-positive f16 input
-hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *mismatch);
+hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, const uint32_t *fb,
+                                   uint32_t *mismatch);
 // largest co-resident grid for the model (0: not supported for this n / B / T)
 // and the vocabulary rows per workgroup that fit in LDS beside the phases' data
 int persist_grid(int device, int n, int B, int T, int V, int *nres);

@@ -49,6 +49,7 @@ constexpr int PMAXB = 8;                // decoder rows
 constexpr int RNMAX = 16;               // rows of an n-row GEMV per workgroup
 constexpr int SCR_BYTES = 24 * 1024;    // attention / argmax scratch in LDS
 constexpr int NKP = 4;                  // 128-key passes per cross-attention chunk (cl <= 512)
+constexpr int EXPFB = 64;               // exp fallback list entries (exp_f16_fast)
 
 __device__ __forceinline__ uint64_t gld(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -106,6 +107,7 @@ struct PShared {
     double redd[4];
     unsigned long long best[4][PMAXB];
     float ored[4][64 * 4];  // per wave: up to NKP 64-float partials
+    __attribute__((aligned(16))) uint32_t expfb[EXPFB];  // exp fallback list (exp_f16_fast)
     float kpart[16 * PMAXB];  // split-K GEMV: per (row, k-slice) partials of every decoder row
     int abort_;
 };
@@ -397,20 +399,37 @@ __device__ __forceinline__ void ln_rows(const float *xf, const LnP<NS> &P, f16 *
 // ggml's table_exp_f16 value f16(exp(double(f16 x))) for x <= 0 without a
 // double exp (whose polynomial constants the compiler would keep live in
 // registers across the whole persistent loop): the f32 exp rounds to the same
-// f16 unless it lies within 4 f32 ulps of an f16 rounding midpoint — 16 of the
-// 31744 non-positive inputs (checked exhaustively on the host) — and those
-// read the host-built table.
-__device__ __forceinline__ float exp_f16_fast(float arg, const uint16_t *tab, int n_exp) {
-    const f16 hx = (f16)arg;
+// f16 unless it lies within 4 f32 ulps of an f16 rounding midpoint.  Those
+// inputs (~19 of the 31744 non-positive ones) are found once per context on
+// the device (k_exp_fallbacks) and their table values kept in a 64-entry
+// list {j << 16 | value} (0xffffffff-padded) that the kernel holds in LDS:
+// the rare lane reads it with 16 independent LDS loads instead of waiting
+// for a global table load.
+__device__ __forceinline__ bool exp_f16_fast_ok(float arg, f16 &hx, float &hv) {
+    hx = (f16)arg;
     const float r = expf((float)hx);
     const uint16_t hr = f2h_bits(r);
-    const float hv = h2f_bits(hr);
+    hv = h2f_bits(hr);
     const float nb = h2f_bits(r >= hv ? (uint16_t)(hr + 1) : (uint16_t)(hr - 1));
     const float mid = 0.5f * (hv + nb);
     const float ulp = __uint_as_float(__float_as_uint(r) & 0x7f800000u) * 1.1920928955078125e-7f;
-    if (fabsf(r - mid) > 4.0f * ulp) return hv;
-    const int j = __builtin_bit_cast(uint16_t, hx) & 0x7fff;
-    return j < n_exp ? h2f_bits(tab[j]) : 0.0f;
+    return fabsf(r - mid) > 4.0f * ulp;
+}
+__device__ __forceinline__ float exp_f16_fast(float arg, const uint32_t *fb) {
+    f16 hx;
+    float hv;
+    if (exp_f16_fast_ok(arg, hx, hv)) return hv;
+    const uint32_t j = __builtin_bit_cast(uint16_t, hx) & 0x7fff;
+    uint32_t hit = 0xffffffffu;
+#pragma unroll
+    for (int i = 0; i < EXPFB; i += 4) {
+        const uint4 e = *(const uint4 *)(fb + i);
+        hit = (e.x >> 16) == j ? e.x : hit;
+        hit = (e.y >> 16) == j ? e.y : hit;
+        hit = (e.z >> 16) == j ? e.z : hit;
+        hit = (e.w >> 16) == j ? e.w : hit;
+    }
+    return hit != 0xffffffffu ? h2f_bits((uint16_t)hit) : hv;
 }
 
 // Every phase re-derives its lane indices from an opaque copy of threadIdx.x
@@ -496,6 +515,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
         for (int i = tid; i < (rs0 - rv0) * NS / 8; i += PT) dst[i] = src[i];
     }
     if (tid == 0) sh.abort_ = 0;
+    if (tid < EXPFB) sh.expfb[tid] = a.exp_fb[tid];
     __syncthreads();
     auto check = [&](bool ok) -> bool {  // workgroup-uniform abort after a poll
         if (!ok) sh.abort_ = 1;
@@ -686,7 +706,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     for (int r = 0; r < 2; ++r) {
                         p[r] = 0.0f;
                         if (tid + 256 * r < M) {
-                            p[r] = exp_f16_fast(sc[r] - mx, a.exp_tab, a.n_exp);
+                            p[r] = exp_f16_fast(sc[r] - mx, sh.expfb);
                             sum += (double)p[r];
                         }
                     }
@@ -914,7 +934,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
                         const int j = tid + 256 * u;
-                        const float pj = exp_f16_fast(sv[u] - m, a.exp_tab, a.n_exp);
+                        const float pj = exp_f16_fast(sv[u] - m, sh.expfb);
                         if (j < T) {
                             sum += (double)pj;
                             Sx[j] = pj;
@@ -1229,12 +1249,26 @@ int grid_nsb(int device, int B, int V, int *nres) {
     return G;
 }
 
-// exp_f16_fast against the host-built ggml exp table over every non-positive f16 input
-__global__ void k_persist_selftest(const uint16_t *tab, int n_exp, uint32_t *mismatch) {
+// the fallback list: every non-positive f16 input whose f32 exp lies too
+// close to an f16 rounding midpoint, with its table value (count in *n;
+// entries beyond EXPFB are counted, not stored — the host then refuses)
+__global__ void k_exp_fallbacks(const uint16_t *tab, int n_exp, uint32_t *list, uint32_t *n) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > 0x7c00) return;
+    f16 hx;
+    float hv;
+    if (exp_f16_fast_ok(h2f_bits((uint16_t)(0x8000u | (uint32_t)j)), hx, hv)) return;
+    const uint32_t k = atomicAdd(n, 1u);
+    if (k < (uint32_t)EXPFB) list[k] = ((uint32_t)j << 16) | (j < n_exp ? tab[j] : 0u);
+}
+
+// exp_f16_fast (with the list) against the host-built ggml exp table over
+// every non-positive f16 input
+__global__ void k_persist_selftest(const uint16_t *tab, int n_exp, const uint32_t *fb, uint32_t *mismatch) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j > 0x7c00) return;
     const float x = h2f_bits((uint16_t)(0x8000u | (uint32_t)j));
-    const uint16_t got = f2h_bits(exp_f16_fast(x, tab, n_exp));
+    const uint16_t got = f2h_bits(exp_f16_fast(x, fb));
     const uint16_t want = j < n_exp ? tab[j] : (uint16_t)0;
     if (got != want) atomicAdd(mismatch, 1u);
 }
@@ -1252,8 +1286,14 @@ int grid_ns(int device, int B, int V, int *nres) {
 
 }  // namespace
 
-hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *mismatch) {
-    hipLaunchKernelGGL(k_persist_selftest, dim3((0x7c01 + 255) / 256), dim3(256), 0, s, exp_tab, n_exp, mismatch);
+hipError_t launch_exp_fallbacks(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *list, uint32_t *n) {
+    hipLaunchKernelGGL(k_exp_fallbacks, dim3((0x7c01 + 255) / 256), dim3(256), 0, s, exp_tab, n_exp, list, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, const uint32_t *fb,
+                                   uint32_t *mismatch) {
+    hipLaunchKernelGGL(k_persist_selftest, dim3((0x7c01 + 255) / 256), dim3(256), 0, s, exp_tab, n_exp, fb, mismatch);
     return hipGetLastError();
 }
 
