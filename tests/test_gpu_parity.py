@@ -416,6 +416,41 @@ def test_small_q5_1(wmi, model_cache):
         om.close()
 
 
+@pytest.mark.parametrize("model,n_clips", [("micro-q5_1", 1), ("micro-q5_1", 3), ("small-q5_1", 1),
+                                           ("small-q5_1", 2)])
+def test_persistent_q5_equals_f16(wmi, model_cache, model, n_clips):
+    """The persistent decoder's q5_1 instances (phases A, C, G2, H, I stream
+    the q5_1 blocks and dequantise them in registers) give bitwise the ids and
+    step logits of its f16 instances on the loader's dequantised copies
+    (WMI_NO_Q5=1): both multiply the same f16 weights in the same order."""
+    import os
+    if model == "micro-q5_1":
+        path = os.path.join(model_cache, "ggml-synth-micro-q5_1.bin")
+        if not os.path.exists(path):
+            synth.write_ggml(path, "micro", quant="q5_1")
+        secs, n_ctx = 2.0, 64
+    else:
+        path, secs, n_ctx = synth.model_path(model, model_cache), 30.0, 1500
+    clips = [synth.synth_pcm_f32(secs, 70 + i) for i in range(n_clips)]
+    ctxs = [_ctx_with_env(wmi, path, env, max_clips=n_clips)
+            for env in ({"WMI_PERSIST_LOGITS": "1", "WMI_PERSIST_Q5": "1"}, {"WMI_PERSIST_LOGITS": "1", "WMI_NO_Q5": "1"})]
+    try:
+        out = []
+        for ctx in ctxs:
+            ctx.set_audio_ctx(n_ctx)
+            ctx.pcm_to_mel_batch(clips)
+            ctx.encode(1, 0)
+            toks = ctx.decode_greedy(24, suppress_eot=True)
+            V = ctx.hparams["n_vocab"]  # last step's logits, rows [n_clips][V] (WMI_PERSIST_LOGITS)
+            out.append((toks, np.frombuffer(ctx.debug_read(2, n_clips * V * 4), np.float32).copy()))
+        for i in range(n_clips):
+            np.testing.assert_array_equal(out[0][0][i], out[1][0][i])
+        np.testing.assert_array_equal(out[0][1], out[1][1])
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+
+
 @pytest.mark.parametrize("model,n_clips,n_ctx", [("micro", 1, 64), ("micro", 3, 64), ("micro", 2, 1500),
                                                  ("tiny.en", 1, 1500), ("base", 2, 1500)])
 def test_persistent_matches_chain(wmi, model_cache, model, n_clips, n_ctx):

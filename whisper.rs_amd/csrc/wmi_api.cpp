@@ -277,6 +277,7 @@ struct wmi_context {
     bool checksums = false;           // WMI_CHECKSUMS=1: the reference's stage sums (debug prints)
     float cks[5] = {0, 0, 0, 0, 0};   // _hann, samples, filters, mel before normalisation, mel window
     bool use_persist = true;          // WMI_PERSIST=0: kernel chain instead
+    int persist_q5 = -1;              // WMI_PERSIST_Q5: 1 always, 0 never, default when B > 1
     bool persist_logits = false;      // WMI_PERSIST_LOGITS=1: also store every step's logits (dlogits)
     int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
     PersistLayer *d_players = nullptr;
@@ -866,13 +867,14 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
                        Q(dq5[i].wqkv), Q(dq5[i].wo), Q(dq5[i].wco), Q(dq5[i].w0), Q(dq5[i].w1)};
     }
     ctx->te5 = q5 ? (const uint8_t *)(base + o_te5) : nullptr;
-    // layer table of the persistent decoder (f16 weights; q5_1 models use the
-    // dequantised f16 copies, the same weights the q5_1 GEMVs dequantise to)
+    // layer table of the persistent decoder: f16 weights, and for q5_1 models
+    // the repacked blocks its GEMVs dequantise in registers (to exactly the f16 copies)
     std::vector<PersistLayer> pl(Lt);
     for (int i = 0; i < Lt; ++i) {
         const DecLayerDev &d = ctx->dec[i];
         pl[i] = {d.ln1_w, d.ln1_b, d.wqkv, d.bqkv, d.wo, d.bo, d.lnc_w, d.lnc_b, d.wcq, d.bcq,
-                 d.wco, d.bco, d.ln2_w, d.ln2_b, d.w0, d.b0, d.w1, d.b1};
+                 d.wco, d.bco, d.ln2_w, d.ln2_b, d.w0, d.b0, d.w1, d.b1,
+                 d.wqkv5, d.wo5, d.wco5, d.w05, d.w15};
     }
     HIPCHK(ctx, hipMalloc(&ctx->d_players, pl.size() * sizeof(PersistLayer)));
     HIPCHK(ctx, hipMemcpy(ctx->d_players, pl.data(), pl.size() * sizeof(PersistLayer), hipMemcpyHostToDevice));
@@ -1546,6 +1548,11 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     a.xg = ctx->d_xg; a.err = ctx->derr;
     a.nres = ctx->persist_nres[B];
     a.logits_out = ctx->persist_logits ? ctx->dlogits : nullptr;
+    // q5_1 blocks in the persistent GEMVs: the dequantisation VALU costs more
+    // than the smaller stream saves at one row (small: 357 vs 329 us/step) and
+    // less at eight (845 vs 918 us/step), so by default only when B > 1
+    const bool have5 = ctx->use_q5 && !ctx->dec.empty() && ctx->dec[0].wqkv5;
+    a.q5 = have5 && (ctx->persist_q5 > 0 || (ctx->persist_q5 < 0 && B > 1)) ? 1 : 0;
     return a;
 }
 
@@ -1978,6 +1985,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (getenv("WMI_NO_FUSE")) ctx->fuse_wo = false;
     if (const char *c = getenv("WMI_PERSIST")) ctx->use_persist = ctx->use_persist && atoi(c) != 0;
     if (getenv("WMI_PERSIST_LOGITS")) ctx->persist_logits = true;
+    if (const char *e = getenv("WMI_PERSIST_Q5")) ctx->persist_q5 = atoi(e) ? 1 : 0;
     if (const char *c = getenv("WMI_CHECKSUMS")) ctx->checksums = atoi(c) != 0;
     ctx->dec_layers = ctx->hp.n_text_layer;
     if (const char *c = getenv("WMI_DEC_LAYERS")) ctx->dec_layers = std::max(1, std::min(atoi(c), ctx->hp.n_text_layer));

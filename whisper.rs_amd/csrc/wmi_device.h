@@ -180,6 +180,31 @@ __device__ __forceinline__ float exp_f16_exact(float arg) {
 }
 
 // f16 x f16 products of 8 lanes accumulated in f32 (ggml_vec_dot_f16 step)
+// q5_1 weights (repacked at load: per row K/2 bytes of nibbles in natural
+// order, then per 32-block a u32 of 5th bits and a u32 {f16 d, f16 m}):
+// eight weights starting at block offset sh, dequantised exactly as the host
+// loader does, w = f16(q * d + m) rounded once.  Packed: two quants per dword
+// as f16 (1024 + q) via v_perm + bit spread, minus 1024 (exact), then one
+// v_pk_fma_f16 per pair.
+__device__ __forceinline__ half8 q5_half8(uint32_t qn, uint32_t qh, uint32_t dm, int sh) {
+    const uint32_t lo = qn & 0x0F0F0F0Fu, hi = (qn >> 4) & 0x0F0F0F0Fu;  // weights 0,2,4,6 / 1,3,5,7
+    const uint32_t hb = qh >> sh;
+    const half2v d2 = __builtin_bit_cast(half2v, __builtin_amdgcn_perm(dm, dm, 0x01000100u));
+    const half2v m2 = __builtin_bit_cast(half2v, __builtin_amdgcn_perm(dm, dm, 0x03020302u));
+    const half2v k1024 = {(f16)1024.0f, (f16)1024.0f};
+    half8 w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t nib = __builtin_amdgcn_perm(hi, lo, 0x0C000C00u | ((uint32_t)(4 + i) << 16) | (uint32_t)i);
+        const uint32_t h5 = ((__builtin_amdgcn_ubfe(hb, 2 * i, 2)) * 0x80010u) & 0x100010u;
+        const half2v q2 = __builtin_bit_cast(half2v, nib | h5 | 0x64006400u) - k1024;
+        const half2v r = __builtin_elementwise_fma(q2, d2, m2);
+        w[2 * i] = r[0];
+        w[2 * i + 1] = r[1];
+    }
+    return w;
+}
+
 __device__ __forceinline__ float dot8(const half8 w, const half8 x, float acc) {
     acc = __builtin_amdgcn_fdot2(half2v{w[0], w[1]}, half2v{x[0], x[1]}, acc, false);
     acc = __builtin_amdgcn_fdot2(half2v{w[2], w[3]}, half2v{x[2], x[3]}, acc, false);

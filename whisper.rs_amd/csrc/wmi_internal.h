@@ -278,6 +278,8 @@ struct PersistLayer {          // decoder layer weights (device pointers)
     const float *ln2_w, *ln2_b;
     const uint16_t *w0; const float *b0;       // [4n][n]
     const uint16_t *w1; const float *b1;       // [n][4n]
+    // q5_1 repacks of wqkv, wo, wco, w0, w1 (wmi_api.cpp repack_q5), or null
+    const uint8_t *wqkv5, *wo5, *wco5, *w05, *w15;
 };
 
 // exchange block layout in granules (host and device agree)
@@ -343,6 +345,7 @@ struct PersistArgs {
     int beam;
     const int32_t *kv_src;       // [B][kv_src_stride] or null
     int kv_src_stride;
+    int q5;                      // GEMVs of phases A, C, G2, H, I read the layers' q5_1 repacks
 };
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G);
 // the inputs whose f32 exp is too close to an f16 midpoint, with their table

@@ -40,6 +40,12 @@
 #pragma clang fp contract(off)
 
 namespace wmi {
+// the q5_1 instances (PersistArgs::q5) are compiled by wmi_persist_q5.hip,
+// which includes this file with WMI_PERSIST_Q5_TU: a second translation unit
+// the build runs in parallel
+hipError_t launch_persist_q5(hipStream_t s, const PersistArgs &a, int G);
+int grid_persist_q5(int device, int n, int B, int V, int *nres);
+
 namespace {
 
 constexpr int PT = 256;                 // threads per workgroup
@@ -155,31 +161,87 @@ __device__ __forceinline__ bool gpoll(int cnt, uint32_t tag, F addr, uint32_t *d
     return ok;
 }
 
+// ---- a weight matrix [N][K] as the GEMVs read it: f16, or (Q5) the q5_1
+// repack of wmi_api.cpp repack_q5 — nibbles of the N*K weights in natural
+// order (two per byte), then per 32-weight block a u32 of 5th bits and a u32
+// {f16 d, f16 m}.  A lane's chunk is 8 consecutive weights: 16 bytes of f16,
+// or 4 nibble bytes + its block's 8-byte word, dequantised at use by
+// q5_half8 to exactly the loader's f16 copy (so both read the same weights).
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+struct WMat {
+    const uint16_t *w;
+    const uint8_t *q;     // nibbles [N * K / 2], or null
+    const u32x2v *qd;     // blocks [N * K / 32]
+};
+__device__ __forceinline__ WMat wmat(const uint16_t *w) { return WMat{w, nullptr, nullptr}; }
+__device__ __forceinline__ WMat wmat(const uint16_t *w, const uint8_t *q, int64_t nk) {
+    return WMat{w, q, (const u32x2v *)(q + nk / 2)};
+}
+// a layer matrix: its q5_1 repack in the Q5 instances, else the f16 weights
+template <bool Q5>
+__device__ __forceinline__ WMat lmat(const uint16_t *w, const uint8_t *q, int64_t nk) {
+    if constexpr (Q5) return wmat(w, q, nk);
+    else return wmat(w);
+}
+template <bool Q5>
+struct WChunk {
+    half8 h;
+};
+template <>
+struct WChunk<true> {
+    uint32_t n;
+    u32x2v hd;
+};
+template <bool Q5>
+__device__ __forceinline__ void wc_zero(WChunk<Q5> &c) {
+    if constexpr (Q5) {
+        c.n = 0u;
+        c.hd = u32x2v{0u, 0u};  // d = m = 0: dequantises to +0
+    } else {
+        c.h = half8{};
+    }
+}
+// weights e .. e + 7 of the matrix (e = row * K + k, k % 8 == 0)
+template <bool Q5>
+__device__ __forceinline__ void wc_load(WChunk<Q5> &c, const WMat &m, int64_t e) {
+    if constexpr (Q5) {
+        c.n = *glb((const uint32_t *)(m.q + e / 2));
+        c.hd = *glb(m.qd + e / 32);
+    } else {
+        c.h = *glb((const half8 *)((const f16 *)m.w + e));
+    }
+}
+// sh = e % 32 (a lane's offset inside its block: (l16 & 3) * 8)
+template <bool Q5>
+__device__ __forceinline__ half8 wc_h8(const WChunk<Q5> &c, int sh) {
+    if constexpr (Q5) return q5_half8(c.n, c.hd[0], c.hd[1], sh);
+    else return c.h;
+}
+
 // ---- GEMV over this workgroup's rows: quarter-wave (16 lanes) per row, row
 // slot = wave * 4 + quarter; pass p covers rows rb + 16 p + slot.  Lane l16
-// holds K chunks c * 128 + l16 * 8 (8 f16 each), the decoder chain's layout.
-template <int KCH, int NP>
+// holds K chunks c * 128 + l16 * 8 (8 weights each), the decoder chain's layout.
+template <int KCH, int NP, bool Q5 = false>
 struct WSet {
-    half8 w[NP][KCH];
+    WChunk<Q5> w[NP][KCH];
     float bias[NP];
 };
 
-template <int KCH, int NP>
-__device__ __forceinline__ void wset_load(WSet<KCH, NP> &S, const uint16_t *W, const float *bias, int K, int rb, int r1,
+template <int KCH, int NP, bool Q5>
+__device__ __forceinline__ void wset_load(WSet<KCH, NP, Q5> &S, const WMat &m, const float *bias, int K, int rb, int r1,
                                           int slot, int l16) {
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         int row = rb + 16 * p + slot;
         const bool ok = row < r1;  // slots past the rows load nothing (zeros)
         row = ok ? row : 0;
-        const f16 *wr = (const f16 *)W + (int64_t)row * K + l16 * 8;
-        const half8 z8 = {};
+        const int64_t e0 = (int64_t)row * K + l16 * 8;
 #pragma unroll
-        for (int c = 0; c < KCH; ++c) S.w[p][c] = z8;
+        for (int c = 0; c < KCH; ++c) wc_zero(S.w[p][c]);
         S.bias[p] = 0.0f;
         if (ok) {  // exec-masked loads straight into the zeroed registers
 #pragma unroll
-            for (int c = 0; c < KCH; ++c) S.w[p][c] = *glb((const half8 *)(wr + c * 128));
+            for (int c = 0; c < KCH; ++c) wc_load(S.w[p][c], m, e0 + c * 128);
             if (bias) S.bias[p] = *glb(bias + row);
         }
     }
@@ -187,29 +249,51 @@ __device__ __forceinline__ void wset_load(WSet<KCH, NP> &S, const uint16_t *W, c
 
 // epi(row, b, v, bias, valid) is called by EVERY lane (pairing shuffles);
 // lane l16 carries the reduced value of row `row` for decoder row b = l16
-template <int BT, int KCH, int NP, typename Epi>
-__device__ __forceinline__ void wset_dot(const WSet<KCH, NP> &S, const f16 *xs, int K, int B, int rb, int r1, int slot,
-                                         int l16, Epi &&epi) {
-    if constexpr (BT == 1 && NP > 1) {
-        // one decoder row: the passes' dot chains and reductions interleaved
-        // (every pass computed — the loads behind them are clamped rows —
-        // and only valid passes reach the epilogue); each sum keeps its order
-        float acc[NP];
+template <int BT, int KCH, int NP, bool Q5, typename Epi>
+__device__ __forceinline__ void wset_dot(const WSet<KCH, NP, Q5> &S, const f16 *xs, int K, int B, int rb, int r1,
+                                         int slot, int l16, Epi &&epi) {
+    const int sh = (l16 & 3) * 8;
+    if constexpr (NP > 1 && BT * KCH <= 32) {
+        // the passes' dot chains and reductions interleaved, each xs chunk
+        // read once for all passes (every pass computed — the loads behind
+        // them are clamped rows — and only valid passes reach the epilogue);
+        // each sum keeps its order.  (BT * KCH <= 32: the compiler hoists
+        // the xs reads of all chunks; more would spill)
+        float acc[NP][BT];
 #pragma unroll
-        for (int p = 0; p < NP; ++p) acc[p] = 0.0f;
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int b = 0; b < BT; ++b) acc[p][b] = 0.0f;
 #pragma unroll
         for (int c = 0; c < KCH; ++c) {
-            const half8 xv = *(const half8 *)(xs + c * 128 + l16 * 8);
+            half8 xv[BT];
 #pragma unroll
-            for (int p = 0; p < NP; ++p) acc[p] = dot8(S.w[p][c], xv, acc[p]);
+            for (int b = 0; b < BT; ++b)
+                if (b < B) xv[b] = *(const half8 *)(xs + b * K + c * 128 + l16 * 8);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                const half8 wv = wc_h8(S.w[p][c], sh);
+#pragma unroll
+                for (int b = 0; b < BT; ++b)
+                    if (b < B) acc[p][b] = dot8(wv, xv[b], acc[p][b]);
+            }
         }
 #pragma unroll
-        for (int p = 0; p < NP; ++p) acc[p] = red16_sum(acc[p]);
+        for (int p = 0; p < NP; ++p) {
+            float v = 0.0f;
+#pragma unroll
+            for (int b = 0; b < BT; ++b)
+                if (b < B) {
+                    const float t = red16_sum(acc[p][b]);
+                    if (l16 == b) v = t;
+                }
+            acc[p][0] = v;
+        }
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
             if (rb + 16 * p >= r1) break;  // workgroup-uniform
             const int row = rb + 16 * p + slot;
-            epi(row, l16, l16 == 0 ? acc[p] : 0.0f, S.bias[p], row < r1 && l16 < 1);
+            epi(row, l16, acc[p][0], S.bias[p], row < r1 && l16 < B);
         }
         return;
     }
@@ -221,10 +305,12 @@ __device__ __forceinline__ void wset_dot(const WSet<KCH, NP> &S, const f16 *xs, 
 #pragma unroll
         for (int b = 0; b < BT; ++b) acc[b] = 0.0f;
 #pragma unroll
-        for (int c = 0; c < KCH; ++c)
+        for (int c = 0; c < KCH; ++c) {
+            const half8 wv = wc_h8(S.w[p][c], sh);
 #pragma unroll
             for (int b = 0; b < BT; ++b)
-                if (b < B) acc[b] = dot8(S.w[p][c], *(const half8 *)(xs + b * K + c * 128 + l16 * 8), acc[b]);
+                if (b < B) acc[b] = dot8(wv, *(const half8 *)(xs + b * K + c * 128 + l16 * 8), acc[b]);
+        }
         float v = 0.0f;
 #pragma unroll
         for (int b = 0; b < BT; ++b)
@@ -242,10 +328,10 @@ __device__ __forceinline__ void wset_dot(const WSet<KCH, NP> &S, const f16 *xs, 
 // row (lane l16 holds c * 128 + l16 * 8 of each, as wset_*), the KS partials
 // added in ks order through LDS.  KS depends on n only (rows per workgroup
 // at the full grid), so a row's sum never depends on the row count B.
-template <int KCH, int KS>
+template <int KCH, int KS, bool Q5 = false>
 struct WSplit {
     static constexpr int CQ = (KCH + KS - 1) / KS;
-    half8 w[CQ];
+    WChunk<Q5> w[CQ];
 };
 // rows per workgroup of an N-row GEMV at the full grid (PX_GMAX), even
 __host__ __device__ constexpr int rows_full(int N) { return (((N + PX_GMAX - 1) / PX_GMAX) + 1) & ~1; }
@@ -257,37 +343,38 @@ __host__ __device__ constexpr int split_of(int kch, int rows) {
     return best;
 }
 
-template <int KCH, int KS>
-__device__ __forceinline__ void wsplit_load(WSplit<KCH, KS> &S, const uint16_t *W, int K, int rb, int r1, int slot,
+template <int KCH, int KS, bool Q5>
+__device__ __forceinline__ void wsplit_load(WSplit<KCH, KS, Q5> &S, const WMat &m, int K, int rb, int r1, int slot,
                                             int l16) {
-    constexpr int CQ = WSplit<KCH, KS>::CQ;
+    constexpr int CQ = WSplit<KCH, KS, Q5>::CQ;
     const int rl = slot / KS, ks = slot - rl * KS, row = rb + rl;
     const bool ok = rl < 16 / KS && row < r1;
-    const f16 *wr = (const f16 *)W + (int64_t)(ok ? row : 0) * K + ks * CQ * 128 + l16 * 8;
-    const half8 z8 = {};
+    const int64_t e0 = (int64_t)(ok ? row : 0) * K + ks * CQ * 128 + l16 * 8;
 #pragma unroll
-    for (int c = 0; c < CQ; ++c) S.w[c] = z8;
+    for (int c = 0; c < CQ; ++c) wc_zero(S.w[c]);
     if (ok) {
 #pragma unroll
-        for (int c = 0; c < CQ; ++c) S.w[c] = *glb((const half8 *)(wr + c * 128));
+        for (int c = 0; c < CQ; ++c) wc_load(S.w[c], m, e0 + c * 128);
     }
 }
 
 // epi(row, b, v, bias, valid) as wset_dot's: called by every lane of the
 // first 16 / KS quarters, quarter q carrying row rb + q (lane l16: decoder row l16)
-template <int BT, int KCH, int KS, typename Epi>
-__device__ __forceinline__ void wsplit_dot(const WSplit<KCH, KS> &S, const f16 *xs, int K, int B, int rb, int r1,
+template <int BT, int KCH, int KS, bool Q5, typename Epi>
+__device__ __forceinline__ void wsplit_dot(const WSplit<KCH, KS, Q5> &S, const f16 *xs, int K, int B, int rb, int r1,
                                            int slot, int l16, float bias, float *kpart, Epi &&epi) {
-    constexpr int CQ = WSplit<KCH, KS>::CQ;
-    const int rl = slot / KS, ks = slot - rl * KS;
+    constexpr int CQ = WSplit<KCH, KS, Q5>::CQ;
+    const int rl = slot / KS, ks = slot - rl * KS, sh = (l16 & 3) * 8;
     float acc[BT];
 #pragma unroll
     for (int b = 0; b < BT; ++b) acc[b] = 0.0f;
 #pragma unroll
-    for (int c = 0; c < CQ; ++c)
+    for (int c = 0; c < CQ; ++c) {
+        const half8 wv = wc_h8(S.w[c], sh);
 #pragma unroll
         for (int b = 0; b < BT; ++b)
-            if (b < B) acc[b] = dot8(S.w[c], *(const half8 *)(xs + b * K + (ks * CQ + c) * 128 + l16 * 8), acc[b]);
+            if (b < B) acc[b] = dot8(wv, *(const half8 *)(xs + b * K + (ks * CQ + c) * 128 + l16 * 8), acc[b]);
+    }
     float v = 0.0f;
 #pragma unroll
     for (int b = 0; b < BT; ++b)
@@ -308,11 +395,11 @@ __device__ __forceinline__ void wsplit_dot(const WSplit<KCH, KS> &S, const f16 *
 }
 
 // a phase's weight set: split-K (KS > 1) or one quarter-wave per row
-template <int KCH, int NP, int KS>
+template <int KCH, int NP, int KS, bool Q5 = false>
 struct GSet {
-    WSplit<KCH, KS> s;
+    WSplit<KCH, KS, Q5> s;
     float bias;
-    __device__ __forceinline__ void load(const uint16_t *W, const float *b, int K, int rb, int r1, int slot, int l16) {
+    __device__ __forceinline__ void load(const WMat &W, const float *b, int K, int rb, int r1, int slot, int l16) {
         wsplit_load(s, W, K, rb, r1, slot, l16);
         bias = 0.0f;
         if (b && slot < 16 / KS && rb + slot < r1) bias = *glb(b + rb + slot);
@@ -323,10 +410,10 @@ struct GSet {
         wsplit_dot<BT>(s, xs, K, B, rb, r1, slot, l16, bias, kpart, epi);
     }
 };
-template <int KCH, int NP>
-struct GSet<KCH, NP, 1> {
-    WSet<KCH, NP> s;
-    __device__ __forceinline__ void load(const uint16_t *W, const float *b, int K, int rb, int r1, int slot, int l16) {
+template <int KCH, int NP, bool Q5>
+struct GSet<KCH, NP, 1, Q5> {
+    WSet<KCH, NP, Q5> s;
+    __device__ __forceinline__ void load(const WMat &W, const float *b, int K, int rb, int r1, int slot, int l16) {
         wset_load(s, W, b, K, rb, r1, slot, l16);
     }
     template <int BT, typename Epi>
@@ -458,7 +545,7 @@ __device__ __forceinline__ float exp_f16_fast(float arg, const uint32_t *fb) {
 // BT: rows at compile time (1) or at most (8, runtime B); BEAM: beam-search
 // launches (self-attention history through kv_src; its index registers stay
 // out of the greedy instances)
-template <int NS, int BT, bool BEAM>
+template <int NS, int BT, bool BEAM, bool Q5>
 __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     constexpr int KC = NS / 128;        // 128-element chunks of a K = n row
     constexpr int H = NS / 64;
@@ -557,9 +644,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 0);
-                GSet<KC, 2, KS_A> S;
+                GSet<KC, 2, KS_A, Q5> S;
                 const bool act = ra0 < ra1;
-                S.load(P.wqkv, P.bqkv, NS, ra0, ra1, slot, l16);
+                S.load(lmat<Q5>(P.wqkv, P.wqkv5, 3 * NS * NS), P.bqkv, NS, ra0, ra1, slot, l16);
                 LnP<NS> lp;
                 ln_params<NS>(P.ln1_w, P.ln1_b, lp, lane);
                 PREFETCH_ISSUED
@@ -765,9 +852,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 2);
-                GSet<KC, 1, KS_N> S;
+                GSet<KC, 1, KS_N, Q5> S;
                 const bool act = rn0 < rn1;
-                S.load(P.wo, P.bo, NS, rn0, rn1, slot, l16);
+                S.load(lmat<Q5>(P.wo, P.wo5, NS * NS), P.bo, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
                 const bool ok = gpoll<PUX>(B * NS / 2, ptag(pos, L, l, 1), ptr_u64(xg + oO), (uint32_t *)xs, abortw, a.err);
@@ -790,7 +877,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 const uint32_t tag = ptag(pos, L, l, 3);
                 GSet<KC, 1, KS_N> S;
                 const bool act = rn0 < rn1;
-                S.load(P.wcq, P.bcq, NS, rn0, rn1, slot, l16);
+                S.load(wmat(P.wcq), P.bcq, NS, rn0, rn1, slot, l16);
                 LnP<NS> lp;
                 ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
                 PREFETCH_ISSUED
@@ -833,7 +920,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         // this head's cross q from x' directly: LNc(x'_b) and
                         // Wcq rows h*64 .. h*64+63, the D phase's arithmetic
                         WSet<KC, 4> S;
-                        wset_load(S, P.wcq, P.bcq, NS, h * 64, h * 64 + 64, slot, l16);
+                        wset_load(S, wmat(P.wcq), P.bcq, NS, h * 64, h * 64 + 64, slot, l16);
                         LnP<NS> lp;
                         ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
                         PREFETCH_ISSUED
@@ -1026,9 +1113,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 7);
-                GSet<KC, 1, KS_N> S;
+                GSet<KC, 1, KS_N, Q5> S;
                 const bool act = rn0 < rn1;
-                S.load(P.wco, P.bco, NS, rn0, rn1, slot, l16);
+                S.load(lmat<Q5>(P.wco, P.wco5, NS * NS), P.bco, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
                 const bool ok = gpoll<PUX>(B * NS / 2, ptag(pos, L, l, 6), ptr_u64(xg + oOC), (uint32_t *)xs, abortw, a.err);
@@ -1048,9 +1135,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 8);
-                GSet<KC, 2, KS_H> S;
+                GSet<KC, 2, KS_H, Q5> S;
                 const bool act = rh0 < rh1;
-                S.load(P.w0, P.b0, NS, rh0, rh1, slot, l16);
+                S.load(lmat<Q5>(P.w0, P.w05, 4 * NS * NS), P.b0, NS, rh0, rh1, slot, l16);
                 LnP<NS> lp;
                 ln_params<NS>(P.ln2_w, P.ln2_b, lp, lane);
                 PREFETCH_ISSUED
@@ -1076,9 +1163,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 9);
-                GSet<4 * KC, 1, KS_I> S;
+                GSet<4 * KC, 1, KS_I, Q5> S;
                 const bool act = rn0 < rn1;
-                S.load(P.w1, P.b1, 4 * NS, rn0, rn1, slot, l16);
+                S.load(lmat<Q5>(P.w1, P.w15, 4 * NS * NS), P.b1, 4 * NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
                 const bool ok = gpoll<PUH>(B * 2 * NS, ptag(pos, L, l, 8), ptr_u64(xg + oH), (uint32_t *)xs, abortw, a.err);
@@ -1102,8 +1189,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PHASE_IDS
             WSet<KC, NPL> S0, S1;
             constexpr int RS = 16 * NPL;  // rows per register set
-            wset_load(S0, a.te, nullptr, NS, rs0, rv1, slot, l16);
-            wset_load(S1, a.te, nullptr, NS, rs0 + RS, rv1, slot, l16);
+            wset_load(S0, wmat(a.te), nullptr, NS, rs0, rv1, slot, l16);
+            wset_load(S1, wmat(a.te), nullptr, NS, rs0 + RS, rv1, slot, l16);
             LnP<NS> lp;
             ln_params<NS>(a.dln_w, a.dln_b, lp, lane);
             PREFETCH_ISSUED
@@ -1122,7 +1209,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)row);
                 best = k > best ? k : best;
             };
-            constexpr int RU = BT == 1 ? 4 : 1;  // row groups interleaved per iteration (one decoder row)
+            // row groups interleaved per iteration; each xs chunk read once for
+            // all (as wset_dot: more than 32 xs chunks in registers would spill)
+            constexpr int RU = BT == 1 || BT * KC <= 32 ? 4 : 1;
             for (int rb = rv0; rb < rs0; rb += 16 * RU) {  // resident rows
                 float acc[RU][BT];
 #pragma unroll
@@ -1131,14 +1220,26 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     for (int b = 0; b < BT; ++b) acc[u][b] = 0.0f;
 #pragma unroll
                 for (int c = 0; c < KC; ++c) {
-#pragma unroll
-                    for (int u = 0; u < RU; ++u) {
-                        const int row = rb + 16 * u + slot;
-                        const f16 *wr = vres + (row < rs0 ? row - rv0 : 0) * NS + l16 * 8;
-                        const half8 wv = *(const half8 *)(wr + c * 128);
+                    if constexpr (RU > 1) {
+                        half8 xv[BT];
 #pragma unroll
                         for (int b = 0; b < BT; ++b)
-                            if (b < B) acc[u][b] = dot8(wv, *(const half8 *)(xs + b * NS + c * 128 + l16 * 8), acc[u][b]);
+                            if (b < B) xv[b] = *(const half8 *)(xs + b * NS + c * 128 + l16 * 8);
+#pragma unroll
+                        for (int u = 0; u < RU; ++u) {
+                            const int row = rb + 16 * u + slot;
+                            const f16 *wr = vres + (row < rs0 ? row - rv0 : 0) * NS + l16 * 8;
+                            const half8 wv = *(const half8 *)(wr + c * 128);
+#pragma unroll
+                            for (int b = 0; b < BT; ++b)
+                                if (b < B) acc[u][b] = dot8(wv, xv[b], acc[u][b]);
+                        }
+                    } else {
+                        const int row = rb + slot;
+                        const half8 wv = *(const half8 *)(vres + (row < rs0 ? row - rv0 : 0) * NS + l16 * 8 + c * 128);
+#pragma unroll
+                        for (int b = 0; b < BT; ++b)
+                            if (b < B) acc[0][b] = dot8(wv, *(const half8 *)(xs + b * NS + c * 128 + l16 * 8), acc[0][b]);
                     }
                 }
 #pragma unroll
@@ -1158,11 +1259,11 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             if (rs0 < rv1)
                 for (int rb = rs0;;) {
                     wset_dot<BT>(S0, xs, NS, B, rb, rv1, slot, l16, epi);
-                    wset_load(S0, a.te, nullptr, NS, rb + 2 * RS, rv1, slot, l16);
+                    wset_load(S0, wmat(a.te), nullptr, NS, rb + 2 * RS, rv1, slot, l16);
                     PREFETCH_ISSUED
                     if (rb + RS >= rv1) break;
                     wset_dot<BT>(S1, xs, NS, B, rb + RS, rv1, slot, l16, epi);
-                    wset_load(S1, a.te, nullptr, NS, rb + 3 * RS, rv1, slot, l16);
+                    wset_load(S1, wmat(a.te), nullptr, NS, rb + 3 * RS, rv1, slot, l16);
                     PREFETCH_ISSUED
                     rb += 2 * RS;
                     if (rb >= rv1) break;
@@ -1205,25 +1306,30 @@ size_t persist_lds(int B) {
 }
 constexpr size_t LDS_CU = 160 * 1024;
 
-template <int NS, int BT, bool BEAM>
+template <int NS, int BT, bool BEAM, bool Q5>
 hipError_t launch_nsb(hipStream_t s, const PersistArgs &a, int G) {
     const size_t lds = persist_lds<NS>(a.B) + (size_t)a.nres * NS * 2;
-    hipError_t e = hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM>,
+    hipError_t e = hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM, Q5>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_dec_persist<NS, BT, BEAM>), dim3(G), dim3(PT), lds, s, a);
+    hipLaunchKernelGGL((k_dec_persist<NS, BT, BEAM, Q5>), dim3(G), dim3(PT), lds, s, a);
     return hipGetLastError();
 }
+#ifndef WMI_PERSIST_Q5_TU
+// beam launches read the f16 copies (the same weights the q5_1 blocks
+// dequantise to); the q5_1 instances live in wmi_persist_q5.hip
 template <int NS>
 hipError_t launch_ns(hipStream_t s, const PersistArgs &a, int G) {
-    if (a.beam) return launch_nsb<NS, PMAXB, true>(s, a, G);
-    return a.B == 1 ? launch_nsb<NS, 1, false>(s, a, G) : launch_nsb<NS, PMAXB, false>(s, a, G);
+    if (a.beam) return launch_nsb<NS, PMAXB, true, false>(s, a, G);
+    if (a.q5) return launch_persist_q5(s, a, G);
+    return a.B == 1 ? launch_nsb<NS, 1, false, false>(s, a, G) : launch_nsb<NS, PMAXB, false, false>(s, a, G);
 }
+#endif
 
-template <int NS, int BT, bool BEAM>
+template <int NS, int BT, bool BEAM, bool Q5>
 int grid_nsb(int device, int B, int V, int *nres) {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void *)k_dec_persist<NS, BT, BEAM>) != hipSuccess) return 0;
+    if (hipFuncGetAttributes(&fa, (const void *)k_dec_persist<NS, BT, BEAM, Q5>) != hipSuccess) return 0;
     const size_t base = persist_lds<NS>(B), avail = LDS_CU - fa.sharedSizeBytes - 1024;
     if (base > avail) return 0;
     // resident vocabulary rows: as many of a workgroup's rows as the LDS holds
@@ -1231,11 +1337,11 @@ int grid_nsb(int device, int B, int V, int *nres) {
     int nr = (int)((avail - base) / (NS * 2));
     *nres = nr < rpw ? nr : rpw;
     const size_t lds = base + (size_t)*nres * NS * 2;
-    if (hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM, Q5>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)
         return 0;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dec_persist<NS, BT, BEAM>, PT, lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dec_persist<NS, BT, BEAM, Q5>, PT, lds) != hipSuccess ||
         per_cu < 1)
         return 0;
     hipDeviceProp_t prop;
@@ -1273,19 +1379,29 @@ __global__ void k_persist_selftest(const uint16_t *tab, int n_exp, const uint32_
     if (got != want) atomicAdd(mismatch, 1u);
 }
 
+// every instance a context may launch at B rows must fit: grid and resident
+// rows are the minimum over them
 template <int NS>
 int grid_ns(int device, int B, int V, int *nres) {
-    if (B == 1) return grid_nsb<NS, 1, false>(device, B, V, nres);
-    // several rows: the beam instance must fit wherever the greedy one does
-    int nb = 0;
-    const int g = grid_nsb<NS, PMAXB, false>(device, B, V, nres);
-    const int gb = grid_nsb<NS, PMAXB, true>(device, B, V, &nb);
-    if (nb < *nres) *nres = nb;
-    return g < gb ? g : gb;
+    int g = PX_GMAX, nr = 1 << 30, ni = 0;
+    auto take = [&](int gi) {
+        g = gi < g ? gi : g;
+        nr = ni < nr ? ni : nr;
+    };
+    if (B == 1) {
+        take(grid_nsb<NS, 1, false, false>(device, B, V, &ni));
+    } else {
+        take(grid_nsb<NS, PMAXB, false, false>(device, B, V, &ni));
+        take(grid_nsb<NS, PMAXB, true, false>(device, B, V, &ni));
+    }
+    take(grid_persist_q5(device, NS, B, V, &ni));
+    *nres = g > 0 ? nr : 0;
+    return g;
 }
 
 }  // namespace
 
+#ifndef WMI_PERSIST_Q5_TU
 hipError_t launch_exp_fallbacks(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *list, uint32_t *n) {
     hipLaunchKernelGGL(k_exp_fallbacks, dim3((0x7c01 + 255) / 256), dim3(256), 0, s, exp_tab, n_exp, list, n);
     return hipGetLastError();
@@ -1326,5 +1442,40 @@ hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G) {
         default: return hipErrorInvalidValue;
     }
 }
+
+#else
+hipError_t launch_persist_q5(hipStream_t s, const PersistArgs &a, int G) {
+#define WMI_Q5_LAUNCH(NS) \
+    case NS: \
+        return a.B == 1 ? launch_nsb<NS, 1, false, true>(s, a, G) : launch_nsb<NS, PMAXB, false, true>(s, a, G);
+    switch (a.n) {
+        WMI_Q5_LAUNCH(128)
+        WMI_Q5_LAUNCH(384)
+        WMI_Q5_LAUNCH(512)
+        WMI_Q5_LAUNCH(768)
+        WMI_Q5_LAUNCH(1024)
+        WMI_Q5_LAUNCH(1280)
+        default: return hipErrorInvalidValue;
+    }
+#undef WMI_Q5_LAUNCH
+}
+
+int grid_persist_q5(int device, int n, int B, int V, int *nres) {
+#define WMI_Q5_GRID(NS) \
+    case NS: \
+        return B == 1 ? grid_nsb<NS, 1, false, true>(device, B, V, nres) \
+                      : grid_nsb<NS, PMAXB, false, true>(device, B, V, nres);
+    switch (n) {
+        WMI_Q5_GRID(128)
+        WMI_Q5_GRID(384)
+        WMI_Q5_GRID(512)
+        WMI_Q5_GRID(768)
+        WMI_Q5_GRID(1024)
+        WMI_Q5_GRID(1280)
+        default: return 0;
+    }
+#undef WMI_Q5_GRID
+}
+#endif
 
 }  // namespace wmi
