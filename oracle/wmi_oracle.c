@@ -107,6 +107,34 @@ static inline float dot_f16(int n, const uint16_t *x, const uint16_t *y) {
     return (float)sumf;
 }
 
+/* ggml_vec_dot_f32 (same AVX2/FMA build): the f16 dot's accumulator layout
+ * and reduction over f32 operands, neither rounded (f32 x f32 mul_mat of
+ * ftype-0 files, main.rs:817-821) */
+static inline float dot_f32(int n, const float *x, const float *y) {
+    if (__builtin_expect(g_dot_double, 0)) {
+        double s = 0.0;
+        for (int i = 0; i < n; ++i) s += (double)x[i] * (double)y[i];
+        return (float)s;
+    }
+    const int np = n & ~31;
+    __m256 s0 = _mm256_setzero_ps(), s1 = _mm256_setzero_ps();
+    __m256 s2 = _mm256_setzero_ps(), s3 = _mm256_setzero_ps();
+    for (int i = 0; i < np; i += 32) {
+        s0 = _mm256_fmadd_ps(_mm256_loadu_ps(x + i), _mm256_loadu_ps(y + i), s0);
+        s1 = _mm256_fmadd_ps(_mm256_loadu_ps(x + i + 8), _mm256_loadu_ps(y + i + 8), s1);
+        s2 = _mm256_fmadd_ps(_mm256_loadu_ps(x + i + 16), _mm256_loadu_ps(y + i + 16), s2);
+        s3 = _mm256_fmadd_ps(_mm256_loadu_ps(x + i + 24), _mm256_loadu_ps(y + i + 24), s3);
+    }
+    s0 = _mm256_add_ps(s0, s1);
+    s2 = _mm256_add_ps(s2, s3);
+    s0 = _mm256_add_ps(s0, s2);
+    __m128 t0 = _mm_add_ps(_mm256_castps256_ps128(s0), _mm256_extractf128_ps(s0, 1));
+    __m128 t1 = _mm_hadd_ps(t0, t0);
+    double sumf = _mm_cvtss_f32(_mm_hadd_ps(t1, t1));
+    for (int i = np; i < n; ++i) sumf += (double)(x[i] * y[i]);
+    return (float)sumf;
+}
+
 /* ------------------------------------------------------------------------ */
 /* model                                                                     */
 /* ------------------------------------------------------------------------ */
@@ -142,6 +170,7 @@ enum { HP_N_VOCAB, HP_N_AUDIO_CTX, HP_N_AUDIO_STATE, HP_N_AUDIO_HEAD, HP_N_AUDIO
 
 struct or_model {
     int32_t hp[11];
+    int wf32; /* ftype 0 file: the uint16_t matrix pointers below address f32 arrays */
     int32_t n_filt_mel, n_filt_ff;
     float *filters;
     int32_t sp[9]; /* eot sot prev solm not beg translate transcribe multilingual */
@@ -522,7 +551,7 @@ int or_load(const char *path, or_model **out, char *err, size_t errcap) {
         }
         {
             const int ft = hp[HP_F16] % 1000, qv = hp[HP_F16] / 1000;
-            const int ok = ft == 1 || ((ft == 2 || ft == 3 || ft == 7 || ft == 8 || ft == 9) && qv == 2);
+            const int ok = ft == 0 || ft == 1 || ((ft == 2 || ft == 3 || ft == 7 || ft == 8 || ft == 9) && qv == 2);
             if (!ok) {
                 set_err(err, errcap, "model ftype %d (hparams.f16 = %d) is not supported by this build", ft, hp[HP_F16]);
                 rc = WMI_E_UNSUPPORTED;
@@ -532,6 +561,7 @@ int or_load(const char *path, or_model **out, char *err, size_t errcap) {
     }
     free(reg);
     fclose(f);
+    m->wf32 = m->hp[HP_F16] % 1000 == 0;
     *out = m;
     return WMI_OK;
 fail:
@@ -747,6 +777,21 @@ static void matmul_f16(int M, int N, int K, const uint16_t *W, const uint16_t *x
         }
 }
 
+/* ggml_mul_mat(W f32 [N][K], x f32 [M][K]): no rounding of either operand */
+static void matmul_f32(int M, int N, int K, const float *W, const float *x, float *y, int nt) {
+    const int OB = 16;
+    const int nob = (N + OB - 1) / OB;
+#pragma omp parallel for num_threads(nt) schedule(dynamic, 1) collapse(2)
+    for (int ob = 0; ob < nob; ++ob)
+        for (int tb = 0; tb < (M + 63) / 64; ++tb) {
+            const int o1 = (ob + 1) * OB < N ? (ob + 1) * OB : N;
+            const int t1 = (tb + 1) * 64 < M ? (tb + 1) * 64 : M;
+            for (int t = tb * 64; t < t1; ++t)
+                for (int o = ob * OB; o < o1; ++o)
+                    y[(int64_t)t * N + o] = dot_f32(K, W + (int64_t)o * K, x + (int64_t)t * K);
+        }
+}
+
 static void to_f16(int64_t n, const float *x, uint16_t *y) {
     for (int64_t i = 0; i < n; ++i) y[i] = f2h(x[i]);
 }
@@ -770,6 +815,27 @@ static void conv1d(int C, int O, int Tin, int stride, const uint16_t *W, const u
             float acc = 0.0f;
             for (int k = 0; k < 3; ++k)
                 acc += dot_f16(Cp, wk + ((size_t)o * 3 + k) * Cp, xs_tm + (size_t)(t * stride + k) * Cp);
+            y[(size_t)o * Tout + t] = acc;
+        }
+    free(wk);
+}
+
+/* ggml_compute_forward_conv_1d_{1s,2s}_f32: the same kernel / source layout
+ * in f32 (ftype-0 files), ggml_vec_dot_f32 per tap */
+static void conv1d_f32(int C, int O, int Tin, int stride, const float *W, const float *xs_tm /*[Tin+2][Cp]*/,
+                       float *y /*[O][Tout]*/, int nt) {
+    const int Cp = (C + 31) & ~31;
+    const int Tout = Tin / stride;
+    float *wk = calloc((size_t)O * 3 * Cp, 4);
+    for (int o = 0; o < O; ++o)
+        for (int c = 0; c < C; ++c)
+            for (int k = 0; k < 3; ++k) wk[((size_t)o * 3 + k) * Cp + c] = W[((size_t)o * C + c) * 3 + k];
+#pragma omp parallel for num_threads(nt) schedule(static)
+    for (int o = 0; o < O; ++o)
+        for (int t = 0; t < Tout; ++t) {
+            float acc = 0.0f;
+            for (int k = 0; k < 3; ++k)
+                acc += dot_f32(Cp, wk + ((size_t)o * 3 + k) * Cp, xs_tm + (size_t)(t * stride + k) * Cp);
             y[(size_t)o * Tout + t] = acc;
         }
     free(wk);
@@ -810,26 +876,43 @@ int or_encode(const or_model *m, const float *mel, int32_t n_len, int mel_offset
     const int T2 = 2 * n_ctx, T = n_ctx;
     const int Cp = (C + 31) & ~31;
 
-    /* mel window (main.rs:1816-1833) -> f16 time-major padded conv input */
+    /* f32 (ftype 0) files: f32 kernels / matrices, nothing rounded to f16
+     * before a conv or matmul (ggml's *_f32 forward paths) */
+    const int f32 = m->wf32;
+    /* mel window (main.rs:1816-1833) -> f16 (f32) time-major padded conv input */
     uint16_t *xs = calloc((size_t)(T2 + 2) * Cp, 2);
+    float *xs32 = f32 ? calloc((size_t)(T2 + 2) * Cp, 4) : NULL;
     {
         const int64_t i0 = mel_offset < n_len ? mel_offset : n_len;
         const int64_t i1 = (int64_t)mel_offset + T2 < n_len ? (int64_t)mel_offset + T2 : n_len;
         for (int c = 0; c < C; ++c)
-            for (int64_t i = i0; i < i1; ++i) xs[(size_t)(i - i0 + 1) * Cp + c] = f2h(mel[(int64_t)c * n_len + i]);
+            for (int64_t i = i0; i < i1; ++i) {
+                const float v = mel[(int64_t)c * n_len + i];
+                xs[(size_t)(i - i0 + 1) * Cp + c] = f2h(v);
+                if (f32) xs32[(size_t)(i - i0 + 1) * Cp + c] = v;
+            }
     }
     /* conv1 + bias + gelu (main.rs:1834-1855) */
     float *y1 = malloc(sizeof(float) * (size_t)n * T2);
-    conv1d(C, n, T2, 1, m->conv1_w, xs, y1, nt);
+    if (f32) conv1d_f32(C, n, T2, 1, (const float *)m->conv1_w, xs32, y1, nt);
+    else conv1d(C, n, T2, 1, m->conv1_w, xs, y1, nt);
     free(xs);
+    free(xs32);
     uint16_t *g1 = calloc((size_t)(T2 + 2) * n, 2);
+    float *g1f = f32 ? calloc((size_t)(T2 + 2) * n, 4) : NULL; /* the same (f16 table) values in f32 */
     for (int o = 0; o < n; ++o)
-        for (int t = 0; t < T2; ++t) g1[(size_t)(t + 1) * n + o] = f2h(gelu_f16(m->conv1_b[o] + y1[(size_t)o * T2 + t]));
+        for (int t = 0; t < T2; ++t) {
+            const float gv = gelu_f16(m->conv1_b[o] + y1[(size_t)o * T2 + t]);
+            g1[(size_t)(t + 1) * n + o] = f2h(gv);
+            if (f32) g1f[(size_t)(t + 1) * n + o] = gv;
+        }
     free(y1);
     /* conv2 + bias + gelu (main.rs:1856-1860) */
     float *y2 = malloc(sizeof(float) * (size_t)n * T);
-    conv1d(n, n, T2, 2, m->conv2_w, g1, y2, nt);
+    if (f32) conv1d_f32(n, n, T2, 2, (const float *)m->conv2_w, g1f, y2, nt);
+    else conv1d(n, n, T2, 2, m->conv2_w, g1, y2, nt);
     free(g1);
+    free(g1f);
     /* + positional embedding, transposed (main.rs:1862-1875) */
     float *h = malloc(sizeof(float) * (size_t)T * n);
     for (int t = 0; t < T; ++t)
@@ -853,11 +936,17 @@ int or_encode(const or_model *m, const float *mel, int32_t n_len, int mel_offset
         /* attn_ln (main.rs:1881-1887) */
 #pragma omp parallel for num_threads(nt)
         for (int t = 0; t < T; ++t) layer_norm_row(n, h + (size_t)t * n, e->attn_ln_w, e->attn_ln_b, xln + (size_t)t * n);
-        to_f16((int64_t)T * n, xln, x16);
         /* Q, K, V (main.rs:1891-1897) */
-        matmul_f16(T, n, n, e->q_w, x16, q, nt);
-        matmul_f16(T, n, n, e->k_w, x16, k, nt);
-        matmul_f16(T, n, n, e->v_w, x16, v, nt);
+        if (f32) {
+            matmul_f32(T, n, n, (const float *)e->q_w, xln, q, nt);
+            matmul_f32(T, n, n, (const float *)e->k_w, xln, k, nt);
+            matmul_f32(T, n, n, (const float *)e->v_w, xln, v, nt);
+        } else {
+            to_f16((int64_t)T * n, xln, x16);
+            matmul_f16(T, n, n, e->q_w, x16, q, nt);
+            matmul_f16(T, n, n, e->k_w, x16, k, nt);
+            matmul_f16(T, n, n, e->v_w, x16, v, nt);
+        }
         for (int t = 0; t < T; ++t)
             for (int c = 0; c < n; ++c) {
                 const size_t i = (size_t)t * n + c;
@@ -880,8 +969,12 @@ int or_encode(const or_model *m, const float *mel, int32_t n_len, int mel_offset
             free(S16);
         }
         /* out-projection + residual (main.rs:1935-1942) */
-        to_f16((int64_t)T * n, att, x16);
-        matmul_f16(T, n, n, e->o_w, x16, y, nt);
+        if (f32) {
+            matmul_f32(T, n, n, (const float *)e->o_w, att, y, nt);
+        } else {
+            to_f16((int64_t)T * n, att, x16);
+            matmul_f16(T, n, n, e->o_w, x16, y, nt);
+        }
         for (int t = 0; t < T; ++t)
             for (int c = 0; c < n; ++c) {
                 const size_t i = (size_t)t * n + c;
@@ -890,14 +983,20 @@ int or_encode(const or_model *m, const float *mel, int32_t n_len, int mel_offset
         /* MLP (main.rs:1945-1968) */
 #pragma omp parallel for num_threads(nt)
         for (int t = 0; t < T; ++t) layer_norm_row(n, h + (size_t)t * n, e->mlp_ln_w, e->mlp_ln_b, xln + (size_t)t * n);
-        to_f16((int64_t)T * n, xln, x16);
-        matmul_f16(T, 4 * n, n, e->mlp0_w, x16, y, nt);
-        for (int t = 0; t < T; ++t)
-            for (int c = 0; c < 4 * n; ++c) {
-                const size_t i = (size_t)t * 4 * n + c;
-                x16[i] = f2h(gelu_f16(e->mlp0_b[c] + y[i]));
-            }
-        matmul_f16(T, n, 4 * n, e->mlp1_w, x16, y, nt);
+        if (f32) {
+            matmul_f32(T, 4 * n, n, (const float *)e->mlp0_w, xln, y, nt);
+            for (size_t i = 0; i < (size_t)T * 4 * n; ++i) xln[i] = gelu_f16(e->mlp0_b[i % (4 * n)] + y[i]);
+            matmul_f32(T, n, 4 * n, (const float *)e->mlp1_w, xln, y, nt);
+        } else {
+            to_f16((int64_t)T * n, xln, x16);
+            matmul_f16(T, 4 * n, n, e->mlp0_w, x16, y, nt);
+            for (int t = 0; t < T; ++t)
+                for (int c = 0; c < 4 * n; ++c) {
+                    const size_t i = (size_t)t * 4 * n + c;
+                    x16[i] = f2h(gelu_f16(e->mlp0_b[c] + y[i]));
+                }
+            matmul_f16(T, n, 4 * n, e->mlp1_w, x16, y, nt);
+        }
         for (int t = 0; t < T; ++t)
             for (int c = 0; c < n; ++c) {
                 const size_t i = (size_t)t * n + c;
@@ -917,8 +1016,13 @@ int or_encode(const or_model *m, const float *mel, int32_t n_len, int mel_offset
         to_f16((int64_t)T * n, enc_out, x16);
         for (int l = 0; l < Lt; ++l) {
             const dec_layer *d = &m->dec[l];
-            matmul_f16(T, n, n, d->ck_w, x16, k, nt);
-            matmul_f16(T, n, n, d->cv_w, x16, v, nt);
+            if (f32) {
+                matmul_f32(T, n, n, (const float *)d->ck_w, enc_out, k, nt);
+                matmul_f32(T, n, n, (const float *)d->cv_w, enc_out, v, nt);
+            } else {
+                matmul_f16(T, n, n, d->ck_w, x16, k, nt);
+                matmul_f16(T, n, n, d->cv_w, x16, v, nt);
+            }
             uint16_t *ko = cross_k + (size_t)l * T * n, *vo = cross_v + (size_t)l * T * n;
             for (int t = 0; t < T; ++t)
                 for (int c = 0; c < n; ++c) {
@@ -941,6 +1045,7 @@ typedef struct {
     uint16_t *mk, *mv; /* [L][n_text_ctx][n] f16 */
     float *x, *xl, *buf, *att, *logits_tmp;
     uint16_t *x16, *h16;
+    float *h32; /* f32 files: the MLP hidden row (GELU table values) */
     float *S;
     uint16_t *S16, *vcol;
 } dec_state;
@@ -975,49 +1080,59 @@ static void gemv_f16(int N, int K, const uint16_t *W, const uint16_t *x16, float
     for (int o = 0; o < N; ++o) y[o] = dot_f16(K, W + (int64_t)o * K, x16);
 }
 
+/* y = W x for the model's matrix type: f16 rows against f16(x) (x16 is
+ * filled here), or f32 rows against x unrounded (ftype-0 files) */
+static void gemv_w(const or_model *m, int N, int K, const uint16_t *W, const float *x, uint16_t *x16, float *y, int nt) {
+    if (m->wf32) {
+        const float *W32 = (const float *)W;
+#pragma omp parallel for num_threads(nt) schedule(static)
+        for (int o = 0; o < N; ++o) y[o] = dot_f32(K, W32 + (int64_t)o * K, x);
+        return;
+    }
+    to_f16(K, x, x16);
+    gemv_f16(N, K, W, x16, y, nt);
+}
+
 static void dec_step(const or_model *m, dec_state *st, const uint16_t *cross_k, const uint16_t *cross_v, int n_ctx,
                      int32_t tok, int pos, float *logits, int nt) {
     const int n = st->n, H = st->H, D = st->D;
     const float sc = powf((float)n / (float)H, -0.25f);
     float *x = st->x, *xl = st->xl, *buf = st->buf, *att = st->att;
-    for (int c = 0; c < n; ++c) x[c] = h2f(m->d_te[(int64_t)tok * n + c]) + m->d_pe[(int64_t)pos * n + c];
+    for (int c = 0; c < n; ++c) {
+        const float te = m->wf32 ? ((const float *)m->d_te)[(int64_t)tok * n + c] : h2f(m->d_te[(int64_t)tok * n + c]);
+        x[c] = te + m->d_pe[(int64_t)pos * n + c];
+    }
     for (int l = 0; l < st->L; ++l) {
         const dec_layer *d = &m->dec[l];
         uint16_t *mk = st->mk + (size_t)l * st->n_text_ctx * n, *mv = st->mv + (size_t)l * st->n_text_ctx * n;
         /* self-attention */
         layer_norm_row(n, x, d->attn_ln_w, d->attn_ln_b, xl);
-        to_f16(n, xl, st->x16);
-        gemv_f16(n, n, d->q_w, st->x16, buf, nt);
+        gemv_w(m, n, n, d->q_w, xl, st->x16, buf, nt);
         for (int c = 0; c < n; ++c) st->h16[c] = f2h((d->q_b[c] + buf[c]) * sc);
-        gemv_f16(n, n, d->k_w, st->x16, buf, nt);
+        gemv_w(m, n, n, d->k_w, xl, st->x16, buf, nt);
         for (int c = 0; c < n; ++c) mk[(size_t)pos * n + c] = f2h(buf[c] * sc);
-        gemv_f16(n, n, d->v_w, st->x16, buf, nt);
+        gemv_w(m, n, n, d->v_w, xl, st->x16, buf, nt);
         for (int c = 0; c < n; ++c) mv[(size_t)pos * n + c] = f2h(d->v_b[c] + buf[c]);
         for (int hh = 0; hh < H; ++hh) dec_attn_head(D, pos + 1, st->h16 + hh * D, mk + hh * D, mv + hh * D, n, st, att + hh * D);
-        to_f16(n, att, st->x16);
-        gemv_f16(n, n, d->o_w, st->x16, buf, nt);
+        gemv_w(m, n, n, d->o_w, att, st->x16, buf, nt);
         for (int c = 0; c < n; ++c) x[c] = (d->o_b[c] + buf[c]) + x[c];
         /* cross-attention over memory_cross_k/v[l] */
         layer_norm_row(n, x, d->cattn_ln_w, d->cattn_ln_b, xl);
-        to_f16(n, xl, st->x16);
-        gemv_f16(n, n, d->cq_w, st->x16, buf, nt);
+        gemv_w(m, n, n, d->cq_w, xl, st->x16, buf, nt);
         for (int c = 0; c < n; ++c) st->h16[c] = f2h((d->cq_b[c] + buf[c]) * sc);
         const uint16_t *ck = cross_k + (size_t)l * n_ctx * n, *cv = cross_v + (size_t)l * n_ctx * n;
         for (int hh = 0; hh < H; ++hh) dec_attn_head(D, n_ctx, st->h16 + hh * D, ck + hh * D, cv + hh * D, n, st, att + hh * D);
-        to_f16(n, att, st->x16);
-        gemv_f16(n, n, d->co_w, st->x16, buf, nt);
+        gemv_w(m, n, n, d->co_w, att, st->x16, buf, nt);
         for (int c = 0; c < n; ++c) x[c] = (d->co_b[c] + buf[c]) + x[c];
         /* MLP */
         layer_norm_row(n, x, d->mlp_ln_w, d->mlp_ln_b, xl);
-        to_f16(n, xl, st->x16);
-        gemv_f16(4 * n, n, d->mlp0_w, st->x16, buf, nt);
-        for (int c = 0; c < 4 * n; ++c) st->x16[c] = f2h(gelu_f16(d->mlp0_b[c] + buf[c]));
-        gemv_f16(n, 4 * n, d->mlp1_w, st->x16, buf, nt);
+        gemv_w(m, 4 * n, n, d->mlp0_w, xl, st->x16, buf, nt);
+        for (int c = 0; c < 4 * n; ++c) st->h32[c] = gelu_f16(d->mlp0_b[c] + buf[c]);
+        gemv_w(m, n, 4 * n, d->mlp1_w, st->h32, st->x16, buf, nt);
         for (int c = 0; c < n; ++c) x[c] = (d->mlp1_b[c] + buf[c]) + x[c];
     }
     layer_norm_row(n, x, m->d_ln_w, m->d_ln_b, xl);
-    to_f16(n, xl, st->x16);
-    gemv_f16(st->V, n, m->d_te, st->x16, logits, nt);
+    gemv_w(m, st->V, n, m->d_te, xl, st->x16, logits, nt);
 }
 
 static int dec_init(const or_model *m, dec_state *st, int n_ctx) {
@@ -1037,6 +1152,7 @@ static int dec_init(const or_model *m, dec_state *st, int n_ctx) {
     st->xl = malloc(sizeof(float) * n);
     st->buf = malloc(sizeof(float) * 4 * n);
     st->att = malloc(sizeof(float) * n);
+    st->h32 = malloc(sizeof(float) * 4 * n);
     st->x16 = malloc(2 * 4 * n);
     st->h16 = malloc(2 * n);
     st->S = malloc(sizeof(float) * maxM);
@@ -1047,7 +1163,7 @@ static int dec_init(const or_model *m, dec_state *st, int n_ctx) {
 
 static void dec_fini(dec_state *st) {
     free(st->mk); free(st->mv); free(st->x); free(st->xl); free(st->buf); free(st->att);
-    free(st->x16); free(st->h16); free(st->S); free(st->S16); free(st->vcol);
+    free(st->x16); free(st->h16); free(st->h32); free(st->S); free(st->S16); free(st->vcol);
 }
 
 int or_decode_logits(const or_model *m, const uint16_t *cross_k, const uint16_t *cross_v, int n_ctx,

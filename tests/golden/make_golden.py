@@ -19,6 +19,8 @@ Restated items (file:line into /root/reference/src/main.rs):
   decoder  SURVEY §A.7 (absent from the reference)
 
 Run:  python tests/golden/make_golden.py   (writes tests/golden/micro_golden.npz)
+      python tests/golden/make_golden.py --f32   (micro_f32_golden.npz: the
+      same model as an f32 / ftype-0 file, whose matmuls round nothing)
 """
 from __future__ import annotations
 
@@ -123,8 +125,10 @@ def layer_norm(x, w, b):
 
 
 def matmul(W, x):
-    """ggml_mul_mat(W f16 [out][in], x): x rounded to f16, exact products."""
-    return f16(x) @ W.astype(np.float64).T
+    """ggml_mul_mat(W [out][in], x), exact products: an f16 W rounds x to f16;
+    an f32 W (ftype-0 file, main.rs:817-821) takes x as it is."""
+    xx = f16(x) if W.dtype == np.float16 else np.asarray(x, np.float64)
+    return xx @ W.astype(np.float64).T
 
 
 def attention(q, k, v, scale):
@@ -140,7 +144,8 @@ def encode(hp, T, mel):
     D = n // H
     X = np.zeros((hp["n_mels"], 2 * N_CTX))
     X[:, :min(2 * N_CTX, mel.shape[1])] = mel[:, :2 * N_CTX]
-    xp = np.pad(f16(X), ((0, 0), (1, 1)))
+    # conv_1d_*_f16_f32 rounds its source to f16; the f32 kernel does not
+    xp = np.pad(f16(X) if T["encoder.conv1.weight"].dtype == np.float16 else X, ((0, 0), (1, 1)))
 
     def conv(W, b, x, stride):
         Tout = (x.shape[1] - 2) // stride
@@ -228,11 +233,12 @@ def greedy(hp, T, ck, cv, n_tok):
     return np.array(toks[np_:], np.int32), np.array(margins)
 
 
-def main(out_path=os.path.join(HERE, "micro_golden.npz")):
+def main(out_path=os.path.join(HERE, "micro_golden.npz"), quant=None):
+    """quant "f32": the micro model as an ftype-0 (f32) file -> micro_f32_golden.npz"""
     import tempfile
     with tempfile.TemporaryDirectory() as d:
         mpath = os.path.join(d, "micro.bin")
-        synth.write_ggml(mpath, "micro")
+        synth.write_ggml(mpath, "micro", quant=quant)
         sha = hashlib.sha256(open(mpath, "rb").read()).hexdigest()
         hp, filters, T = read_ggml(mpath)
     pcm = synth.synth_pcm_f32(SECONDS, SEED)
@@ -250,4 +256,7 @@ def main(out_path=os.path.join(HERE, "micro_golden.npz")):
 
 
 if __name__ == "__main__":
-    main()
+    if "--f32" in sys.argv:
+        main(os.path.join(HERE, "micro_f32_golden.npz"), quant="f32")
+    else:
+        main()

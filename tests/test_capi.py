@@ -115,17 +115,25 @@ def test_bad_magic_and_truncation(tmp_path, micro_model):
         wmi.WhisperContext.new(os.path.join(str(tmp_path), "does-not-exist.bin"))
 
 
-def test_f32_model_is_reported_unsupported(tmp_path):
-    path = os.path.join(str(tmp_path), "f32.bin")
-    hp = dict(synth.MODEL_DIMS["micro"], f16=0)
-    # f16 = 0: every matrix is expected as f32 (main.rs:817-821)
+def test_f32_model_parses(tmp_path):
+    """ftype-0 files load (main.rs:817-821, 1423-1427: every matrix f32): the
+    host parse passes and only device init remains; an f16 record in such a
+    file is a wrong-bytes error, as in the reference's record loop."""
     path = _write_variant(str(tmp_path), "f32.bin",
                           lambda n, ne, ft, p: (n, ne, 0, np.frombuffer(p, "<f2").astype("<f4").tobytes()) if ft else (n, ne, ft, p))
     raw = bytearray(open(path, "rb").read())
     raw[4 + 40:4 + 44] = struct.pack("<i", 0)
     open(path, "wb").write(raw)
-    with pytest.raises(wmi.Unsupported):
-        wmi.WhisperContext.new(path)
+    try:
+        wmi.WhisperContext.new(path).close()
+    except wmi.HipError as e:
+        assert "no HIP device" in str(e)
+    pyoracle.OracleModel(path).close()
+    mixed = os.path.join(str(tmp_path), "mixed.bin")
+    data = open(_write_variant(str(tmp_path), "f16.bin", lambda *r: r), "rb").read()
+    open(mixed, "wb").write(data[:44] + struct.pack("<i", 0) + data[48:])
+    with pytest.raises(wmi.WrongBytesTensor):
+        wmi.WhisperContext.new(mixed)
 
 
 def test_valid_model_reaches_device_init(micro_model):

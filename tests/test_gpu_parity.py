@@ -595,3 +595,29 @@ def test_reference_checksums(wmi, micro_model, oracle_micro):
             assert abs(got[k] - ref[k]) <= 2e-6 * n + 1e-5 * abs(ref[k]), (k, got[k], ref[k])
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("model,n_ctx,secs", [("micro-f32", 64, 2.0), ("tiny.en-f32", 1500, 30.0)])
+def test_f32_model(wmi, model_cache, model, n_ctx, secs):
+    """ftype-0 (f32) files (main.rs:817-821, 1423-1427): f32 MFMA GEMMs for the
+    conv stem / encoder / cross K/V and f32 decoder GEMVs, neither operand
+    rounded to f16 (wmi_f32.hip), held to the oracle's f32 path: the encoder
+    bar, greedy ids over every decisive step, teacher-forced logits, beam K=2."""
+    path = synth.model_path(model, model_cache)
+    om = pyoracle.OracleModel(path)
+    ctx = wmi.WhisperContext.new(path, 0, max_clips=1)
+    try:
+        assert om.hp["f16"] == 0
+        _, seed, (_, ck_ref, cv_ref), pcm, ref = _greedy_case(ctx, om, range(99, 129), 16, n_ctx, secs, min_len=12)
+        toks = np.array(om.prompt() + list(ref[:8]), np.int32)
+        lref = om.decode_logits(ck_ref, cv_ref, toks, n_threads=threads())
+        err = np.abs(ctx.decode_logits(toks, 0) - lref).max()
+        print(f"[f32 parity] {model}: teacher-forced logits max err {err:.3e}")
+        assert err <= 2e-3, err
+        if model == "micro-f32":
+            bref, score, got, got_score = _beam_case(ctx, om, range(100, 130), 2, 12, True)
+            np.testing.assert_array_equal(got, bref)
+            assert abs(got_score - score) < 1e-2
+    finally:
+        ctx.close()
+        om.close()

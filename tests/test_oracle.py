@@ -61,6 +61,32 @@ def test_oracle_decoder_vs_golden(oracle_micro, golden):
     np.testing.assert_array_equal(toks, golden["greedy"])
 
 
+def test_oracle_f32_model_vs_golden(model_cache):
+    """ftype-0 (f32) files (main.rs:817-821, 1423-1427): f32 conv / matmul
+    operands never rounded to f16, pinned against the NumPy restatement of the
+    same file (tests/golden/micro_f32_golden.npz)."""
+    g = np.load(os.path.join(ROOT, "tests", "golden", "micro_f32_golden.npz"))
+    path = synth.model_path("micro-f32", model_cache)
+    assert hashlib.sha256(open(path, "rb").read()).hexdigest() == str(g["model_sha256"])
+    om = pyoracle.OracleModel(path)
+    try:
+        assert om.hp["f16"] == 0
+        mel = om.mel(synth.synth_pcm_f32(2.0, 1234))
+        assert np.abs(mel - g["mel"]).max() < 5e-4
+        enc, ck, cv = om.encode(mel, n_ctx=int(g["n_ctx"]), n_threads=threads())
+        assert np.abs(enc - g["enc"]).max() < 1e-3
+        assert np.abs(enc - g["enc"]).mean() < 1e-4
+        assert np.abs(f16(ck) - g["ck"].astype(np.float32)).max() <= 1e-3
+        assert np.abs(f16(cv) - g["cv"].astype(np.float32)).max() <= 1e-3
+        lg = om.decode_logits(ck, cv, g["tf_tokens"], n_threads=threads())
+        np.testing.assert_array_equal(np.argsort(-lg, axis=1, kind="stable")[:, :5], g["tf_top5"])
+        assert np.abs(np.take_along_axis(lg, g["tf_top5"], 1) - g["tf_top5_logits"]).max() < 2e-3
+        toks, _ = om.decode_greedy(ck, cv, len(g["greedy"]), suppress_eot=True, n_threads=threads())
+        np.testing.assert_array_equal(toks, g["greedy"])
+    finally:
+        om.close()
+
+
 def test_tables():
     gelu, expt = pyoracle.tables()
     h = lambda x: np.float16(x).view(np.uint16)

@@ -143,6 +143,8 @@ struct HostTensor {
     const uint16_t *f16() const { return (const uint16_t *)data.data(); }
 };
 
+// f32 models (wmi_context::wf32): the matrix pointers below address f32 arrays
+// (ggml ftype 0 keeps them unrounded); the f32 kernels read them as such
 struct EncLayerDev {
     float *ln1_w, *ln1_b;
     uint16_t *wqkv; float *bqkv;
@@ -192,6 +194,7 @@ struct wmi_context {
     uint16_t *te = nullptr;
     const uint8_t *te5 = nullptr;  // q5_1 token embedding for the logits GEMV (q5_1 models)
     bool use_q5 = true;            // WMI_NO_Q5=1: decoder GEMVs read the dequantised f16 copies
+    bool wf32 = false;             // ggml ftype 0 file: f32 matrices, f32 GEMM / GEMV kernels (wmi_f32.hip)
     float *d_pe = nullptr, *dln_w = nullptr, *dln_b = nullptr;
     std::vector<DecLayerDev> dec;
     // workspace
@@ -202,6 +205,7 @@ struct wmi_context {
     uint16_t *att = nullptr, *hid = nullptr, *enc16 = nullptr, *ck = nullptr, *cv = nullptr;
     uint16_t *kcache = nullptr, *vcache = nullptr;
     float *h = nullptr, *enc32 = nullptr;
+    float *xconv32 = nullptr, *xln32 = nullptr, *att32 = nullptr;  // f32 models: unrounded matmul inputs
     // decoder small state
     float *dx = nullptr, *dlogits = nullptr;
     uint16_t *dq16 = nullptr, *datt16 = nullptr, *dhid16 = nullptr;
@@ -580,7 +584,7 @@ int parse_file(const char *path, ParsedModel &pm, std::string &err) {
     }
     {
         const int ft = hp.f16 % 1000, qv = hp.f16 / 1000;
-        const bool ok = ft == 1 || ((ft == 2 || ft == 3 || ft == 7 || ft == 8 || ft == 9) && qv == 2);
+        const bool ok = ft == 0 || ft == 1 || ((ft == 2 || ft == 3 || ft == 7 || ft == 8 || ft == 9) && qv == 2);
         if (!ok) {
             char b[160];
             snprintf(b, sizeof b, "model ftype %d (hparams.f16 = %d) is not supported by this build", ft, hp.f16);
@@ -716,14 +720,17 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
     expneg.resize((expneg.size() + 7) / 8 * 8, 0);  // whole 16-byte chunks for the LDS copy
     const size_t o_exp = add(expneg.data(), expneg.size() * 2);
     // conv weights -> [o][tap][Cp] (implicit-GEMM B operand)
+    const size_t ws = ctx->wf32 ? 4 : 2;  // bytes per matrix element (f32 files keep f32)
     auto pack_conv = [&](const HostTensor &w, int Cin, int Cp) {
-        std::vector<uint16_t> p((size_t)n * 3 * Cp, 0);
-        const uint16_t *s = w.f16();
+        std::vector<uint8_t> p((size_t)n * 3 * Cp * ws, 0);
+        const uint8_t *s = w.data.data();
         for (int64_t o = 0; o < n; ++o)
             for (int c = 0; c < Cin; ++c)
-                for (int k = 0; k < 3; ++k) p[((size_t)o * 3 + k) * Cp + c] = s[((size_t)o * Cin + c) * 3 + k];
-        return add(p.data(), p.size() * 2);
+                for (int k = 0; k < 3; ++k)
+                    memcpy(&p[(((size_t)o * 3 + k) * Cp + c) * ws], s + (((size_t)o * Cin + c) * 3 + k) * ws, ws);
+        return add(p.data(), p.size());
     };
+    auto M = [&](const std::string &name, int64_t nel) { return add(T(name).data.data(), (size_t)nel * ws); };
     const size_t o_c1w = pack_conv(T("encoder.conv1.weight"), C, Cp1);
     const size_t o_c1b = add(T("encoder.conv1.bias").f32(), n * 4);
     const size_t o_c2w = pack_conv(T("encoder.conv2.weight"), (int)n, (int)n);
@@ -732,14 +739,14 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
     const size_t o_lnpw = add(T("encoder.ln_post.weight").f32(), n * 4);
     const size_t o_lnpb = add(T("encoder.ln_post.bias").f32(), n * 4);
     auto cat3 = [&](const std::string &p, int64_t dim) {
-        std::vector<uint16_t> w((size_t)3 * dim * dim);
-        memcpy(&w[0], T(p + "query.weight").f16(), dim * dim * 2);
-        memcpy(&w[dim * dim], T(p + "key.weight").f16(), dim * dim * 2);
-        memcpy(&w[2 * dim * dim], T(p + "value.weight").f16(), dim * dim * 2);
+        std::vector<uint8_t> w((size_t)3 * dim * dim * ws);
+        memcpy(&w[0], T(p + "query.weight").data.data(), dim * dim * ws);
+        memcpy(&w[dim * dim * ws], T(p + "key.weight").data.data(), dim * dim * ws);
+        memcpy(&w[2 * dim * dim * ws], T(p + "value.weight").data.data(), dim * dim * ws);
         std::vector<float> b((size_t)3 * dim, 0.0f);
         memcpy(&b[0], T(p + "query.bias").f32(), dim * 4);
         memcpy(&b[2 * dim], T(p + "value.bias").f32(), dim * 4);
-        return std::make_pair(add(w.data(), w.size() * 2), add(b.data(), b.size() * 4));
+        return std::make_pair(add(w.data(), w.size()), add(b.data(), b.size() * 4));
     };
     struct EncOff { size_t l1w, l1b, wqkv, bqkv, wo, bo, l2w, l2b, w0, b0, w1, b1; };
     std::vector<EncOff> eo(La);
@@ -752,31 +759,31 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
         e.l1b = add(T(p + "attn_ln.bias").f32(), n * 4);
         auto qkv = cat3(p + "attn.", n);
         e.wqkv = qkv.first; e.bqkv = qkv.second;
-        e.wo = add(T(p + "attn.out.weight").f16(), n * n * 2);
+        e.wo = M(p + "attn.out.weight", n * n);
         e.bo = add(T(p + "attn.out.bias").f32(), n * 4);
         e.l2w = add(T(p + "mlp_ln.weight").f32(), n * 4);
         e.l2b = add(T(p + "mlp_ln.bias").f32(), n * 4);
-        e.w0 = add(T(p + "mlp.0.weight").f16(), 4 * n * n * 2);
+        e.w0 = M(p + "mlp.0.weight", 4 * n * n);
         e.b0 = add(T(p + "mlp.0.bias").f32(), 4 * n * 4);
-        e.w1 = add(T(p + "mlp.2.weight").f16(), 4 * n * n * 2);
+        e.w1 = M(p + "mlp.2.weight", 4 * n * n);
         e.b1 = add(T(p + "mlp.2.bias").f32(), n * 4);
     }
     // cross-attention K/V of every decoder layer as ONE [Lt*2*nt][n] matrix
     size_t o_wckv, o_bckv;
     {
-        std::vector<uint16_t> w((size_t)Lt * 2 * nt * n);
+        std::vector<uint8_t> w((size_t)Lt * 2 * nt * n * ws);
         std::vector<float> b((size_t)Lt * 2 * nt, 0.0f);
         for (int l = 0; l < Lt; ++l) {
             snprintf(nm, sizeof nm, "decoder.blocks.%d.cross_attn.", l);
             const std::string p(nm);
-            memcpy(&w[(size_t)(2 * l) * nt * n], T(p + "key.weight").f16(), nt * n * 2);
-            memcpy(&w[(size_t)(2 * l + 1) * nt * n], T(p + "value.weight").f16(), nt * n * 2);
+            memcpy(&w[(size_t)(2 * l) * nt * n * ws], T(p + "key.weight").data.data(), nt * n * ws);
+            memcpy(&w[(size_t)(2 * l + 1) * nt * n * ws], T(p + "value.weight").data.data(), nt * n * ws);
             memcpy(&b[(size_t)(2 * l + 1) * nt], T(p + "value.bias").f32(), nt * 4);
         }
-        o_wckv = add(w.data(), w.size() * 2);
+        o_wckv = add(w.data(), w.size());
         o_bckv = add(b.data(), b.size() * 4);
     }
-    const size_t o_te = add(T("decoder.token_embedding.weight").f16(), (size_t)hp.n_vocab * nt * 2);
+    const size_t o_te = M("decoder.token_embedding.weight", (int64_t)hp.n_vocab * nt);
     const size_t o_dpe = add(T("decoder.positional_embedding").f32(), (size_t)hp.n_text_ctx * nt * 4);
     const size_t o_dlnw = add(T("decoder.ln.weight").f32(), nt * 4);
     const size_t o_dlnb = add(T("decoder.ln.bias").f32(), nt * 4);
@@ -790,19 +797,19 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
         d.l1b = add(T(p + "attn_ln.bias").f32(), nt * 4);
         auto qkv = cat3(p + "attn.", nt);
         d.wqkv = qkv.first; d.bqkv = qkv.second;
-        d.wo = add(T(p + "attn.out.weight").f16(), nt * nt * 2);
+        d.wo = M(p + "attn.out.weight", nt * nt);
         d.bo = add(T(p + "attn.out.bias").f32(), nt * 4);
         d.lcw = add(T(p + "cross_attn_ln.weight").f32(), nt * 4);
         d.lcb = add(T(p + "cross_attn_ln.bias").f32(), nt * 4);
-        d.wcq = add(T(p + "cross_attn.query.weight").f16(), nt * nt * 2);
+        d.wcq = M(p + "cross_attn.query.weight", nt * nt);
         d.bcq = add(T(p + "cross_attn.query.bias").f32(), nt * 4);
-        d.wco = add(T(p + "cross_attn.out.weight").f16(), nt * nt * 2);
+        d.wco = M(p + "cross_attn.out.weight", nt * nt);
         d.bco = add(T(p + "cross_attn.out.bias").f32(), nt * 4);
         d.l2w = add(T(p + "mlp_ln.weight").f32(), nt * 4);
         d.l2b = add(T(p + "mlp_ln.bias").f32(), nt * 4);
-        d.w0 = add(T(p + "mlp.0.weight").f16(), 4 * nt * nt * 2);
+        d.w0 = M(p + "mlp.0.weight", 4 * nt * nt);
         d.b0 = add(T(p + "mlp.0.bias").f32(), 4 * nt * 4);
-        d.w1 = add(T(p + "mlp.2.weight").f16(), 4 * nt * nt * 2);
+        d.w1 = M(p + "mlp.2.weight", 4 * nt * nt);
         d.b1 = add(T(p + "mlp.2.bias").f32(), nt * 4);
     }
     // q5_1 decoder: the GEMVs stream the blocks (0.75 B/weight instead of 2)
@@ -887,6 +894,7 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
     HIPCHK(ctx, hipMemcpy(&nfb, ctx->d_expfb + 64, 4, hipMemcpyDeviceToHost));
     ctx->n_expfb = (int)nfb;
     if (nfb > 64) ctx->use_persist = false;  // (not seen: ~19 inputs) the kernel chain then decodes
+    if (ctx->wf32) ctx->use_persist = false;  // f32 matrices: the kernel chain with the f32 GEMVs
     return WMI_OK;
 }
 
@@ -897,14 +905,15 @@ int alloc_workspace(wmi_context *ctx) {
     const int64_t n = hp.n_audio_state, nt = hp.n_text_state, H = hp.n_audio_head;
     const int64_t Lt = hp.n_text_layer;
     Arena A;
-    const size_t o_xconv = A.take(B * (T2 + 2) * ctx->Cp1 * 2);
+    const int64_t ab = ctx->wf32 ? 4 : 2;  // f32 models: conv1 / LN / attention outputs stay f32
+    const size_t o_xconv = A.take(B * (T2 + 2) * ctx->Cp1 * ab);
     const size_t o_g1 = A.take(B * (T2 + 2) * n * 2);
     const size_t o_h = A.take(B * T * n * 4);
-    const size_t o_xln = A.take(B * T * n * 2);
+    const size_t o_xln = A.take(B * T * n * ab);
     const size_t o_q = A.take(B * H * Tp * 64 * 2);
     const size_t o_k = A.take(B * H * Tp * 64 * 2);
     const size_t o_vt = A.take(B * H * Tp * 64 * 2);
-    const size_t o_att = A.take(B * T * n * 2);
+    const size_t o_att = A.take(B * T * n * ab);
     const size_t o_hid = A.take(B * T * 4 * n * 2);
     const size_t o_enc32 = A.take(B * T * n * 4);
     const size_t o_enc16 = A.take(B * T * n * 2);
@@ -956,6 +965,11 @@ int alloc_workspace(wmi_context *ctx) {
     ctx->att = (uint16_t *)(b + o_att);
     ctx->hid = (uint16_t *)(b + o_hid);
     ctx->enc32 = (float *)(b + o_enc32);
+    if (ctx->wf32) {
+        ctx->xconv32 = (float *)(b + o_xconv);
+        ctx->xln32 = (float *)(b + o_xln);
+        ctx->att32 = (float *)(b + o_att);
+    }
     ctx->enc16 = (uint16_t *)(b + o_enc16);
     ctx->ck = (uint16_t *)(b + o_ck);
     ctx->cv = (uint16_t *)(b + o_cv);
@@ -1102,18 +1116,23 @@ int run_encode(wmi_context *ctx, int mel_offset) {
     }
     // mel window -> conv1 input (main.rs:1816-1833)
     HIPCHK(ctx, launch_mel_window(s, ctx->d_mel, ctx->mel_stride, hp.n_mels, ctx->d_nlen, mel_offset, T2, ctx->Cp1,
-                                  ctx->xconv, B));
+                                  ctx->xconv, B, ctx->xconv32));
+    // f32 models: f32 weights and unrounded f32 A operands (GELU outputs g1 /
+    // hid stay f16: table values, exact in f32) -> the f32 GEMM
+    const bool f32 = ctx->wf32;
+    auto W32 = [&](const uint16_t *w) { return f32 ? (const float *)w : nullptr; };
     HIPCHK(ctx, hipMemsetAsync(ctx->g1, 0, (size_t)B * (T2 + 2) * n * 2, s));
     GemmArgs g{};
     // conv1 + bias + GELU (main.rs:1834-1855)
     g.A = ctx->xconv; g.B = ctx->conv1_w; g.bias = ctx->conv1_b;
+    g.A32 = ctx->xconv32; g.B32 = W32(ctx->conv1_w);
     g.M = B * T2; g.N = n; g.K = 3 * ctx->Cp1;
     g.conv = 1; g.conv_stride = 1; g.conv_tin = T2; g.conv_cp = ctx->Cp1; g.conv_tout = T2;
     g.out16 = ctx->g1; g.ldo = n; g.gelu_tab = ctx->gelu_tab; g.T = T2;
     HIPCHK(ctx, launch_gemm(s, EPI_CONV1, g));
     // conv2 + bias + GELU + positional embedding (main.rs:1856-1875)
     g = GemmArgs{};
-    g.A = ctx->g1; g.B = ctx->conv2_w; g.bias = ctx->conv2_b;
+    g.A = ctx->g1; g.B = ctx->conv2_w; g.bias = ctx->conv2_b; g.B32 = W32(ctx->conv2_w);
     g.M = B * T; g.N = n; g.K = 3 * n;
     g.conv = 1; g.conv_stride = 2; g.conv_tin = T2; g.conv_cp = n; g.conv_tout = T;
     g.out32 = ctx->h; g.ldo = n; g.gelu_tab = ctx->gelu_tab; g.pe = ctx->e_pe; g.T = T;
@@ -1121,27 +1140,30 @@ int run_encode(wmi_context *ctx, int mel_offset) {
     const int M = B * T;
     for (int l = 0; l < hp.n_audio_layer; ++l) {
         const EncLayerDev &e = ctx->enc[l];
-        HIPCHK(ctx, launch_layernorm(s, ctx->h, M, n, e.ln1_w, e.ln1_b, ctx->xln, nullptr));
+        HIPCHK(ctx, launch_layernorm(s, ctx->h, M, n, e.ln1_w, e.ln1_b, f32 ? nullptr : ctx->xln, ctx->xln32));
         g = GemmArgs{};
         g.A = ctx->xln; g.lda = n; g.B = e.wqkv; g.bias = e.bqkv; g.M = M; g.N = 3 * n; g.K = n;
+        g.A32 = ctx->xln32; g.B32 = W32(e.wqkv);
         g.q = ctx->q; g.k = ctx->k; g.vt = ctx->vt; g.T = T; g.Tp = Tp; g.n_state = n;
         HIPCHK(ctx, launch_gemm(s, EPI_QKV, g));
         AttnArgs at{}; at.tune = &ctx->tune;
-        at.q = ctx->q; at.k = ctx->k; at.vt = ctx->vt; at.out = ctx->att; at.exp_tab = ctx->exp_tab;
+        at.q = ctx->q; at.k = ctx->k; at.vt = ctx->vt; at.out = ctx->att; at.out32 = ctx->att32; at.exp_tab = ctx->exp_tab;
         at.n_exp = ctx->n_exp; at.T = T; at.Tp = Tp; at.H = H; at.n_state = n; at.n_clips = B;
         at.scale = (float)(1.0 / sqrt(64.0));
         HIPCHK(ctx, launch_attn_enc(s, at));
         g = GemmArgs{};
         g.A = ctx->att; g.lda = n; g.B = e.wo; g.bias = e.bo; g.M = M; g.N = n; g.K = n;
+        g.A32 = ctx->att32; g.B32 = W32(e.wo);
         g.out32 = ctx->h; g.ldo = n;
         HIPCHK(ctx, launch_gemm(s, EPI_RESID, g));
-        HIPCHK(ctx, launch_layernorm(s, ctx->h, M, n, e.ln2_w, e.ln2_b, ctx->xln, nullptr));
+        HIPCHK(ctx, launch_layernorm(s, ctx->h, M, n, e.ln2_w, e.ln2_b, f32 ? nullptr : ctx->xln, ctx->xln32));
         g = GemmArgs{};
         g.A = ctx->xln; g.lda = n; g.B = e.w0; g.bias = e.b0; g.M = M; g.N = 4 * n; g.K = n;
+        g.A32 = ctx->xln32; g.B32 = W32(e.w0);
         g.out16 = ctx->hid; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
         HIPCHK(ctx, launch_gemm(s, EPI_GELU16, g));
         g = GemmArgs{};
-        g.A = ctx->hid; g.lda = 4 * n; g.B = e.w1; g.bias = e.b1; g.M = M; g.N = n; g.K = 4 * n;
+        g.A = ctx->hid; g.lda = 4 * n; g.B = e.w1; g.bias = e.b1; g.M = M; g.N = n; g.K = 4 * n; g.B32 = W32(e.w1);
         g.out32 = ctx->h; g.ldo = n;
         HIPCHK(ctx, launch_gemm(s, EPI_RESID, g));
     }
@@ -1151,6 +1173,7 @@ int run_encode(wmi_context *ctx, int mel_offset) {
     // cross-attention K/V for every decoder layer in one GEMM (main.rs:1990-2060)
     g = GemmArgs{};
     g.A = ctx->enc16; g.lda = n; g.B = ctx->wckv; g.bias = ctx->bckv; g.M = M; g.N = hp.n_text_layer * 2 * nt; g.K = n;
+    if (f32) { g.A32 = ctx->enc32; g.B32 = W32(ctx->wckv); }
     g.ck = ctx->ck; g.cv = ctx->cv; g.T = T; g.n_state = nt; g.n_clips = B;
     g.kscale = powf((float)n / (float)H, -0.25f);  // main.rs:1994
     HIPCHK(ctx, launch_gemm(s, EPI_CROSSKV, g));
@@ -1246,7 +1269,11 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     // kernel while that re-read stays small (base/small greedy or 5 beams,
     // base 8 clips), not at large-v3 x 5 beams (12 H^2 B n 4 B = 123 MB a
     // layer; measured 554 -> 498 ms decode unfused)
-    const bool fuse_wo = ctx->fuse_wo && (int64_t)H * H * B * n <= ((int64_t)1 << 20);
+    const bool fuse_wo = ctx->fuse_wo && !ctx->wf32 && (int64_t)H * H * B * n <= ((int64_t)1 << 20);
+    // f32 models: every GEMV streams f32 rows (W32); cross q gets its own
+    // GEMV (the score kernels fold only f16 Wq rows in)
+    const bool f32 = ctx->wf32;
+    auto W32 = [&](const uint16_t *w) { return f32 ? (const float *)w : nullptr; };
     for (int l = 0; l < ctx->dec_layers; ++l) {
         const DecLayerDev &d = ctx->dec[l];
         uint16_t *kc = ctx->kcache + (size_t)l * DEC_ROWS * hp.n_text_ctx * n;
@@ -1255,10 +1282,12 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         const bool q5 = ctx->use_q5;
         g.x = X[cur]; g.ln_w = d.ln1_w; g.ln_b = d.ln1_b; g.W = d.wqkv; g.bias = d.bqkv; g.N = 3 * n; g.K = n; g.B = B;
         g.Wq5 = q5 ? d.wqkv5 : nullptr;
+        g.W32 = W32(d.wqkv);
         g.qscale = qs; g.out16 = ctx->dq16; g.ldo = n; g.kcache = kc; g.vcache = vc; g.n_text_ctx = hp.n_text_ctx;
         g.st = ctx->dstate;
         if (l == 0) {
             g.te = ctx->te; g.pe = ctx->d_pe; g.feed = ctx->dfeed; g.feed_len = feed_len; g.feed_stride = feed_stride;
+            if (f32) { g.te32 = W32(ctx->te); g.te = nullptr; }
             g.amax = ctx->damax; g.tokens_out = ctx->dtokens + (size_t)b0 * out_stride; g.out_stride = out_stride;
             g.x_out = X[cur];
             if (beam) {
@@ -1295,11 +1324,19 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
             g = DecGemvArgs{};
             g.parts = ctx->dopart; g.n_parts = 1; g.W = d.wo; g.bias = d.bo; g.N = n; g.K = n; g.B = B;
             g.Wq5 = q5 ? d.wo5 : nullptr;
+            g.W32 = W32(d.wo);
             g.out32 = X[cur];
             g.trace = tslot(ctx, "wo", l);
             HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
         }
         const int c_cross = (T + 127) / 128;
+        if (f32) {  // q = f16((Wq LN(x) + bq) * qscale) on f32 rows
+            g = DecGemvArgs{}; g.tune = &ctx->tune;
+            g.x = X[cur]; g.ln_w = d.lnc_w; g.ln_b = d.lnc_b; g.W32 = W32(d.wcq); g.bias = d.bcq;
+            g.N = n; g.K = n; g.B = B; g.qscale = qs; g.out16 = ctx->dq16; g.ldo = n;
+            g.trace = tslot(ctx, "cross_q", l);
+            HIPCHK(ctx, launch_dec_gemv(s, DEC_Q, g));
+        }
         at = DecAttnArgs{};
         at.K = ctx->ck + ((size_t)l * Bt + b0) * T * n;
         at.V = ctx->cv + ((size_t)l * Bt + b0) * T * n;
@@ -1308,6 +1345,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         at.n_chunks = c_cross; at.exp_tab = ctx->exp_tab; at.n_exp = ctx->n_exp; at.H = H; at.n = n; at.B = B;
         at.x = X[cur]; at.ln_w = d.lnc_w; at.ln_b = d.lnc_b; at.Wq = d.wcq; at.bq = d.bcq; at.qscale = qs;
         at.sync = ctx->use_coop ? ctx->dsync + (size_t)l * 8 * H : nullptr;
+        if (f32) { at.Wq = nullptr; at.q = ctx->dq16; at.sync = nullptr; }
         at.err = ctx->derr;
         at.clip_div = beam ? B : 1;  // beam rows all read clip b0's cross K/V
         if (fuse_wo) {
@@ -1320,6 +1358,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         g = DecGemvArgs{};
         g.parts = ctx->dopart; g.n_parts = c_cross; g.W = d.wco; g.bias = d.bco; g.N = n; g.K = n; g.B = B;
         g.Wq5 = q5 ? d.wco5 : nullptr;
+        g.W32 = W32(d.wco);
         g.out32 = X[cur];
         g.trace = tslot(ctx, "wco", l);
         if (l == 0) g.phase = pslot(ctx, 2, "wco[0]");
@@ -1327,6 +1366,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         g = DecGemvArgs{};
         g.x = X[cur]; g.ln_w = d.ln2_w; g.ln_b = d.ln2_b; g.W = d.w0; g.bias = d.b0; g.N = 4 * n; g.K = n; g.B = B;
         g.Wq5 = q5 ? d.w05 : nullptr;
+        g.W32 = W32(d.w0);
         g.out16 = ctx->dhid16; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
         g.trace = tslot(ctx, "mlp0", l);
         if (l == 0) g.phase = pslot(ctx, 3, "mlp0[0]");
@@ -1334,6 +1374,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
         g = DecGemvArgs{};
         g.xin16 = ctx->dhid16; g.W = d.w1; g.bias = d.b1; g.N = n; g.K = 4 * n; g.B = B; g.out32 = X[cur];
         g.Wq5 = q5 ? d.w15 : nullptr;
+        g.W32 = W32(d.w1);
         g.trace = tslot(ctx, "mlp1", l);
         if (l == 0) g.phase = pslot(ctx, 4, "mlp1[0]");
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
@@ -1341,6 +1382,7 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     DecGemvArgs g{}; g.tune = &ctx->tune;
     g.x = X[cur]; g.ln_w = ctx->dln_w; g.ln_b = ctx->dln_b; g.W = ctx->te; g.N = hp.n_vocab; g.K = n; g.B = B;
     g.Wq5 = ctx->use_q5 ? ctx->te5 : nullptr;
+    g.W32 = W32(ctx->te);
     g.out32 = ctx->dlogits; g.amax = ctx->damax; g.suppress_id = suppress_eot ? ctx->sp.eot : -1;
     g.st_advance = ctx->dstate;
     g.trace = tslot(ctx, "logits", 0);
@@ -1958,6 +2000,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     ctx->device = device;
     ctx->max_clips = max_clips;
     ctx->hp = pm.hp;
+    ctx->wf32 = pm.hp.f16 % 1000 == 0;
     init_specials(pm.hp.n_vocab, ctx->sp);
     // id_to_token incl. extra-token names (main.rs:442-467)
     ctx->vocab = std::move(pm.vocab);
@@ -2437,6 +2480,7 @@ int wmi_get_cross_kv(const wmi_context *ctx, int clip, uint16_t *k, uint16_t *v,
 int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *out) {
     if (!valid(ctx) || !out || iters < 1) return WMI_E_INVALID_ARG;
     if (ctx->enc_T <= 0) return set_err(ctx, WMI_E_INVALID_ARG, "bench_kernel before a pipeline run");
+    if (ctx->wf32) return set_err(ctx, WMI_E_UNSUPPORTED, "bench_kernel probes the f16 kernels");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     const wmi_hparams &hp = ctx->hp;
     const int n = hp.n_audio_state, T = ctx->enc_T, B = ctx->enc_clips, M = B * T;

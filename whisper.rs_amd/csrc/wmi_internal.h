@@ -34,7 +34,8 @@ hipError_t launch_mel_norm(hipStream_t s, float *mel, int64_t mel_stride, int n_
 // mel window (main.rs:1816-1833) -> conv1 input, f16 time-major, zero-padded
 // by one frame at each end and to Cp channels: X[b][T2 + 2][Cp].
 hipError_t launch_mel_window(hipStream_t s, const float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
-                             int mel_offset, int T2, int Cp, uint16_t *xconv, int n_clips);
+                             int mel_offset, int T2, int Cp, uint16_t *xconv, int n_clips,
+                             float *xconv32 = nullptr);
 
 // ---- LayerNorm (ggml norm + mul(repeat(w)) + add(repeat(b))) ----------------
 hipError_t launch_layernorm(hipStream_t s, const float *x, int rows, int n, const float *w, const float *b,
@@ -88,14 +89,20 @@ struct GemmArgs {
     uint16_t *ck, *cv;
     int n_clips;
     float kscale;
+    // f32 models (ggml f32 x f32 mul_mat / conv: neither operand rounded):
+    // B32 = f32 weights [N][K] selects the f32 MFMA GEMM (wmi_f32.hip); its
+    // A operand is A32 (f32) when set, else A (f16: GELU-table outputs, exact)
+    const float *A32, *B32;
 };
 hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a);
+hipError_t launch_gemm32(hipStream_t s, int epi, const GemmArgs &a);  // wmi_f32.hip
 
 // ---- encoder self-attention (ggml flash_attn_f16 semantics, exact softmax) --
 struct AttnArgs {
     const Tune *tune;  // context knobs (null: defaults)
     const uint16_t *q, *k, *vt;  // [b][h][Tp][64], vt [b][h][64][Tp]
     uint16_t *out;               // [b*T + t][n_state]
+    float *out32;                // or f32 output (f32 models: Wo takes it unrounded)
     const uint16_t *exp_tab;     // f16 exp table, negative half
     int n_exp;                   // entries in exp_tab
     int T, Tp, H, n_state, n_clips;
@@ -146,10 +153,14 @@ struct DecGemvArgs {
     const int32_t *beam_tok;    // beam search: token of row b past the prompt (BeamState::tok), else null
     unsigned long long *trace;  // WMI_TRACE: {min start, ~max end} s_memrealtime of this launch
     unsigned long long *phase;  // WMI_TRACE: [2][8] phase times of the first and last workgroup
+    // f32 models: W32 = f32 weights [N][K] (W / Wq5 unused), te32 = f32 token
+    // embedding for IN = 3; activations stay f32 into the dot (wmi_f32.hip)
+    const float *W32, *te32;
 };
 constexpr int AMAX_SHARDS = 64;
 constexpr int DEC_ROWS = 8;  // decoder rows per step: clips (greedy) or beam hypotheses
 hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a);
+hipError_t launch_dec_gemv32(hipStream_t s, int epi, const DecGemvArgs &a);  // wmi_f32.hip
 
 struct DecAttnArgs {
     const Tune *tune;  // context knobs (null: defaults)

@@ -20,6 +20,7 @@
 
 #include "wmi_device.h"
 #include "wmi_internal.h"
+#include "wmi_gemm_epi.h"
 
 #pragma clang fp contract(off)
 
@@ -184,7 +185,7 @@ __global__ void k_mel_norm(float *mel, int64_t mel_stride, int n_mel, const int6
 }
 
 __global__ void k_mel_window(const float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len, int mel_offset,
-                             int T2, int Cp, uint16_t *xconv) {
+                             int T2, int Cp, uint16_t *xconv, float *xconv32) {
     const int b = blockIdx.y;
     const int64_t nl = n_len[b];
     const int64_t tot = (int64_t)(T2 + 2) * Cp;
@@ -192,13 +193,15 @@ __global__ void k_mel_window(const float *mel, int64_t mel_stride, int n_mel, co
     const int64_t i1 = (int64_t)mel_offset + T2 < nl ? (int64_t)mel_offset + T2 : nl;
     const float *p = mel + (int64_t)b * mel_stride;
     uint16_t *o = xconv + (int64_t)b * tot;
+    float *o32 = xconv32 ? xconv32 + (int64_t)b * tot : nullptr;  // f32 models: conv1 input unrounded
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += (int64_t)gridDim.x * blockDim.x) {
         const int64_t row = idx / Cp;
         const int c = (int)(idx - row * Cp);
         const int64_t t = row - 1;
         float v = 0.0f;
         if (t >= 0 && t < T2 && c < n_mel && i0 + t < i1) v = p[(int64_t)c * nl + i0 + t];
-        o[idx] = f2h_bits(v);
+        if (xconv32) o32[idx] = v;
+        else o[idx] = f2h_bits(v);
     }
 }
 
@@ -224,10 +227,11 @@ hipError_t launch_mel_norm(hipStream_t s, float *mel, int64_t mel_stride, int n_
 }
 
 hipError_t launch_mel_window(hipStream_t s, const float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
-                             int mel_offset, int T2, int Cp, uint16_t *xconv, int n_clips) {
+                             int mel_offset, int T2, int Cp, uint16_t *xconv, int n_clips,
+                             float *xconv32) {
     const int64_t tot = (int64_t)(T2 + 2) * Cp;
     dim3 grid(cdiv(tot, 1024) < 512 ? cdiv(tot, 1024) : 512, n_clips);
-    hipLaunchKernelGGL(k_mel_window, grid, dim3(256), 0, s, mel, mel_stride, n_mel, n_len, mel_offset, T2, Cp, xconv);
+    hipLaunchKernelGGL(k_mel_window, grid, dim3(256), 0, s, mel, mel_stride, n_mel, n_len, mel_offset, T2, Cp, xconv, xconv32);
     return hipGetLastError();
 }
 
@@ -296,71 +300,6 @@ __device__ __forceinline__ uint4 gemm_load_a(const GemmArgs &a, int m, int k) {
     return *(const uint4 *)p;
 }
 
-template <int EPI>
-__device__ __forceinline__ void gemm_epi4(const GemmArgs &a, int m, int n, const float *v) {
-    // v[0..3] = rows m..m+3 of column n
-    if (n >= a.N) return;
-    const float bias = a.bias ? a.bias[n] : 0.0f;
-    if (EPI == EPI_QKV) {
-        const int ns = a.n_state;
-        const int which = n / ns, c = n - which * ns, h = c >> 6, d = c & 63;
-        const int H = ns >> 6;
-        if (which < 2) {
-            uint16_t *dst = which == 0 ? a.q : a.k;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int mm = m + r;
-                if (mm >= a.M) break;
-                const int b = mm / a.T, t = mm - b * a.T;
-                dst[(((int64_t)b * H + h) * a.Tp + t) * 64 + d] = f2h_bits(v[r] + bias);
-            }
-        } else {
-            const int b0 = m / a.T, t0 = m - b0 * a.T;
-            if (m + 3 < a.M && t0 + 3 < a.T && (t0 & 3) == 0) {
-                half4 hv;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) hv[r] = (f16)(v[r] + bias);
-                *(half4 *)(a.vt + (((int64_t)b0 * H + h) * 64 + d) * a.Tp + t0) = hv;
-            } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int mm = m + r;
-                    if (mm >= a.M) break;
-                    const int b = mm / a.T, t = mm - b * a.T;
-                    a.vt[(((int64_t)b * H + h) * 64 + d) * a.Tp + t] = f2h_bits(v[r] + bias);
-                }
-            }
-        }
-        return;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int mm = m + r;
-        if (mm >= a.M) break;
-        if (EPI == EPI_F32) {
-            a.out32[(int64_t)mm * a.ldo + n] = v[r] + bias;
-        } else if (EPI == EPI_RESID) {
-            float *p = a.out32 + (int64_t)mm * a.ldo + n;
-            *p = (v[r] + bias) + *p;
-        } else if (EPI == EPI_GELU16) {
-            a.out16[(int64_t)mm * a.ldo + n] = a.gelu_tab[f2h_bits(v[r] + bias)];
-        } else if (EPI == EPI_CONV1) {
-            const int b = mm / a.T, t = mm - b * a.T;
-            a.out16[((int64_t)b * (a.T + 2) + t + 1) * a.ldo + n] = a.gelu_tab[f2h_bits(v[r] + bias)];
-        } else if (EPI == EPI_CONV2PE) {
-            const int b = mm / a.T, t = mm - b * a.T;
-            (void)b;
-            a.out32[(int64_t)mm * a.ldo + n] = a.pe[(int64_t)t * a.ldo + n] + gelu_lookup(a.gelu_tab, v[r] + bias);
-        } else if (EPI == EPI_CROSSKV) {
-            const int ns = a.n_state;
-            const int l = n / (2 * ns), rr = n - l * 2 * ns;
-            const int b = mm / a.T, t = mm - b * a.T;
-            const int64_t base = (((int64_t)l * a.n_clips + b) * a.T + t) * ns;
-            if (rr < ns) a.ck[base + rr] = f2h_bits(v[r] * a.kscale);
-            else a.cv[base + rr - ns] = f2h_bits(v[r] + bias);
-        }
-    }
-}
 
 template <int BM, int BN, int EPI, bool CONV>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
@@ -491,6 +430,7 @@ static hipError_t gemm_dispatch_epi(hipStream_t s, int epi, const GemmArgs &a) {
 
 hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a) {
     if (a.M <= 0 || a.N <= 0) return hipSuccess;
+    if (a.B32) return launch_gemm32(s, epi, a);
     if (a.K % GBK != 0 || a.K <= 0) return hipErrorInvalidValue;
     if (a.conv && a.conv_cp % GBK != 0) return hipErrorInvalidValue;
     const int64_t t128 = (int64_t)cdiv(a.M, 128) * cdiv(a.N, 128);
@@ -694,8 +634,14 @@ __global__ __launch_bounds__(512) void k_attn_enc3(AttnArgs a) {
             }
             if (t < T) {
                 uint16_t *dst = a.out + ((int64_t)b * T + t) * a.n_state + h * 64;
-                dst[lr] = f2h_bits(v0);
-                dst[32 + lr] = f2h_bits(v1);
+                if (a.out32) {  // f32 models: the output projection takes it unrounded
+                    float *d32 = a.out32 + ((int64_t)b * T + t) * a.n_state + h * 64;
+                    d32[lr] = v0;
+                    d32[32 + lr] = v1;
+                } else {
+                    dst[lr] = f2h_bits(v0);
+                    dst[32 + lr] = f2h_bits(v1);
+                }
             }
         }
     }
@@ -1214,6 +1160,7 @@ static hipError_t dec_gemv_w(hipStream_t s, const DecGemvArgs &a) {
 // (epilogue, input) pairs the decoder step uses
 hipError_t launch_dec_gemv(hipStream_t s, int epi, const DecGemvArgs &a) {
     if (a.B < 1 || a.B > DG_MAXB || a.K % 128) return hipErrorInvalidValue;
+    if (a.W32) return launch_dec_gemv32(s, epi, a);
     const int in = a.te ? 3 : (a.ln_w ? 0 : (a.parts ? 2 : 1));
     if (epi == DEC_QKV && in == 3) return dec_gemv_w<DEC_QKV, 3>(s, a);
     if (epi == DEC_QKV && in == 0) return dec_gemv_w<DEC_QKV, 0>(s, a);
@@ -1772,6 +1719,32 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
 }
 
 
+// Phase A of cross-attention with the query given (f32 models: q =
+// f16((Wq LN(x) + bq) * qscale) comes from the DEC_Q GEMV, whose f32 weights
+// the score kernels cannot fold in): the chunk's scores -> S, its max -> cmax,
+// with k_dec_xattn's key / half-row split and combine; k_dec_attn_pv follows.
+__global__ __launch_bounds__(256) void k_dec_xscore_q(DecAttnArgs a) {
+    const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int M = a.M_fixed, n = a.n;
+    __shared__ float red[4];
+    const int key = c * DA_CK + (tid >> 1), half = tid & 1;
+    const f16 *kr = (const f16 *)a.K + (int64_t)(b / a.clip_div) * a.clip_stride + (int64_t)(key < M ? key : M - 1) * n +
+                    h * 64 + half * 32;
+    const f16 *qr = (const f16 *)a.q + (int64_t)b * n + h * 64 + half * 32;
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s = dot8(*(const half8 *)(kr + 8 * i), *(const half8 *)(qr + 8 * i), s);
+    s = xstep<XSum, 1>(s);
+    float *S = a.S + ((int64_t)b * a.H + h) * a.s_stride;
+    if (half == 0 && key < M) S[key] = s;
+    float m = (key < M) ? s : -INFINITY;
+    m = wave_max(m);
+    if (lane == 0) red[w] = m;
+    __syncthreads();
+    if (tid == 0) a.cmax[((int64_t)b * a.H + h) * a.n_chunks + c] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
 const Tune kTuneDefault{};
 
 hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
@@ -1794,6 +1767,14 @@ hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
         (a.res_parts && (a.H * 64 != a.n || !a.res_bias || !a.x_out || a.x_out == a.x)))
         return hipErrorInvalidValue;
     dim3 grid(a.n_chunks, a.H, a.B);
+    if (!a.Wq) {  // query precomputed (f32 models)
+        if (!a.q || a.res_parts) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_dec_xscore_q, grid, dim3(256), 0, s, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_dec_attn_pv, grid, dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     // cooperative single kernel while the grid stays far inside residency
     // (<= 2 workgroups per CU) and the Wq rows fit the register budget;
     // otherwise the two-kernel form

@@ -161,10 +161,13 @@ def tensor_specs(hp: dict):
     yield "decoder.ln.bias", (nt,), "lnb"
 
 
-def tensor_value(name: str, shape, kind: str, hp: dict, wscale: float = 0.02) -> np.ndarray:
+def tensor_value(name: str, shape, kind: str, hp: dict, wscale: float = 0.02, wf32: bool = False) -> np.ndarray:
+    """wf32: weight matrices / conv kernels stay f32 (an ftype-0 file; values
+    not representable in f16, so a path that rounded them would show)."""
     rng = np.random.default_rng(zlib.crc32(name.encode()))
     if kind == "w":
-        return (rng.standard_normal(shape, dtype=np.float32) * wscale).astype(np.float16)
+        w = rng.standard_normal(shape, dtype=np.float32) * wscale
+        return w.astype(np.float32) if wf32 else w.astype(np.float16)
     if kind in ("b", "lnb"):
         return (rng.standard_normal(shape, dtype=np.float32) * 0.01).astype(np.float32)
     if kind == "g":
@@ -272,12 +275,16 @@ def write_ggml(path: str, model: str = "base", hp_override: dict | None = None,
                quant: str | None = None) -> dict:
     """Write a synthetic ggml-v1 Whisper file; returns the hparams used.
     tensor_hook(name, array) -> array may edit tensors before they are written.
-    quant ("q5_1", "q8_0", ...) stores every 2-D weight matrix in that ggml block format,
+    quant "f32" writes an ftype-0 file (hparams.f16 = 0: every matrix and conv
+    kernel f32, main.rs:817-821); "q5_1", "q8_0", ... store every 2-D weight matrix in that ggml block format,
     as whisper.cpp's quantize tool does (conv kernels, biases, LN parameters
     and positional embeddings keep their type); hparams.f16 then carries the
     file ftype + 1000 * GGML_QNT_VERSION."""
     hp = dict(MODEL_DIMS[model])
-    hp["f16"] = 1 if quant is None else QUANT_TYPES[quant][1] + 1000 * GGML_QNT_VERSION
+    wf32 = quant == "f32"
+    if wf32:
+        quant = None
+    hp["f16"] = (0 if wf32 else 1) if quant is None else QUANT_TYPES[quant][1] + 1000 * GGML_QNT_VERSION
     if hp_override:
         hp.update(hp_override)
     n_vocab_file = 50257 if n_vocab_file is None else n_vocab_file
@@ -293,7 +300,7 @@ def write_ggml(path: str, model: str = "base", hp_override: dict | None = None,
             f.write(struct.pack("<I", len(tok)))
             f.write(tok)
         for name, shape, kind in tensor_specs(hp):
-            arr = tensor_value(name, shape, kind, hp, wscale)
+            arr = tensor_value(name, shape, kind, hp, wscale, wf32=wf32)
             if tensor_hook is not None:
                 arr = tensor_hook(name, arr)
             ftype = 1 if arr.dtype == np.float16 else 0
@@ -319,7 +326,9 @@ def model_path(model: str, cache_dir: str | None = None) -> str:
     p = os.path.join(cache_dir, f"ggml-synth-{model}.bin")
     if not os.path.exists(p):
         base, _, quant = model.partition("-q")
-        if quant:  # e.g. "small-q5_1": the small model's weights in ggml q5_1
+        if model.endswith("-f32"):  # e.g. "micro-f32": an ftype-0 (f32) file
+            write_ggml(p, model[:-4], quant="f32")
+        elif quant:  # e.g. "small-q5_1": the small model's weights in ggml q5_1
             write_ggml(p, base, quant="q" + quant)
         else:
             write_ggml(p, model)
