@@ -46,7 +46,7 @@ enum wmi_status {
     WMI_E_UNEXPECTED = 10,    /* WsError::Unexpected        main.rs:52-53 */
     WMI_E_HIP = 11,           /* HIP runtime / kernel launch failure */
     WMI_E_RCCL = 12,          /* RCCL failure */
-    WMI_E_UNSUPPORTED = 13,   /* valid file, feature not built (e.g. f32 matrices) */
+    WMI_E_UNSUPPORTED = 13,   /* valid file, feature not built (e.g. a ggml type other than f32 / f16 / q4_0 / q4_1 / q5_0 / q5_1 / q8_0) */
     WMI_E_INVALID_ARG = 14    /* bad pointer / size / state order */
 };
 
@@ -87,7 +87,9 @@ typedef struct wmi_context wmi_context;
 
 /* WhisperContext::new(fname) (main.rs:366-503): open, magic, hparams,
  * filters, vocab (+extra tokens), weights; then upload to `device`.
- * max_clips sizes the device workspace for batched calls (>= 1). */
+ * max_clips sizes the device workspace for batched calls (>= 1).  Weight
+ * types: f16 and f32 files (hparams.f16 = 1 / 0, main.rs:817-821; f32
+ * matrices are kept f32 on the device) and the ggml quantised types. */
 int wmi_init_from_file(const char *path, int device, int max_clips, wmi_context **out);
 void wmi_free(wmi_context *ctx);
 const char *wmi_strerror(int status);

@@ -2053,6 +2053,8 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     knob("WMI_COOP_MAX", tn.coop_max, 1);
     knob("WMI_XATTN_ROWS", tn.xattn_rows, 0);
     knob("WMI_SELF_SPLIT", tn.self_split, 0);
+    knob("WMI_ENC_ATTN", tn.enc_attn, 3);
+    knob("WMI_ENC_ATTN_NW", tn.enc_attn_nw, 0);
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_trace, TRACE_SLOTS * 16 + 64 * 16 * 8));

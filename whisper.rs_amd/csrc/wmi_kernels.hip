@@ -239,25 +239,54 @@ hipError_t launch_mel_window(hipStream_t s, const float *mel, int64_t mel_stride
 // LayerNorm: ggml_compute_forward_norm_f32 (double mean / variance, eps 1e-5)
 // followed by mul(repeat(w)) and add(repeat(b)) (main.rs:1881-1886)
 // ============================================================================
+// one wave per row, the row held in registers (n <= 1280, n % 4 == 0): one
+// round trip for the loads instead of one per pass over the row
+constexpr int LNW_V = 5;
 __device__ __forceinline__ void layernorm_wave(const float *x, int n, const float *w, const float *b, uint16_t *y16,
                                                float *y32, int lane) {
+    float4 v[LNW_V], gw[LNW_V], gb[LNW_V];
+#pragma unroll
+    for (int i = 0; i < LNW_V; ++i) {
+        const int e = (lane + 64 * i) * 4, ec = e < n ? e : 0;  // clamped, unconditional loads
+        v[i] = *(const float4 *)(x + ec);
+        gw[i] = *(const float4 *)(w + ec);
+        gb[i] = *(const float4 *)(b + ec);
+    }
     double s = 0.0;
-    for (int i = lane; i < n; i += 64) s += (double)x[i];
+#pragma unroll
+    for (int i = 0; i < LNW_V; ++i)
+        if ((lane + 64 * i) * 4 < n) s += ((double)v[i].x + (double)v[i].y) + ((double)v[i].z + (double)v[i].w);
     s = wave_sum(s);
     const double mean = s / n;
     double s2 = 0.0;
-    for (int i = lane; i < n; i += 64) {
-        const double v = (double)x[i] - mean;
-        s2 += v * v;
-    }
+#pragma unroll
+    for (int i = 0; i < LNW_V; ++i)
+        if ((lane + 64 * i) * 4 < n) {
+            const double d0 = (double)v[i].x - mean, d1 = (double)v[i].y - mean;
+            const double d2 = (double)v[i].z - mean, d3 = (double)v[i].w - mean;
+            s2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+        }
     s2 = wave_sum(s2);
     const float scale = (float)(1.0 / sqrt(s2 / n + (double)1e-5f));
-    for (int i = lane; i < n; i += 64) {
-        const float yv = (float)((double)x[i] - mean);
-        const float t = yv * scale;
-        const float o = b[i] + w[i] * t;
-        if (y16) y16[i] = f2h_bits(o);
-        if (y32) y32[i] = o;
+#pragma unroll
+    for (int i = 0; i < LNW_V; ++i) {
+        const int e = (lane + 64 * i) * 4;
+        if (e < n) {
+            const float xx[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+            const float ww[4] = {gw[i].x, gw[i].y, gw[i].z, gw[i].w}, bb[4] = {gb[i].x, gb[i].y, gb[i].z, gb[i].w};
+            float o[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float yv = (float)((double)xx[u] - mean);
+                o[u] = bb[u] + ww[u] * (yv * scale);
+            }
+            if (y16) {
+                half4 hv;
+                hv[0] = (f16)o[0]; hv[1] = (f16)o[1]; hv[2] = (f16)o[2]; hv[3] = (f16)o[3];
+                *(half4 *)(y16 + e) = hv;
+            }
+            if (y32) *(float4 *)(y32 + e) = make_float4(o[0], o[1], o[2], o[3]);
+        }
     }
 }
 
@@ -271,6 +300,7 @@ __global__ __launch_bounds__(256) void k_layernorm(const float *x, int rows, int
 
 hipError_t launch_layernorm(hipStream_t s, const float *x, int rows, int n, const float *w, const float *b,
                             uint16_t *y16, float *y32) {
+    if (n % 4 || n > 256 * LNW_V) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_layernorm, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, rows, n, w, b, y16, y32);
     return hipGetLastError();
 }
@@ -282,7 +312,6 @@ hipError_t launch_layernorm(hipStream_t s, const float *x, int rows, int n, cons
 // LDS with 80-byte rows (conflict-free ds_read_b128 fragment reads).
 // ============================================================================
 constexpr int GBK = 32;
-constexpr int GLDS = 40;  // halfs per LDS row (32 + 8 pad)
 
 template <bool CONV>
 __device__ __forceinline__ uint4 gemm_load_a(const GemmArgs &a, int m, int k) {
@@ -301,13 +330,19 @@ __device__ __forceinline__ uint4 gemm_load_a(const GemmArgs &a, int m, int k) {
 }
 
 
-template <int BM, int BN, int EPI, bool CONV>
+// BK = k per LDS stage.  Small tiles (2-4 MFMAs per wave per 32 k) spend
+// their k loop on barriers and LDS round trips, so they take 64 or 128 k per
+// stage; the k steps of 16 still run in order, so the result is bitwise the
+// same for every BK (and every tile size).
+template <int BM, int BN, int BK, int EPI, bool CONV>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
-    constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave (2x2 waves)
-    constexpr int ACH = BM / 64, BCH = BN / 64;  // 16-byte chunks per thread per k-tile
-    __shared__ __attribute__((aligned(16))) f16 smem[2 * (BM + BN) * GLDS];
+    constexpr int TM = BM / 64, TN = BN / 64;          // 32x32 tiles per wave (2x2 waves)
+    constexpr int LD = BK + 8;                          // halfs per LDS row (16-byte pad)
+    constexpr int CPR = BK / 8;                         // 16-byte chunks per row of a stage
+    constexpr int ACH = BM * CPR / 256, BCH = BN * CPR / 256;  // chunks per thread per stage
+    __shared__ __attribute__((aligned(16))) f16 smem[2 * (BM + BN) * LD];
     f16 *As = smem;
-    f16 *Bs = smem + 2 * BM * GLDS;
+    f16 *Bs = smem + 2 * BM * LD;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
     // XCD-aware tile order: consecutive block ids land on different XCDs, so
@@ -321,32 +356,33 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
     }
     const int bn = bid % nbn, bm = bid / nbn;
     const int m0 = bm * BM, n0 = bn * BN;
-    const int nk = a.K / GBK;
+    const int nk = a.K / BK;
 
-    uint4 ra[ACH], rb[BCH];
+    typedef uint32_t g4 __attribute__((ext_vector_type(4)));  // native vector: stays in registers
+    g4 ra[ACH], rb[BCH];
     auto gload = [&](int kt) {
 #pragma unroll
         for (int i = 0; i < ACH; ++i) {
-            const int c = tid + i * 256, row = c >> 2, col = (c & 3) * 8;
-            ra[i] = gemm_load_a<CONV>(a, m0 + row, kt * GBK + col);
+            const int c = tid + i * 256, row = c / CPR, col = (c % CPR) * 8;
+            ra[i] = __builtin_bit_cast(g4, gemm_load_a<CONV>(a, m0 + row, kt * BK + col));
         }
 #pragma unroll
         for (int i = 0; i < BCH; ++i) {
-            const int c = tid + i * 256, row = c >> 2, col = (c & 3) * 8;
+            const int c = tid + i * 256, row = c / CPR, col = (c % CPR) * 8;
             const int n = n0 + row;
-            rb[i] = n < a.N ? *(const uint4 *)(a.B + (int64_t)n * a.K + kt * GBK + col) : make_uint4(0, 0, 0, 0);
+            rb[i] = n < a.N ? *(const g4 *)(a.B + (int64_t)n * a.K + kt * BK + col) : g4{0u, 0u, 0u, 0u};
         }
     };
     auto sstore = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < ACH; ++i) {
-            const int c = tid + i * 256, row = c >> 2, col = (c & 3) * 8;
-            *(uint4 *)(As + buf * BM * GLDS + row * GLDS + col) = ra[i];
+            const int c = tid + i * 256, row = c / CPR, col = (c % CPR) * 8;
+            *(g4 *)(As + buf * BM * LD + row * LD + col) = ra[i];
         }
 #pragma unroll
         for (int i = 0; i < BCH; ++i) {
-            const int c = tid + i * 256, row = c >> 2, col = (c & 3) * 8;
-            *(uint4 *)(Bs + buf * BN * GLDS + row * GLDS + col) = rb[i];
+            const int c = tid + i * 256, row = c / CPR, col = (c % CPR) * 8;
+            *(g4 *)(Bs + buf * BN * LD + row * LD + col) = rb[i];
         }
     };
 
@@ -364,25 +400,25 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
     const int lr = lane & 31, lh = lane >> 5;
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
-        if (kt + 1 < nk) gload(kt + 1);
-        const f16 *Ab = As + buf * BM * GLDS;
-        const f16 *Bb = Bs + buf * BN * GLDS;
+        gload(kt + 1 < nk ? kt + 1 : kt);  // unconditional (clamped): no undef phi
+        const f16 *Ab = As + buf * BM * LD;
+        const f16 *Bb = Bs + buf * BN * LD;
 #pragma unroll
-        for (int ks = 0; ks < GBK / 16; ++ks) {
+        for (int ks = 0; ks < BK / 16; ++ks) {
             half8 af[TM], bf[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
-                af[i] = *(const half8 *)(Ab + (wm * (BM / 2) + i * 32 + lr) * GLDS + ks * 16 + lh * 8);
+                af[i] = *(const half8 *)(Ab + (wm * (BM / 2) + i * 32 + lr) * LD + ks * 16 + lh * 8);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                bf[j] = *(const half8 *)(Bb + (wn * (BN / 2) + j * 32 + lr) * GLDS + ks * 16 + lh * 8);
+                bf[j] = *(const half8 *)(Bb + (wn * (BN / 2) + j * 32 + lr) * LD + ks * 16 + lh * 8);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
         }
-        if (kt + 1 < nk) sstore(buf ^ 1);
+        sstore(buf ^ 1);  // (after the last stage: a clamped copy, unread)
         __syncthreads();
     }
     // epilogue: lane holds column n, rows (reg&3) + 8(reg>>2) + 4(lane>>5)
@@ -400,13 +436,13 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
         }
 }
 
-template <int BM, int BN, bool CONV>
+template <int BM, int BN, int BK, bool CONV>
 static hipError_t gemm_dispatch_epi(hipStream_t s, int epi, const GemmArgs &a) {
     const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     dim3 grid(nwg), block(256);
 #define GEMM_CASE(E)                                                                  \
     case E:                                                                          \
-        hipLaunchKernelGGL((k_gemm<BM, BN, E, CONV>), grid, block, 0, s, a);         \
+        hipLaunchKernelGGL((k_gemm<BM, BN, BK, E, CONV>), grid, block, 0, s, a);     \
         break;
     if constexpr (CONV) {
         switch (epi) {
@@ -435,14 +471,19 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a) {
     if (a.conv && a.conv_cp % GBK != 0) return hipErrorInvalidValue;
     const int64_t t128 = (int64_t)cdiv(a.M, 128) * cdiv(a.N, 128);
     const int64_t t12864 = (int64_t)cdiv(a.M, 128) * cdiv(a.N, 64);
+    // k per stage: 64 for the smaller tiles when it divides K (and, for the
+    // implicit-GEMM conv, a tap's channel block); LDS stays <= 64 KB
+    const bool k64 = (a.conv ? a.conv_cp : a.K) % 64 == 0;
     if (a.conv) {
-        if (t128 >= 240) return gemm_dispatch_epi<128, 128, true>(s, epi, a);
-        if (t12864 >= 240) return gemm_dispatch_epi<128, 64, true>(s, epi, a);
-        return gemm_dispatch_epi<64, 64, true>(s, epi, a);
+        if (t128 >= 240) return gemm_dispatch_epi<128, 128, GBK, true>(s, epi, a);
+        if (t12864 >= 240) return k64 ? gemm_dispatch_epi<128, 64, 64, true>(s, epi, a)
+                                       : gemm_dispatch_epi<128, 64, GBK, true>(s, epi, a);
+        return k64 ? gemm_dispatch_epi<64, 64, 64, true>(s, epi, a) : gemm_dispatch_epi<64, 64, GBK, true>(s, epi, a);
     }
-    if (t128 >= 240) return gemm_dispatch_epi<128, 128, false>(s, epi, a);
-    if (t12864 >= 240) return gemm_dispatch_epi<128, 64, false>(s, epi, a);
-    return gemm_dispatch_epi<64, 64, false>(s, epi, a);
+    if (t128 >= 240) return gemm_dispatch_epi<128, 128, GBK, false>(s, epi, a);
+    if (t12864 >= 240) return k64 ? gemm_dispatch_epi<128, 64, 64, false>(s, epi, a)
+                                  : gemm_dispatch_epi<128, 64, GBK, false>(s, epi, a);
+    return k64 ? gemm_dispatch_epi<64, 64, 64, false>(s, epi, a) : gemm_dispatch_epi<64, 64, GBK, false>(s, epi, a);
 }
 
 // ============================================================================
@@ -567,7 +608,8 @@ __global__ __launch_bounds__(512) void k_attn_enc3(AttnArgs a) {
         for (int r = 0; r < 16; ++r) {
             const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
             const uint32_t i = f2h_bits(sc[j][r] - mrow) & 0x7fffu;
-            const uint16_t e = (key < T && (int)i < a.n_exp) ? tab[i] : (uint16_t)0;
+            const bool ok = key < T && (int)i < a.n_exp;
+            const uint16_t e = tab[ok ? i : 0u] & (ok ? 0xffffu : 0u);  // unguarded read, clamped index
             ev[j][r >> 3][r & 7] = __builtin_bit_cast(f16, e);
             if (key < T) sum += (double)h2f_bits(e);
         }
@@ -648,7 +690,216 @@ __global__ __launch_bounds__(512) void k_attn_enc3(AttnArgs a) {
 }
 
 
+// Version 4: NW waves x 32 queries per workgroup share every K / V tile
+// through LDS (64-key tiles, double-buffered, one global->LDS copy per tile
+// for the whole workgroup instead of one per 32 queries), and the exact
+// ggml softmax is kept with three sweeps over the keys instead of holding
+// the scores in registers:
+//   sweep 0: S = scale * K Q^T (MFMA) -> row max
+//   sweep 1: S again -> sum of exp_tab[f16(S - max)]  (double)
+//   sweep 2: S again -> P16 = f16(e * (1/sum)); O += P16 V (MFMA)
+// A wave owns its 32 queries over every key, so no cross-wave reduction or
+// partial-O combine exists; recomputing Q K^T twice costs MFMA time the
+// kernel has to spare (enc3 ran at 3 % MFMA busy, bound by its per-32-query
+// K / V streams).
+constexpr int AT4_KT = 64;  // keys per tile
+constexpr int AT4_LD = 72;  // halfs per LDS row (64 + 8 pad: 144-byte rows)
+
+// 16-byte staging chunks as a native vector (SROA keeps arrays of these in
+// registers; the struct uint4 arrays of the staging loop went to scratch)
+typedef uint32_t a4vec __attribute__((ext_vector_type(4)));
+
+// one 64-key tile from LDS (buffer Kb / Vb) for this wave's 32 queries
+template <int PASS>
+__device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, const f16 *Vb, int key0,
+                                           const uint16_t *tab, const half8 (&qf)[4], float &mx, double &sum,
+                                           float m, float inv, floatx16 &o0, floatx16 &o1) {
+    const int lane = threadIdx.x & 63, lr = lane & 31, lh = lane >> 5;
+    const int T = a.T, n_exp = a.n_exp;
+    const float scale = a.scale;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        floatx16 sc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[r] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8 *)(Kb + (kb * 32 + lr) * AT4_LD + 16 * s + 8 * lh),
+                                                        qf[s], sc, 0, 0, 0);
+        if constexpr (PASS == 0) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (key < T) mx = fmaxf(mx, sc[r] * scale);
+            }
+        } else {
+            half8 pa[2];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const uint32_t i = f2h_bits(sc[r] * scale - m) & 0x7fffu;
+                // unguarded read from a clamped index (a lane-guarded LDS read
+                // becomes a branch that waits one LDS latency per element)
+                const bool ok = key < T && (int)i < n_exp;
+                const float e = h2f_bits(tab[ok ? i : 0u]) * (ok ? 1.0f : 0.0f);
+                if constexpr (PASS == 1) sum += (double)e;
+                else pa[r >> 3][r & 7] = (f16)(e * inv);
+            }
+            if constexpr (PASS == 2) {
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    half8 vb[2];
+#pragma unroll
+                    for (int dt = 0; dt < 2; ++dt) {
+                        const f16 *vp = Vb + (dt * 32 + lr) * AT4_LD + kb * 32 + 16 * s + 4 * lh;
+                        const half4 v0 = *(const half4 *)vp, v1 = *(const half4 *)(vp + 8);
+                        vb[dt][0] = v0[0]; vb[dt][1] = v0[1]; vb[dt][2] = v0[2]; vb[dt][3] = v0[3];
+                        vb[dt][4] = v1[0]; vb[dt][5] = v1[1]; vb[dt][6] = v1[2]; vb[dt][7] = v1[3];
+                    }
+                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[s], vb[0], o0, 0, 0, 0);
+                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[s], vb[1], o1, 0, 0, 0);
+                }
+            }
+        }
+    }
+}
+
+// One sweep over the key tiles (PASS 0: max, 1: exp sum, 2: P16 V).  Tiles
+// go global -> registers -> LDS with two register stages: while tile kt is
+// computed from LDS, tile kt + 1 sits in one register set (stored to the
+// other LDS buffer after the compute) and tile kt + 2's loads are in flight
+// into the other, so a load has two tiles of compute to land (the loop is
+// unrolled by two so the register sets are named statically; every load is
+// unconditional from a clamped tile, so no undef phi reaches scratch).
+template <int NW, int PASS>
+__device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, const f16 *Vt, f16 *Ks, f16 *Vs,
+                                            const uint16_t *tab, const half8 (&qf)[4], float &mx, double &sum,
+                                            float m, float inv, floatx16 &o0, floatx16 &o1) {
+    const int tid = threadIdx.x;
+    const int Tp = a.Tp;
+    const int ntiles = (a.T + AT4_KT - 1) / AT4_KT;
+    constexpr int SCH = 512 / (64 * NW);  // 16-byte chunks per thread of an 8 KB tile
+    constexpr int VCH = PASS == 2 ? SCH : 1;
+    a4vec kA[SCH], vA[VCH], kB[SCH], vB[VCH];
+    // this thread's 16-byte chunks of a tile: rows (tid >> 3) + 8 NW i, column (tid & 7) * 8
+    const int crow = tid >> 3, ccol = (tid & 7) * 8;
+#define ATT4_GLOAD(KT, KR, VR)                                                                  \
+    {                                                                                           \
+        const int kt_ = (KT) < ntiles ? (KT) : ntiles - 1;                                      \
+        const int key0_ = kt_ * AT4_KT;                                                         \
+        _Pragma("unroll") for (int i = 0; i < SCH; ++i) {                                       \
+            const int row = crow + i * 8 * NW;                                                  \
+            KR[i] = *(const a4vec *)(K + (int64_t)(key0_ + row) * 64 + ccol);                   \
+            if constexpr (PASS == 2) VR[i] = *(const a4vec *)(Vt + (int64_t)row * Tp + key0_ + ccol); \
+        }                                                                                       \
+    }
+#define ATT4_SSTORE(BUF, KR, VR)                                                                \
+    {                                                                                           \
+        _Pragma("unroll") for (int i = 0; i < SCH; ++i) {                                       \
+            const int row = crow + i * 8 * NW;                                                  \
+            *(a4vec *)(Ks + ((BUF) * AT4_KT + row) * AT4_LD + ccol) = KR[i];                    \
+            if constexpr (PASS == 2) *(a4vec *)(Vs + ((BUF) * AT4_KT + row) * AT4_LD + ccol) = VR[i]; \
+        }                                                                                       \
+    }
+    ATT4_GLOAD(0, kA, vA)
+    ATT4_SSTORE(0, kA, vA)
+    ATT4_GLOAD(1, kB, vB)  // (kB, vB): the next tile, loop-carried
+    __syncthreads();
+    for (int kt = 0; kt < ntiles; ++kt) {
+        const int buf = kt & 1;
+        a4vec kF[SCH], vF[VCH];  // tile kt + 2, requested before this tile's compute
+        ATT4_GLOAD(kt + 2, kF, vF)
+        attn4_tile<PASS>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * AT4_KT * AT4_LD, kt * AT4_KT, tab, qf, mx, sum, m,
+                         inv, o0, o1);
+        ATT4_SSTORE(buf ^ 1, kB, vB)  // (after the last tile: unread)
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < SCH; ++i) kB[i] = kF[i];
+#pragma unroll
+        for (int i = 0; i < VCH; ++i) vB[i] = vF[i];
+    }
+#undef ATT4_GLOAD
+#undef ATT4_SSTORE
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_attn_enc4(AttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+    uint16_t *tab = (uint16_t *)smraw;
+    const int tab_bytes = ((a.n_exp * 2 + 15) / 16) * 16;
+    f16 *Ks = (f16 *)(smraw + tab_bytes);      // [2][64 keys][AT4_LD]
+    f16 *Vs = Ks + 2 * AT4_KT * AT4_LD;        // [2][64 dims][AT4_LD] (V^T tile)
+    const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int64_t bh = (int64_t)b * a.H + h;
+    const f16 *Q = (const f16 *)a.q + bh * a.Tp * 64;
+    const f16 *K = (const f16 *)a.k + bh * a.Tp * 64;
+    const f16 *Vt = (const f16 *)a.vt + bh * 64 * a.Tp;
+    const int T = a.T;
+    const int q0 = (qb * NW + w) * 32;  // this wave's queries
+    half8 qf[4];
+    {
+        const int qrow = q0 + lr < a.Tp ? q0 + lr : a.Tp - 1;  // rows past T: computed, never stored
+#pragma unroll
+        for (int s = 0; s < 4; ++s) qf[s] = *(const half8 *)(Q + (int64_t)qrow * 64 + 16 * s + 8 * lh);
+    }
+    {
+        const int nch = (a.n_exp + 7) / 8;
+        const uint4 *tsrc = (const uint4 *)a.exp_tab;
+        for (int i = tid; i < nch; i += 64 * NW) ((uint4 *)tab)[i] = tsrc[i];
+    }
+    float mx = -INFINITY;
+    double sum = 0.0;
+    floatx16 o0, o1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] = 0.0f; o1[r] = 0.0f; }
+    attn4_sweep<NW, 0>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, 0.0f, 0.0f, o0, o1);
+    const float m = fmaxf(mx, __shfl_xor(mx, 32));
+    attn4_sweep<NW, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
+    const double d = sum + __shfl_xor(sum, 32);
+    const float inv = (float)(1.0 / (double)(float)d);
+    attn4_sweep<NW, 2>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, inv, o0, o1);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int t = q0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (t < T) {
+            const int64_t o = ((int64_t)b * T + t) * a.n_state + h * 64;
+            if (a.out32) {  // f32 models: the output projection takes it unrounded
+                a.out32[o + lr] = o0[r];
+                a.out32[o + 32 + lr] = o1[r];
+            } else {
+                a.out[o + lr] = f2h_bits(o0[r]);
+                a.out[o + 32 + lr] = f2h_bits(o1[r]);
+            }
+        }
+    }
+}
+
+template <int NW>
+static hipError_t attn_enc4_launch(hipStream_t s, const AttnArgs &a) {
+    const size_t tabb = ((a.n_exp * 2 + 15) / 16) * 16;
+    const size_t lds = tabb + (size_t)4 * AT4_KT * AT4_LD * 2;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    hipError_t e = allow_lds(k_attn_enc4<NW>, lds);
+    if (e != hipSuccess) return e;
+    dim3 grid(cdiv(a.T, 32 * NW), a.H, a.n_clips);
+    hipLaunchKernelGGL(k_attn_enc4<NW>, grid, dim3(64 * NW), lds, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a) {
+    const Tune &tn = tune_of(a.tune);
+    if (a.T < 1 || a.Tp % 64 || a.Tp < a.T) return hipErrorInvalidValue;
+    if (tn.enc_attn == 4) {
+        // 4 waves (128 queries) once the grid holds >= 2 workgroups per CU,
+        // else 2 (more workgroups for one clip)
+        int nw = tn.enc_attn_nw;
+        if (nw != 1 && nw != 2 && nw != 4) nw = (int64_t)cdiv(a.T, 128) * a.H * a.n_clips >= 512 ? 4 : 2;
+        if (nw == 4) return attn_enc4_launch<4>(s, a);
+        if (nw == 2) return attn_enc4_launch<2>(s, a);
+        return attn_enc4_launch<1>(s, a);
+    }
     dim3 grid(cdiv(a.T, ATT_QB), a.H, a.n_clips);
     const size_t tabb = ((a.n_exp * 2 + 15) / 16) * 16;
     const size_t obytes = (size_t)(ATT2_W - 1) * 32 * 64 * 4;
