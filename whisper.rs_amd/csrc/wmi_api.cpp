@@ -717,7 +717,9 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
     const size_t o_filt = add(filt_t.data(), filt_t.size() * 4);
     const size_t o_gelu = add(gelu.data(), gelu.size() * 2);
     std::vector<uint16_t> expneg(expt.begin() + 0x8000, expt.begin() + 0x8000 + n_exp);
-    expneg.resize((expneg.size() + 7) / 8 * 8, 0);  // whole 16-byte chunks for the LDS copy
+    // whole 16-byte chunks for the LDS copy, and always a 0 at index n_exp
+    // (k_attn_enc4 clamps its indices to it instead of masking)
+    expneg.resize((expneg.size() + 1 + 7) / 8 * 8, 0);
     const size_t o_exp = add(expneg.data(), expneg.size() * 2);
     // conv weights -> [o][tap][Cp] (implicit-GEMM B operand)
     const size_t ws = ctx->wf32 ? 4 : 2;  // bytes per matrix element (f32 files keep f32)
@@ -2554,7 +2556,14 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
     } else if (which == 2) {
         out->alg_flops = 4.0 * T * (double)T * n * B;
         out->alg_bytes = 4.0 * (double)M * n * 2;
-        snprintf(out->name, sizeof out->name, "k_attn_enc3");
+        const Tune &tn = ctx->tune;
+        if (tn.enc_attn == 4) {
+            int nw = tn.enc_attn_nw;  // as launch_attn_enc picks it
+            if (nw != 1 && nw != 2 && nw != 4) nw = (int64_t)((T + 127) / 128) * hp.n_audio_head * B >= 512 ? 4 : 2;
+            snprintf(out->name, sizeof out->name, "k_attn_enc4<%d>", nw);
+        } else {
+            snprintf(out->name, sizeof out->name, "k_attn_enc3");
+        }
     } else if (which == 14) {
         // algorithmic bytes of one decode: every step reads each decoder
         // weight, bias and LayerNorm vector once (shared by the block's rows),

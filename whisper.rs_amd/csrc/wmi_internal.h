@@ -22,6 +22,7 @@ struct MelTables {
     float c400[200], s400[200], c200[100], s200[100], c100[50], s100[50], c50[25], s50[25];
     float dc[625], ds[625];
 };
+static_assert(sizeof(MelTables) % 16 == 0, "k_mel_frames copies MelTables in 16-byte chunks");
 
 // frames -> raw log10 mel [n_mel][n_len] + per-clip ordered-uint max.
 // pcm: n_clips pointers (device) with n_samples each (device arrays).

@@ -97,10 +97,25 @@ __global__ __launch_bounds__(256) void k_mel_frames(const MelTables *__restrict_
     float *F = sm + sizeof(MelTables) / 4;
     float *scratch = F + 201 * n_mel;
     {
-        const float *src = (const float *)tabs_g;
-        float *dst = (float *)tabs;
-        for (int i = threadIdx.x; i < (int)(sizeof(MelTables) / 4); i += 256) dst[i] = src[i];
-        for (int i = threadIdx.x; i < 201 * n_mel; i += 256) F[i] = filt_t[i];
+        // tables + filterbank (~74 KB at 80 mels) -> LDS in 16-byte chunks,
+        // eight requests in flight per thread before the first store (a
+        // one-load-per-iteration copy loop waited one round trip per chunk)
+        const float4 *s1 = (const float4 *)tabs_g, *s2 = (const float4 *)filt_t;
+        float4 *dst = (float4 *)tabs;  // tabs, then F (contiguous)
+        const int n1 = (int)(sizeof(MelTables) / 16), n2 = 201 * n_mel / 4, nt = n1 + n2;
+        for (int base = threadIdx.x; base < nt; base += 256 * 8) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = base + 256 * u;
+                const int ic = i < nt ? i : nt - 1;
+                v[u] = ic < n1 ? s1[ic] : s2[ic - n1];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (base + 256 * u < nt) dst[base + 256 * u] = v[u];
+        }
+        for (int i = 4 * n2 + (int)threadIdx.x; i < 201 * n_mel; i += 256) F[i] = filt_t[i];  // (n_mel % 4 != 0)
     }
     __syncthreads();
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -709,14 +724,21 @@ constexpr int AT4_LD = 72;  // halfs per LDS row (64 + 8 pad: 144-byte rows)
 // registers; the struct uint4 arrays of the staging loop went to scratch)
 typedef uint32_t a4vec __attribute__((ext_vector_type(4)));
 
-// one 64-key tile from LDS (buffer Kb / Vb) for this wave's 32 queries
-template <int PASS>
+// one 64-key tile from LDS (buffer Kb / Vb) for this wave's 32 queries.
+// TAIL: the tile holds keys >= T (masked); full tiles skip every key test.
+// Sweep 0 keeps the max of the raw scores (scale > 0 and rounding are
+// monotone, so fl(max_raw * scale) is the max of the scaled scores); sweeps
+// 1 and 2 clamp the table index to n_exp, where the table holds a 0 (no
+// compare / select per element); scale and subtract run as packed f32 pairs.
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <int PASS, bool TAIL>
 __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, const f16 *Vb, int key0,
                                            const uint16_t *tab, const half8 (&qf)[4], float &mx, double &sum,
                                            float m, float inv, floatx16 &o0, floatx16 &o1) {
     const int lane = threadIdx.x & 63, lr = lane & 31, lh = lane >> 5;
-    const int T = a.T, n_exp = a.n_exp;
-    const float scale = a.scale;
+    const int T = a.T;
+    const uint32_t n_exp = (uint32_t)a.n_exp;
+    const f2v scale2 = {a.scale, a.scale}, m2 = {m, m};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
         floatx16 sc;
@@ -730,20 +752,25 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (key < T) mx = fmaxf(mx, sc[r] * scale);
+                if (!TAIL || key < T) mx = fmaxf(mx, sc[r]);
             }
         } else {
             half8 pa[2];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                const uint32_t i = f2h_bits(sc[r] * scale - m) & 0x7fffu;
-                // unguarded read from a clamped index (a lane-guarded LDS read
-                // becomes a branch that waits one LDS latency per element)
-                const bool ok = key < T && (int)i < n_exp;
-                const float e = h2f_bits(tab[ok ? i : 0u]) * (ok ? 1.0f : 0.0f);
-                if constexpr (PASS == 1) sum += (double)e;
-                else pa[r >> 3][r & 7] = (f16)(e * inv);
+            for (int r = 0; r < 16; r += 2) {
+                f2v v = {sc[r], sc[r + 1]};
+                v = v * scale2;
+                v = v - m2;
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int key = key0 + kb * 32 + ((r + u) & 3) + 8 * ((r + u) >> 2) + 4 * lh;
+                    uint32_t i = f2h_bits(v[u]) & 0x7fffu;
+                    i = i < n_exp ? i : n_exp;  // v_min: index n_exp holds 0
+                    if (TAIL) i = key < T ? i : n_exp;
+                    const float e = h2f_bits(tab[i]);  // unguarded read (a guarded one branches per element)
+                    if constexpr (PASS == 1) sum += (double)e;
+                    else pa[(r + u) >> 3][(r + u) & 7] = (f16)(e * inv);
+                }
             }
             if constexpr (PASS == 2) {
 #pragma unroll
@@ -809,8 +836,12 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
         const int buf = kt & 1;
         a4vec kF[SCH], vF[VCH];  // tile kt + 2, requested before this tile's compute
         ATT4_GLOAD(kt + 2, kF, vF)
-        attn4_tile<PASS>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * AT4_KT * AT4_LD, kt * AT4_KT, tab, qf, mx, sum, m,
-                         inv, o0, o1);
+        if (kt * AT4_KT + AT4_KT <= a.T)
+            attn4_tile<PASS, false>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * AT4_KT * AT4_LD, kt * AT4_KT, tab, qf, mx,
+                                    sum, m, inv, o0, o1);
+        else
+            attn4_tile<PASS, true>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * AT4_KT * AT4_LD, kt * AT4_KT, tab, qf, mx,
+                                   sum, m, inv, o0, o1);
         ATT4_SSTORE(buf ^ 1, kB, vB)  // (after the last tile: unread)
         __syncthreads();
 #pragma unroll
@@ -826,7 +857,7 @@ template <int NW>
 __global__ __launch_bounds__(64 * NW) void k_attn_enc4(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
     uint16_t *tab = (uint16_t *)smraw;
-    const int tab_bytes = ((a.n_exp * 2 + 15) / 16) * 16;
+    const int tab_bytes = (((a.n_exp + 1) * 2 + 15) / 16) * 16;
     f16 *Ks = (f16 *)(smraw + tab_bytes);      // [2][64 keys][AT4_LD]
     f16 *Vs = Ks + 2 * AT4_KT * AT4_LD;        // [2][64 dims][AT4_LD] (V^T tile)
     const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
@@ -845,7 +876,7 @@ __global__ __launch_bounds__(64 * NW) void k_attn_enc4(AttnArgs a) {
         for (int s = 0; s < 4; ++s) qf[s] = *(const half8 *)(Q + (int64_t)qrow * 64 + 16 * s + 8 * lh);
     }
     {
-        const int nch = (a.n_exp + 7) / 8;
+        const int nch = (a.n_exp + 1 + 7) / 8;  // through the 0 at index n_exp
         const uint4 *tsrc = (const uint4 *)a.exp_tab;
         for (int i = tid; i < nch; i += 64 * NW) ((uint4 *)tab)[i] = tsrc[i];
     }
@@ -855,7 +886,7 @@ __global__ __launch_bounds__(64 * NW) void k_attn_enc4(AttnArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) { o0[r] = 0.0f; o1[r] = 0.0f; }
     attn4_sweep<NW, 0>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, 0.0f, 0.0f, o0, o1);
-    const float m = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;  // max of the raw scores, scaled once
     attn4_sweep<NW, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
     const double d = sum + __shfl_xor(sum, 32);
     const float inv = (float)(1.0 / (double)(float)d);
@@ -878,7 +909,7 @@ __global__ __launch_bounds__(64 * NW) void k_attn_enc4(AttnArgs a) {
 
 template <int NW>
 static hipError_t attn_enc4_launch(hipStream_t s, const AttnArgs &a) {
-    const size_t tabb = ((a.n_exp * 2 + 15) / 16) * 16;
+    const size_t tabb = (((a.n_exp + 1) * 2 + 15) / 16) * 16;
     const size_t lds = tabb + (size_t)4 * AT4_KT * AT4_LD * 2;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     hipError_t e = allow_lds(k_attn_enc4<NW>, lds);
