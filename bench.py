@@ -167,11 +167,6 @@ def main():
     clips = [synth.synth_pcm_f32(30.0, sd) for sd in clip_seeds(rank, cpg)]
     audio_s = 30.0 * cpg
 
-    # encoder attention: at >= 4 clips per GPU the LDS-shared-K/V kernel
-    # (k_attn_enc4, 8 clips: 360 -> 242 us per layer); at 1-2 clips the
-    # 32-query kernel (k_attn_enc3, 61 vs 106-121 us at one clip).  A context
-    # knob (WMI_ENC_ATTN), recorded in the config; an explicit setting wins.
-    enc_attn = int(os.environ.setdefault("WMI_ENC_ATTN", "4" if cpg >= 4 else "3"))
     import wmi
     ctx = wmi.WhisperContext.new(path, device=local, max_clips=cpg)
     if world > 1:
@@ -259,7 +254,7 @@ def main():
                              f"per GPU: mel + conv stem + encoder + cross-KV + {args.n_decode} "
                              + (f"tokens of {args.beam}-beam search" if args.beam else "greedy tokens")),
                 "beam": args.beam,
-                "clips_per_gpu": cpg, "enc_attn": enc_attn,
+                "clips_per_gpu": cpg,
                 "global_clips": world * cpg,
                 "n_decode": args.n_decode,
                 "parallelism": f"{world} replica(s), RCCL gather of token ids" if world > 1 else "1 GPU",

@@ -11,7 +11,7 @@ import csv
 import json
 import sys
 
-KERNELS = {1: ("k_gemm", "enc_mlp0"), 2: ("k_attn_enc3", "enc_attn"), 3: ("k_gemm", "cross_kv")}
+KERNELS = {1: ("k_gemm", "enc_mlp0"), 2: ("k_attn_enc4", "enc_attn"), 3: ("k_gemm", "cross_kv")}
 CLOCK_HZ, SIMDS = 2.4e9, 1024
 
 

@@ -11,10 +11,4 @@ timeout -k 10 700 python3 -u -m pytest -x -q --timeout 300 --timeout-method thre
 tail -1 $O/r02b_tests.log
 timeout -k 10 200 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --clips-per-gpu 8 > $O/r02b_bench8.log 2>&1 || { echo "BENCH8 FAILED"; exit 1; }
 bash $R/scripts/r02_measure.sh || exit 1
-cd $R
-for cfg in "1 3 0" "1 4 4" "1 4 2" "8 4 4"; do
-  set -- $cfg
-  WMI_ENC_ATTN=$2 WMI_ENC_ATTN_NW=$3 timeout -k 10 200 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --clips-per-gpu $1 \
-    > $O/r02b_attn_c$1_v$2_nw$3.log 2>&1 || { echo "ATTN BENCH FAILED $cfg"; exit 1; }
-done
 echo "ALL DONE"

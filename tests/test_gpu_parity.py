@@ -623,15 +623,15 @@ def test_f32_model(wmi, model_cache, model, n_ctx, secs):
         om.close()
 
 
-@pytest.mark.parametrize("nw", ["2", "4"])
-def test_enc_attn4_parity_and_batch_invariance(wmi, model_cache, nw):
-    """k_attn_enc4 (WMI_ENC_ATTN=4: NW x 32-query workgroups sharing LDS K / V
-    tiles, three exact-softmax sweeps): the encoder bar against the oracle at
-    base's full 1500 frames, and a clip's result bitwise independent of the
-    batch (8 clips vs 1)."""
+@pytest.mark.parametrize("nw", ["1", "2", "4"])
+def test_enc_attn_nw_parity_and_batch_invariance(wmi, model_cache, nw):
+    """k_attn_enc4 with 1, 2 and 4 query blocks per workgroup (WMI_ENC_ATTN_NW;
+    the default picks 2 or 4 by grid size): the encoder bar against the
+    oracle at base's full 1500 frames, and a clip's result bitwise independent
+    of the batch (8 clips vs 1)."""
     path = synth.model_path("base", model_cache)
     om = pyoracle.OracleModel(path)
-    ctx = _ctx_with_env(wmi, path, {"WMI_ENC_ATTN": "4", "WMI_ENC_ATTN_NW": nw}, max_clips=8)
+    ctx = _ctx_with_env(wmi, path, {"WMI_ENC_ATTN_NW": nw}, max_clips=8)
     try:
         pcm = synth.synth_pcm_f32(30.0, 1234)
         _check_encoder(ctx, om, pcm, 1500)

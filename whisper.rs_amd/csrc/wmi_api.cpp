@@ -2055,7 +2055,6 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     knob("WMI_COOP_MAX", tn.coop_max, 1);
     knob("WMI_XATTN_ROWS", tn.xattn_rows, 0);
     knob("WMI_SELF_SPLIT", tn.self_split, 0);
-    knob("WMI_ENC_ATTN", tn.enc_attn, 3);
     knob("WMI_ENC_ATTN_NW", tn.enc_attn_nw, 0);
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;
@@ -2556,14 +2555,9 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
     } else if (which == 2) {
         out->alg_flops = 4.0 * T * (double)T * n * B;
         out->alg_bytes = 4.0 * (double)M * n * 2;
-        const Tune &tn = ctx->tune;
-        if (tn.enc_attn == 4) {
-            int nw = tn.enc_attn_nw;  // as launch_attn_enc picks it
-            if (nw != 1 && nw != 2 && nw != 4) nw = (int64_t)((T + 127) / 128) * hp.n_audio_head * B >= 512 ? 4 : 2;
-            snprintf(out->name, sizeof out->name, "k_attn_enc4<%d>", nw);
-        } else {
-            snprintf(out->name, sizeof out->name, "k_attn_enc3");
-        }
+        int nw = ctx->tune.enc_attn_nw;  // as launch_attn_enc picks it
+        if (nw != 1 && nw != 2 && nw != 4) nw = (int64_t)((T + 127) / 128) * hp.n_audio_head * B >= 512 ? 4 : 2;
+        snprintf(out->name, sizeof out->name, "k_attn_enc4<%d>", nw);
     } else if (which == 14) {
         // algorithmic bytes of one decode: every step reads each decoder
         // weight, bias and LayerNorm vector once (shared by the block's rows),

@@ -66,8 +66,7 @@ struct Tune {
     int xattn_rows = 1;     // WMI_XATTN_ROWS: beam rows share cross-attention phase A (1 auto, 2 always, 0 never)
     int self_split = 1;     // WMI_SELF_SPLIT: self-attention output projection over n / 128 WGs per head
     int graph_steps = 8;    // WMI_GRAPH_STEPS: chain decoder steps per captured graph
-    int enc_attn = 3;       // WMI_ENC_ATTN: encoder attention kernel (3: 32-query blocks, scores in registers; 4: NW x 32-query blocks sharing LDS K / V tiles, three sweeps)
-    int enc_attn_nw = 0;    // WMI_ENC_ATTN_NW: waves (32 queries each) per k_attn_enc4 workgroup (0 auto, 1, 2, 4)
+    int enc_attn_nw = 0;    // WMI_ENC_ATTN_NW: 32-query blocks (two waves each) per k_attn_enc4 workgroup (0 auto, 1, 2, 4)
 };
 extern const Tune kTuneDefault;
 inline const Tune &tune_of(const Tune *t) { return t ? *t : kTuneDefault; }

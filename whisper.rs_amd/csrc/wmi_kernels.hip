@@ -502,210 +502,13 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a) {
 }
 
 // ============================================================================
-// Encoder self-attention, ggml flash_attn_f16 semantics (masked = false).
-// One workgroup = 32 queries of one (clip, head); its 4 waves split the keys
-// in 32-key tiles.  S^T = K Q^T per tile on MFMA (keys in registers, the
-// query on the lane), so row reductions are lane-local.
-//   pass 1: row max of scale*S            (exact, as ggml_vec_max_f32)
-//   pass 2: sum of exp_tab[f16(s - max)]  (double)
-//   pass 3: P16 = f16(p * (1/sum)); O += P16 V on MFMA (P16 used straight
-//           from the S^T accumulator registers as the A operand)
-// The f16 exp table's negative half lives in LDS.
+// Encoder self-attention, ggml flash_attn_f16 semantics (masked = false):
+// S = scale * K q (f16 dot, f32), exact row max, table exp of f16(S - max),
+// double sum, P16 = f16(e * (1/sum)), O = P16 V.  (Round 1's k_attn_enc3 —
+// 8 waves splitting the keys of one 32-query block, scores in registers — is
+// in the git history; k_attn_enc4 replaced it at every batch size.)
 // ============================================================================
-constexpr int ATT_QB = 32;
-
-// Version 3: 8 waves (two per SIMD) split the 32-key tiles of one
-// 32-query block; a wave holds at most ATT2_TPW key tiles in registers.
-constexpr int ATT2_W = 8;
-constexpr int ATT2_TPW = 6;  // key tiles per wave held in registers: T <= 8 * 6 * 32 = 1536
-
-// One QK^T pass.  Each of the 8 waves holds its (<= 6) key tiles' scores
-// S = scale * K Q^T in registers (issued as 24 back-to-back MFMAs after one
-// round trip for all its K fragments), takes the row max from them (pass 1),
-// turns them into the table values e = exp_tab[f16(S - max)] kept as packed
-// f16 registers (pass 2; V tiles requested meanwhile), and multiplies
-// P16 = f16(e * (1/sum)) with V (pass 3).  (Earlier versions recomputed Q K^T
-// per pass; they are in the git history.)
-__global__ __launch_bounds__(512) void k_attn_enc3(AttnArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
-    uint16_t *tab = (uint16_t *)smraw;
-    const int tab_bytes = ((a.n_exp * 2 + 15) / 16) * 16;
-    float *red = (float *)(smraw + tab_bytes);                 // [8][32] f32
-    double *redd = (double *)(red + ATT2_W * 32);              // [8][32] f64
-    float *opart = (float *)(redd + ATT2_W * 32);              // [7][32][64] f32
-    const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int lr = lane & 31, lh = lane >> 5;
-    constexpr int TCH = 6;
-    const int nch = (a.n_exp + 7) / 8;
-    const uint4 *tsrc = (const uint4 *)a.exp_tab;
-    uint4 tch[TCH];
-#pragma unroll
-    for (int c = 0; c < TCH; ++c) {
-        const int i = tid + c * 64 * ATT2_W;
-        tch[c] = tsrc[i < nch ? i : 0];
-    }
-    const int64_t bh = (int64_t)b * a.H + h;
-    const f16 *Q = (const f16 *)a.q + bh * a.Tp * 64;
-    const f16 *K = (const f16 *)a.k + bh * a.Tp * 64;
-    const f16 *Vt = (const f16 *)a.vt + bh * 64 * a.Tp;
-    const int q0 = qb * ATT_QB;
-    const int T = a.T;
-    const float scale = a.scale;
-    const int ntiles = (T + 31) / 32;
-    half8 qf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = *(const half8 *)(Q + (int64_t)(q0 + lr) * 64 + 16 * s + 8 * lh);
-    half8 kr[ATT2_TPW][4];
-#pragma unroll
-    for (int j = 0; j < ATT2_TPW; ++j) {
-        const int kt = w + ATT2_W * j;
-        const int key0 = (kt < ntiles ? kt : ntiles - 1) * 32;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) kr[j][s] = *(const half8 *)(K + (int64_t)(key0 + lr) * 64 + 16 * s + 8 * lh);
-    }
-#pragma unroll
-    for (int c = 0; c < TCH; ++c) {
-        const int i = tid + c * 64 * ATT2_W;
-        if (i < nch) ((uint4 *)tab)[i] = tch[c];
-    }
-    for (int i = tid + TCH * 64 * ATT2_W; i < nch; i += 64 * ATT2_W) ((uint4 *)tab)[i] = tsrc[i];
-    // scores of every tile of this wave
-    floatx16 sc[ATT2_TPW];
-#pragma unroll
-    for (int j = 0; j < ATT2_TPW; ++j) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sc[j][r] = 0.0f;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) sc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kr[j][s], qf[s], sc[j], 0, 0, 0);
-    }
-    // pass 1: max of scale * S over the valid keys
-    float mx = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < ATT2_TPW; ++j) {
-        const int key0 = (w + ATT2_W * j) * 32;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            sc[j][r] = sc[j][r] * scale;
-            if (key < T) mx = fmaxf(mx, sc[j][r]);
-        }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    if (lh == 0) red[w * 32 + lr] = mx;
-    __syncthreads();  // also publishes the exp table
-    float mrow = red[lr];
-#pragma unroll
-    for (int ww = 1; ww < ATT2_W; ++ww) mrow = fmaxf(mrow, red[ww * 32 + lr]);
-    // V tiles requested now, in flight during pass 2
-    half4 vr[ATT2_TPW][8];
-#pragma unroll
-    for (int j = 0; j < ATT2_TPW; ++j) {
-        const int kt = w + ATT2_W * j;
-        const int key0 = (kt < ntiles ? kt : ntiles - 1) * 32;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-            const f16 *vrow = Vt + (int64_t)(dt * 32 + lr) * a.Tp + key0;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                vr[j][dt * 4 + s * 2] = *(const half4 *)(vrow + 16 * s + 4 * lh);
-                vr[j][dt * 4 + s * 2 + 1] = *(const half4 *)(vrow + 16 * s + 8 + 4 * lh);
-            }
-        }
-    }
-    // pass 2: e = exp_tab[f16(S - max)] (0 past T), sum in double
-    half8 ev[ATT2_TPW][2];
-    double sum = 0.0;
-#pragma unroll
-    for (int j = 0; j < ATT2_TPW; ++j) {
-        const int key0 = (w + ATT2_W * j) * 32;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            const uint32_t i = f2h_bits(sc[j][r] - mrow) & 0x7fffu;
-            const bool ok = key < T && (int)i < a.n_exp;
-            const uint16_t e = tab[ok ? i : 0u] & (ok ? 0xffffu : 0u);  // unguarded read, clamped index
-            ev[j][r >> 3][r & 7] = __builtin_bit_cast(f16, e);
-            if (key < T) sum += (double)h2f_bits(e);
-        }
-    }
-    sum += __shfl_xor(sum, 32);
-    if (lh == 0) redd[w * 32 + lr] = sum;
-    __syncthreads();
-    double dsum = redd[lr];
-#pragma unroll
-    for (int ww = 1; ww < ATT2_W; ++ww) dsum = dsum + redd[ww * 32 + lr];
-    const float sumf = (float)dsum;
-    const float inv = (float)(1.0 / (double)sumf);
-    // pass 3: O = P16 V
-    floatx16 o0, o1;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { o0[r] = 0.0f; o1[r] = 0.0f; }
-#pragma unroll
-    for (int j = 0; j < ATT2_TPW; ++j) {
-        const int kt = w + ATT2_W * j;
-        if (kt < ntiles) {
-            const int key0 = kt * 32;
-            half8 pa[2];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                const float p = key < T ? (float)ev[j][r >> 3][r & 7] * inv : 0.0f;
-                pa[r >> 3][r & 7] = (f16)p;
-            }
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const half4 v0 = vr[j][dt * 4 + s * 2], v1 = vr[j][dt * 4 + s * 2 + 1];
-                    half8 vb;
-                    vb[0] = v0[0]; vb[1] = v0[1]; vb[2] = v0[2]; vb[3] = v0[3];
-                    vb[4] = v1[0]; vb[5] = v1[1]; vb[6] = v1[2]; vb[7] = v1[3];
-                    if (dt == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[s], vb, o0, 0, 0, 0);
-                    else o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[s], vb, o1, 0, 0, 0);
-                }
-            }
-        }
-    }
-    // combine the waves' partial O in wave order
-    if (w > 0) {
-        float *op = opart + (w - 1) * 32 * 64;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int q = (r & 3) + 8 * (r >> 2) + 4 * lh;
-            op[q * 64 + lr] = o0[r];
-            op[q * 64 + 32 + lr] = o1[r];
-        }
-    }
-    __syncthreads();
-    if (w == 0) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int q = (r & 3) + 8 * (r >> 2) + 4 * lh;
-            const int t = q0 + q;
-            float v0 = o0[r], v1 = o1[r];
-#pragma unroll
-            for (int ww = 0; ww < ATT2_W - 1; ++ww) {
-                v0 = v0 + opart[ww * 2048 + q * 64 + lr];
-                v1 = v1 + opart[ww * 2048 + q * 64 + 32 + lr];
-            }
-            if (t < T) {
-                uint16_t *dst = a.out + ((int64_t)b * T + t) * a.n_state + h * 64;
-                if (a.out32) {  // f32 models: the output projection takes it unrounded
-                    float *d32 = a.out32 + ((int64_t)b * T + t) * a.n_state + h * 64;
-                    d32[lr] = v0;
-                    d32[32 + lr] = v1;
-                } else {
-                    dst[lr] = f2h_bits(v0);
-                    dst[32 + lr] = f2h_bits(v1);
-                }
-            }
-        }
-    }
-}
-
-
-// Version 4: NW waves x 32 queries per workgroup share every K / V tile
+// NW waves x 32 queries per workgroup share every K / V tile
 // through LDS (64-key tiles, double-buffered, one global->LDS copy per tile
 // for the whole workgroup instead of one per 32 queries), and the exact
 // ggml softmax is kept with three sweeps over the keys instead of holding
@@ -732,15 +535,14 @@ typedef uint32_t a4vec __attribute__((ext_vector_type(4)));
 // compare / select per element); scale and subtract run as packed f32 pairs.
 typedef float f2v __attribute__((ext_vector_type(2)));
 template <int PASS, bool TAIL>
-__device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, const f16 *Vb, int key0,
+__device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, const f16 *Vb, int key0, int kb,
                                            const uint16_t *tab, const half8 (&qf)[4], float &mx, double &sum,
                                            float m, float inv, floatx16 &o0, floatx16 &o1) {
     const int lane = threadIdx.x & 63, lr = lane & 31, lh = lane >> 5;
     const int T = a.T;
     const uint32_t n_exp = (uint32_t)a.n_exp;
     const f2v scale2 = {a.scale, a.scale}, m2 = {m, m};
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+    {  // this wave's 32-key half kb of the tile
         floatx16 sc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) sc[r] = 0.0f;
@@ -764,7 +566,9 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     const int key = key0 + kb * 32 + ((r + u) & 3) + 8 * ((r + u) >> 2) + 4 * lh;
-                    uint32_t i = f2h_bits(v[u]) & 0x7fffu;
+                    // f16(|v|) = the magnitude bits of f16(v) (v <= 0): the abs is a
+                    // free source modifier of the conversion
+                    uint32_t i = f2h_bits(fabsf(v[u]));
                     i = i < n_exp ? i : n_exp;  // v_min: index n_exp holds 0
                     if (TAIL) i = key < T ? i : n_exp;
                     const float e = h2f_bits(tab[i]);  // unguarded read (a guarded one branches per element)
@@ -805,8 +609,10 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
     const int tid = threadIdx.x;
     const int Tp = a.Tp;
     const int ntiles = (a.T + AT4_KT - 1) / AT4_KT;
-    constexpr int SCH = 512 / (64 * NW);  // 16-byte chunks per thread of an 8 KB tile
+    constexpr int NT = 128 * NW;          // threads: NW query blocks x 2 key halves
+    constexpr int SCH = 512 / NT;         // 16-byte chunks per thread of an 8 KB tile
     constexpr int VCH = PASS == 2 ? SCH : 1;
+    const int kb = (threadIdx.x >> 6) / NW;  // this wave's 32-key half of every tile
     a4vec kA[SCH], vA[VCH], kB[SCH], vB[VCH];
     // this thread's 16-byte chunks of a tile: rows (tid >> 3) + 8 NW i, column (tid & 7) * 8
     const int crow = tid >> 3, ccol = (tid & 7) * 8;
@@ -815,7 +621,7 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
         const int kt_ = (KT) < ntiles ? (KT) : ntiles - 1;                                      \
         const int key0_ = kt_ * AT4_KT;                                                         \
         _Pragma("unroll") for (int i = 0; i < SCH; ++i) {                                       \
-            const int row = crow + i * 8 * NW;                                                  \
+            const int row = crow + i * (NT / 8);                                                \
             KR[i] = *(const a4vec *)(K + (int64_t)(key0_ + row) * 64 + ccol);                   \
             if constexpr (PASS == 2) VR[i] = *(const a4vec *)(Vt + (int64_t)row * Tp + key0_ + ccol); \
         }                                                                                       \
@@ -823,7 +629,7 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
 #define ATT4_SSTORE(BUF, KR, VR)                                                                \
     {                                                                                           \
         _Pragma("unroll") for (int i = 0; i < SCH; ++i) {                                       \
-            const int row = crow + i * 8 * NW;                                                  \
+            const int row = crow + i * (NT / 8);                                                \
             *(a4vec *)(Ks + ((BUF) * AT4_KT + row) * AT4_LD + ccol) = KR[i];                    \
             if constexpr (PASS == 2) *(a4vec *)(Vs + ((BUF) * AT4_KT + row) * AT4_LD + ccol) = VR[i]; \
         }                                                                                       \
@@ -837,11 +643,11 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
         a4vec kF[SCH], vF[VCH];  // tile kt + 2, requested before this tile's compute
         ATT4_GLOAD(kt + 2, kF, vF)
         if (kt * AT4_KT + AT4_KT <= a.T)
-            attn4_tile<PASS, false>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * AT4_KT * AT4_LD, kt * AT4_KT, tab, qf, mx,
-                                    sum, m, inv, o0, o1);
+            attn4_tile<PASS, false>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * AT4_KT * AT4_LD, kt * AT4_KT, kb, tab, qf,
+                                    mx, sum, m, inv, o0, o1);
         else
-            attn4_tile<PASS, true>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * AT4_KT * AT4_LD, kt * AT4_KT, tab, qf, mx,
-                                   sum, m, inv, o0, o1);
+            attn4_tile<PASS, true>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * AT4_KT * AT4_LD, kt * AT4_KT, kb, tab, qf,
+                                   mx, sum, m, inv, o0, o1);
         ATT4_SSTORE(buf ^ 1, kB, vB)  // (after the last tile: unread)
         __syncthreads();
 #pragma unroll
@@ -853,8 +659,11 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
 #undef ATT4_SSTORE
 }
 
+// Waves w and w + NW share query block w and split every 64-key tile into
+// its two 32-key halves (twice the waves per query, for one clip's small
+// grid); their maxima, exact double sums and partial P16 V meet in LDS.
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void k_attn_enc4(AttnArgs a) {
+__global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
     uint16_t *tab = (uint16_t *)smraw;
     const int tab_bytes = (((a.n_exp + 1) * 2 + 15) / 16) * 16;
@@ -868,7 +677,8 @@ __global__ __launch_bounds__(64 * NW) void k_attn_enc4(AttnArgs a) {
     const f16 *K = (const f16 *)a.k + bh * a.Tp * 64;
     const f16 *Vt = (const f16 *)a.vt + bh * 64 * a.Tp;
     const int T = a.T;
-    const int q0 = (qb * NW + w) * 32;  // this wave's queries
+    const int qw = w % NW, kb = w / NW;  // query block, key half
+    const int q0 = (qb * NW + qw) * 32;  // this wave's queries
     half8 qf[4];
     {
         const int qrow = q0 + lr < a.Tp ? q0 + lr : a.Tp - 1;  // rows past T: computed, never stored
@@ -878,19 +688,50 @@ __global__ __launch_bounds__(64 * NW) void k_attn_enc4(AttnArgs a) {
     {
         const int nch = (a.n_exp + 1 + 7) / 8;  // through the 0 at index n_exp
         const uint4 *tsrc = (const uint4 *)a.exp_tab;
-        for (int i = tid; i < nch; i += 64 * NW) ((uint4 *)tab)[i] = tsrc[i];
+        for (int i = tid; i < nch; i += 128 * NW) ((uint4 *)tab)[i] = tsrc[i];
     }
+    // exchange slots for the key-half partner (the V buffers: unused until sweep 2)
+    float *xm = (float *)Vs;                    // [2 NW][64]
+    double *xd = (double *)(xm + 2 * NW * 64);  // [2 NW][64]
+    const int partner = kb ? w - NW : w + NW;
     float mx = -INFINITY;
     double sum = 0.0;
     floatx16 o0, o1;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { o0[r] = 0.0f; o1[r] = 0.0f; }
     attn4_sweep<NW, 0>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, 0.0f, 0.0f, o0, o1);
-    const float m = fmaxf(mx, __shfl_xor(mx, 32)) * a.scale;  // max of the raw scores, scaled once
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    xm[w * 64 + lane] = mx;
+    __syncthreads();
+    const float m = fmaxf(mx, xm[partner * 64 + lane]) * a.scale;  // max of the raw scores, scaled once
     attn4_sweep<NW, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
-    const double d = sum + __shfl_xor(sum, 32);
+    sum = sum + __shfl_xor(sum, 32);
+    xd[w * 64 + lane] = sum;
+    __syncthreads();
+    // exact double sums of f16 table values: the total is order-independent
+    const double d = kb ? xd[partner * 64 + lane] + sum : sum + xd[partner * 64 + lane];
     const float inv = (float)(1.0 / (double)(float)d);
+    __syncthreads();  // the exchange slots are V buffers again in sweep 2
     attn4_sweep<NW, 2>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, inv, o0, o1);
+    // second key half's partial O -> LDS (the K / V buffers are free now),
+    // added to the first half's in that order
+    float *xo = (float *)Ks;  // [NW][32][64]
+    if (kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int qq = (r & 3) + 8 * (r >> 2) + 4 * lh;
+            xo[(qw * 32 + qq) * 64 + lr] = o0[r];
+            xo[(qw * 32 + qq) * 64 + 32 + lr] = o1[r];
+        }
+    }
+    __syncthreads();
+    if (kb) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int qq = (r & 3) + 8 * (r >> 2) + 4 * lh;
+        o0[r] = o0[r] + xo[(qw * 32 + qq) * 64 + lr];
+        o1[r] = o1[r] + xo[(qw * 32 + qq) * 64 + 32 + lr];
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int t = q0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -915,31 +756,21 @@ static hipError_t attn_enc4_launch(hipStream_t s, const AttnArgs &a) {
     hipError_t e = allow_lds(k_attn_enc4<NW>, lds);
     if (e != hipSuccess) return e;
     dim3 grid(cdiv(a.T, 32 * NW), a.H, a.n_clips);
-    hipLaunchKernelGGL(k_attn_enc4<NW>, grid, dim3(64 * NW), lds, s, a);
+    hipLaunchKernelGGL(k_attn_enc4<NW>, grid, dim3(128 * NW), lds, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a) {
     const Tune &tn = tune_of(a.tune);
     if (a.T < 1 || a.Tp % 64 || a.Tp < a.T) return hipErrorInvalidValue;
-    if (tn.enc_attn == 4) {
-        // 4 waves (128 queries) once the grid holds >= 2 workgroups per CU,
-        // else 2 (more workgroups for one clip)
-        int nw = tn.enc_attn_nw;
-        if (nw != 1 && nw != 2 && nw != 4) nw = (int64_t)cdiv(a.T, 128) * a.H * a.n_clips >= 512 ? 4 : 2;
-        if (nw == 4) return attn_enc4_launch<4>(s, a);
-        if (nw == 2) return attn_enc4_launch<2>(s, a);
-        return attn_enc4_launch<1>(s, a);
-    }
-    dim3 grid(cdiv(a.T, ATT_QB), a.H, a.n_clips);
-    const size_t tabb = ((a.n_exp * 2 + 15) / 16) * 16;
-    const size_t obytes = (size_t)(ATT2_W - 1) * 32 * 64 * 4;
-    const size_t lds3 = tabb + ATT2_W * 32 * 4 + ATT2_W * 32 * 8 + obytes;
-    if (lds3 > 160 * 1024 || cdiv(a.T, 32) > ATT2_W * ATT2_TPW) return hipErrorInvalidValue;  // T <= 1536
-    hipError_t e = allow_lds(k_attn_enc3, lds3);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_attn_enc3, grid, dim3(64 * ATT2_W), lds3, s, a);
-    return hipGetLastError();
+    // 4 query blocks per workgroup once the grid holds >= 2 workgroups per
+    // CU, else 2 (one clip: 52 vs 62 us at NW 2 / 4); the arithmetic per wave
+    // does not depend on NW, so a clip's result is batch-independent
+    int nw = tn.enc_attn_nw;
+    if (nw != 1 && nw != 2 && nw != 4) nw = (int64_t)cdiv(a.T, 128) * a.H * a.n_clips >= 512 ? 4 : 2;
+    if (nw == 4) return attn_enc4_launch<4>(s, a);
+    if (nw == 2) return attn_enc4_launch<2>(s, a);
+    return attn_enc4_launch<1>(s, a);
 }
 
 // ============================================================================
