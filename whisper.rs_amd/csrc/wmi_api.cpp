@@ -709,11 +709,23 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
     ctx->cks[2] = 0.0f;
     for (float f : pm.filters) ctx->cks[2] += f;  // main.rs:1689
     const size_t o_mt = add(&mt, sizeof(mt));
-    std::vector<float> filt_t((size_t)201 * C, 0.0f);
+    // [201][C] transposed filterbank, then per mel the [first, end) range of
+    // its non-zero weights (int32 pairs): k_mel_frames sums only that range —
+    // the skipped terms are exact zeros (weight 0 times a finite power), so
+    // the sequential f32 sum of main.rs:1620-1633 is unchanged
+    std::vector<float> filt_t((size_t)201 * C + 2 * (size_t)C, 0.0f);
     if ((int64_t)pm.n_filt_mel * pm.n_filt_ff < (int64_t)C * 201)
         return set_err(ctx, WMI_E_UNEXPECTED, "filterbank too small: %d x %d for %d mels", pm.n_filt_mel, pm.n_filt_ff, C);
     for (int m = 0; m < C; ++m)
         for (int k = 0; k < 201; ++k) filt_t[(size_t)k * C + m] = pm.filters[(size_t)m * 201 + k];  // main.rs:1624
+    for (int m = 0; m < C; ++m) {
+        int k0 = 201, k1 = 0;
+        for (int k = 0; k < 201; ++k)
+            if (pm.filters[(size_t)m * 201 + k] != 0.0f) { k0 = std::min(k0, k); k1 = k + 1; }
+        if (k1 == 0) k0 = 0;
+        const int32_t r[2] = {k0, k1};
+        memcpy(&filt_t[(size_t)201 * C + 2 * (size_t)m], r, 8);
+    }
     const size_t o_filt = add(filt_t.data(), filt_t.size() * 4);
     const size_t o_gelu = add(gelu.data(), gelu.size() * 2);
     std::vector<uint16_t> expneg(expt.begin() + 0x8000, expt.begin() + 0x8000 + n_exp);

@@ -95,14 +95,14 @@ __global__ __launch_bounds__(256) void k_mel_frames(const MelTables *__restrict_
     if (frame0 >= nl) return;
     MelTables *tabs = (MelTables *)sm;
     float *F = sm + sizeof(MelTables) / 4;
-    float *scratch = F + 201 * n_mel;
+    float *scratch = F + 203 * n_mel;  // after the filterbank and its per-mel ranges
     {
         // tables + filterbank (~74 KB at 80 mels) -> LDS in 16-byte chunks,
         // eight requests in flight per thread before the first store (a
         // one-load-per-iteration copy loop waited one round trip per chunk)
         const float4 *s1 = (const float4 *)tabs_g, *s2 = (const float4 *)filt_t;
         float4 *dst = (float4 *)tabs;  // tabs, then F (contiguous)
-        const int n1 = (int)(sizeof(MelTables) / 16), n2 = 201 * n_mel / 4, nt = n1 + n2;
+        const int n1 = (int)(sizeof(MelTables) / 16), n2 = 203 * n_mel / 4, nt = n1 + n2;  // + the ranges
         for (int base = threadIdx.x; base < nt; base += 256 * 8) {
             float4 v[8];
 #pragma unroll
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256) void k_mel_frames(const MelTables *__restrict_
             for (int u = 0; u < 8; ++u)
                 if (base + 256 * u < nt) dst[base + 256 * u] = v[u];
         }
-        for (int i = 4 * n2 + (int)threadIdx.x; i < 201 * n_mel; i += 256) F[i] = filt_t[i];  // (n_mel % 4 != 0)
+        for (int i = 4 * n2 + (int)threadIdx.x; i < 203 * n_mel; i += 256) F[i] = filt_t[i];  // (n_mel % 4 != 0)
     }
     __syncthreads();
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -170,9 +170,11 @@ __global__ __launch_bounds__(256) void k_mel_frames(const MelTables *__restrict_
         }
         wave_sync();
         // filterbank, clamp, log10 (main.rs:1620-1634)
+        const int *rng = (const int *)(F + 201 * n_mel);  // per mel: [first, end) of its non-zero weights
         for (int m = lane; m < n_mel; m += 64) {
             float sum = 0.0f;
-            for (int k = 0; k < 201; ++k) sum = sum + fin[k] * F[k * n_mel + m];
+            const int k0 = rng[2 * m], k1 = rng[2 * m + 1];  // outside: weight 0 -> exact +0 terms
+            for (int k = k0; k < k1; ++k) sum = sum + fin[k] * F[k * n_mel + m];
             if (sum < 1e-10f) sum = 1e-10f;
             // glibc's log10f (what Rust's f32::log10 calls) is within an ulp of
             // the correctly rounded result; the double path lands on the same
@@ -223,7 +225,7 @@ __global__ void k_mel_window(const float *mel, int64_t mel_stride, int n_mel, co
 hipError_t launch_mel_frames(hipStream_t s, const MelTables *tabs, const float *filt_t, int n_mel,
                              const float *const *pcm, const int64_t *n_samples, float *mel, int64_t mel_stride,
                              const int64_t *n_len, int64_t max_len, uint32_t *mel_max, int n_clips) {
-    const size_t lds = sizeof(MelTables) + sizeof(float) * (201 * n_mel + MEL_WAVES * MEL_SCRATCH);
+    const size_t lds = sizeof(MelTables) + sizeof(float) * (203 * n_mel + MEL_WAVES * MEL_SCRATCH);
     dim3 grid(cdiv(max_len, MEL_WAVES * MEL_FPW), n_clips);
     if (max_len <= 0) return hipSuccess;
     hipError_t e = allow_lds(k_mel_frames, lds);
