@@ -49,6 +49,34 @@ def test_two_rank_shard_and_gather(micro_model):
     np.testing.assert_array_equal(tcp.reshape(world * cpg, n_tok), full)
 
 
+def test_bench_launches_its_own_ranks():
+    """`python3 bench.py --gpus 2` without torchrun's environment starts its two
+    rank processes itself (configs[3]'s 8 clips per GPU by default), they meet
+    over the TCP rendezvous, and rank 0's line carries n_gpus 2 and the max over
+    ranks of the timed region (rank r sleeps (r + 1) * 10 ms per dry-run step)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+                        "--dry-run"], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["dry_run"] is True
+    assert res["config"]["clips_per_gpu"] == 8 and res["config"]["global_clips"] == 16
+    assert res["rendezvous"].startswith("tcp 127.0.0.1")
+    assert len(res["rank_ms"]) == 2 and res["rank_ms"][1] >= 4 * 20.0
+    assert abs(res["ms_per_step"] - max(res["rank_ms"]) / 4) < 1e-2
+    assert abs(res["value"] / (2 * 8 * 30.0 * 4 / (max(res["rank_ms"]) / 1e3)) - 1) < 1e-3
+
+
+def test_bench_launcher_fails_when_a_rank_fails():
+    """A rank that exits non-zero makes the launcher exit non-zero."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--dry-run",
+                        "--roofline-kernel", "99"], env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0
+
+
 def test_rendezvous_messages_are_data_only():
     """The TCP star carries JSON (bytes hex-tagged), never pickles."""
     import dist

@@ -284,10 +284,12 @@ def test_beam_search_tiny_en_beam5(wmi, model_cache):
         om.close()
 
 
-def test_beam_one_equals_greedy(wmi, micro_model):
-    # beam search runs on the kernel chain: compare with the chain's greedy
-    # (the persistent decoder is held to the chain by test_persistent_matches_chain)
-    ctx = _ctx_with_env(wmi, micro_model, {"WMI_PERSIST": "0"})
+@pytest.mark.parametrize("persist", ["0", "1"])
+def test_beam_one_equals_greedy(wmi, micro_model, persist):
+    """beam_size 1 == greedy, on the kernel chain (WMI_PERSIST=0) and on the
+    default path (the persistent decoder: one beam-mode launch per step against
+    the greedy launch of all steps)."""
+    ctx = _ctx_with_env(wmi, micro_model, {"WMI_PERSIST": persist})
     try:
         ctx.set_audio_ctx(64)
         ctx.pcm_to_mel_batch([synth.synth_pcm_f32(2.0, 4)])
@@ -297,6 +299,29 @@ def test_beam_one_equals_greedy(wmi, micro_model):
         np.testing.assert_array_equal(b, g)
     finally:
         ctx.close()
+
+
+def test_persistent_timeout_is_kept_and_recovered(wmi, micro_model):
+    """A persistent exchange timeout (err bit 3) in the first 8-row block must
+    survive the next block's exchange memset: with WMI_FAULT_INJECT=1 the host
+    marks block 0 as timed out, and the decode is re-run on the kernel chain —
+    same tokens as a chain-only context, one fallback counted."""
+    import struct
+    clips = [synth.synth_pcm_f32(2.0, 300 + i) for i in range(9)]  # two 8-row blocks
+    out = {}
+    for tag, env in (("inject", {"WMI_FAULT_INJECT": "1"}), ("chain", {"WMI_PERSIST": "0"})):
+        ctx = _ctx_with_env(wmi, micro_model, env, max_clips=9)
+        try:
+            ctx.set_audio_ctx(64)
+            ctx.pcm_to_mel_batch(clips)
+            ctx.encode(1, 0)
+            out[tag] = ctx.decode_greedy(10, suppress_eot=True)
+            out[tag + "_fb"] = struct.unpack("<i", ctx.debug_read(11, 4))[0]
+        finally:
+            ctx.close()
+    assert out["inject_fb"] == 1 and out["chain_fb"] == 0
+    for a, b in zip(out["inject"], out["chain"]):
+        np.testing.assert_array_equal(a, b)
 
 
 @pytest.fixture(scope="module")

@@ -284,6 +284,8 @@ struct wmi_context {
     int persist_q5 = -1;              // WMI_PERSIST_Q5: 1 always, 0 never, default when B > 1
     bool persist_logits = false;      // WMI_PERSIST_LOGITS=1: also store every step's logits (dlogits)
     int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
+    int fault_inject = 0;             // WMI_FAULT_INJECT=1 (test): mark the first persistent block as timed out
+    int n_fallbacks = 0;              // decodes re-run on the kernel chain after a persistent exchange timeout
     PersistLayer *d_players = nullptr;
     uint32_t *d_expfb = nullptr;       // exp fallback list of the persistent decoder [64] + count
     int n_expfb = 0;
@@ -1009,7 +1011,9 @@ int alloc_workspace(wmi_context *ctx) {
     ctx->dwoparts = (float *)(b + o_woparts);
     ctx->dx2 = (float *)(b + o_dx2);
     ctx->derr = (uint32_t *)(b + o_sync + sync_bytes);
-    ctx->sync_bytes = sync_bytes + 256;
+    // the error word sits past the exchange words: the per-block / per-clip
+    // exchange memsets leave it alone, every decode call clears it once
+    ctx->sync_bytes = sync_bytes;
     ctx->s_stride = (int)Smax;
     ctx->n_chunks_max = (int)Cmax;
     ctx->damax = (unsigned long long *)(b + o_amax);
@@ -1631,6 +1635,7 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
     HIPCHK(ctx, hipMemcpyAsync(ctx->dfeed, feed.data(), feed.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     if (host_tokens) host_tokens->assign((size_t)Bt * n_gen, 0);
     if (host_counts) host_counts->assign(Bt, n_gen);
+    HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));
     for (int b0 = 0; b0 < Bt; b0 += 8) {
         const int B = Bt - b0 < 8 ? Bt - b0 : 8;
         HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
@@ -1648,6 +1653,8 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
                 pa.n_steps = chunk;
                 if (ctx->d_ptrace && done_steps == 0 && b0 == 0) pa.ptrace = ctx->d_ptrace;
                 HIPCHK(ctx, launch_dec_persist(ctx->stream, pa, G));
+                if (ctx->fault_inject && b0 == 0 && done_steps == 0)  // as a stranded grid reports it
+                    HIPCHK(ctx, hipMemsetAsync(ctx->derr, 8, 1, ctx->stream));
                 if (pa.ptrace) rc = ptrace_dump(ctx, chunk);
                 else rc = 0;
             } else {
@@ -1685,6 +1692,17 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
         uint32_t err = 0;
         HIPCHK(ctx, hipMemcpyAsync(&err, ctx->derr, 4, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if ((err & 8u) && ctx->use_persist) {
+            // a persistent grid was not co-resident (the decoder assumes one
+            // context per GPU and nothing else running on it): the kernels
+            // drained through the abort word; decode again on the kernel chain
+            fprintf(stderr, "[wmi] persistent decoder exchange timed out; decoding on the kernel chain\n");
+            ++ctx->n_fallbacks;
+            ctx->use_persist = false;
+            const int r2 = run_greedy(ctx, n_gen, suppress_eot, early_stop, host_tokens, host_counts);
+            ctx->use_persist = true;
+            return r2;
+        }
         if (err) return dec_err(ctx, err);
     }
     if (ctx->trace_on) {
@@ -1733,6 +1751,7 @@ int run_ts_window(wmi_context *ctx, int clip, const std::vector<int32_t> &prompt
     HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * AMAX_SHARDS * 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->dsync, 0, ctx->sync_bytes, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));
     ctx->ts_mode = true;
     struct Reset { wmi_context *c; ~Reset() { c->ts_mode = false; } } reset{ctx};
     const int total = np + max_tokens - 1;
@@ -1865,6 +1884,7 @@ int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_st
     ctx->beam_k = K;
     ctx->beam_max_tokens = n_gen;
     struct Reset { wmi_context *c; ~Reset() { c->beam_k = 0; } } reset{ctx};
+    HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));
     for (int clip = 0; clip < Bt; ++clip) {
         HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
         HIPCHK(ctx, hipMemsetAsync(ctx->dsync, 0, ctx->sync_bytes, ctx->stream));
@@ -2044,6 +2064,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (getenv("WMI_PERSIST_LOGITS")) ctx->persist_logits = true;
     if (const char *e = getenv("WMI_PERSIST_Q5")) ctx->persist_q5 = atoi(e) ? 1 : 0;
     if (const char *c = getenv("WMI_CHECKSUMS")) ctx->checksums = atoi(c) != 0;
+    if (const char *c = getenv("WMI_FAULT_INJECT")) ctx->fault_inject = atoi(c);
     ctx->dec_layers = ctx->hp.n_text_layer;
     if (const char *c = getenv("WMI_DEC_LAYERS")) ctx->dec_layers = std::max(1, std::min(atoi(c), ctx->hp.n_text_layer));
     if (getenv("WMI_PTRACE")) {
@@ -2336,6 +2357,7 @@ static int wmi_decode_logits_impl(wmi_context *ctx, int clip, const int32_t *tok
     HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * AMAX_SHARDS * 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->dsync, 0, ctx->sync_bytes, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));
     const size_t V = ctx->hp.n_vocab;
     const int G = persist_grid_for(ctx, 1);
     if (G > 0) HIPCHK(ctx, hipMemsetAsync(ctx->d_xg, 0, ctx->xg_bytes, ctx->stream));
@@ -2344,6 +2366,7 @@ static int wmi_decode_logits_impl(wmi_context *ctx, int clip, const int32_t *tok
             PersistArgs pa = persist_args(ctx, clip, 1, G, n_tokens, n_tokens, 0, 1);
             pa.n_steps = 1;
             pa.logits_out = ctx->dlogits;
+            pa.out_stride = 0;  // teacher forcing: record no token (dtokens holds staged results)
             HIPCHK(ctx, launch_dec_persist(ctx->stream, pa, G));
         } else {
             rc = run_dec_steps(ctx, clip, 1, n_tokens, n_tokens, 0, 1, i, 1);
@@ -2622,6 +2645,11 @@ int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes) {
             const int32_t v[9] = {t.logits_cap, t.logits_g, t.logits_cap2, t.down_nw1_b, t.gemv_nw,
                                   t.coop_max, t.xattn_rows, t.self_split, t.graph_steps};
             memcpy(out, v, std::min(sizeof v, bytes));
+            return WMI_OK;
+        }
+        case 11: {  // host: decodes re-run on the kernel chain after a persistent exchange timeout
+            const int32_t v = ctx->n_fallbacks;
+            memcpy(out, &v, std::min(sizeof v, bytes));
             return WMI_OK;
         }
         default: return WMI_E_INVALID_ARG;
