@@ -1513,17 +1513,17 @@ int ptrace_dump(wmi_context *ctx, int steps) {
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     HIPCHK(ctx, hipMemcpy(t.data(), ctx->d_ptrace, t.size() * 8, hipMemcpyDeviceToHost));
     auto at = [&](int st, int l, int k, int w) { return t[(((size_t)st * (L + 1) + l) * 32 + k) * 2 + w]; };
-    static const char *nm[11] = {"A qkv", "B self", "C wo", "D xq", "E xscore", "F xpv", "G1 xred", "G2 wco", "H mlp0", "I mlp1", "logits"};
+    static const char *nm[12] = {"A qkv", "B self", "C wo", "D xq", "E xscore", "F1 xexp", "F2 xpv", "G1 xred", "G2 wco", "H mlp0", "I mlp1", "logits"};
     for (int w = 0; w < 2; ++w) {
-        double ph[11] = {0}, pw[11] = {0}, tot = 0;
+        double ph[12] = {0}, pw[12] = {0}, tot = 0;
         int ns = 0;
         for (int st = 1; st < steps; ++st) {  // step 0 includes the launch
             unsigned long long prev = at(st - 1, L, 0, w);
             const unsigned long long s0 = prev;
             for (int l = 0; l <= L; ++l)
-                for (int k = 0; k < (l < L ? 10 : 1); ++k) {
+                for (int k = 0; k < (l < L ? 11 : 1); ++k) {
                     const unsigned long long v = at(st, l, k, w), pd = at(st, l, 16 + k, w);
-                    const int kk = l < L ? k : 10;
+                    const int kk = l < L ? k : 11;
                     ph[kk] += (double)(v - prev) * 0.01;
                     if (pd) pw[kk] += (double)((long long)pd - (long long)prev) * 0.01;  // phase start -> poll done
                     prev = v;
@@ -1534,7 +1534,7 @@ int ptrace_dump(wmi_context *ctx, int steps) {
         if (!ns) return WMI_OK;
         double l1 = 0, l2 = 0, l3 = 0;
         for (int st = 1; st < steps; ++st) {
-            const unsigned long long e = at(st, L - 1, 9, w);
+            const unsigned long long e = at(st, L - 1, 10, w);
             l1 += (double)(at(st, L, 1, w) - e) * 0.01;
             l2 += (double)(at(st, L, 2, w) - e) * 0.01;
             l3 += (double)(at(st, L, 3, w) - e) * 0.01;
@@ -1547,20 +1547,20 @@ int ptrace_dump(wmi_context *ctx, int steps) {
             fprintf(stderr, "[wmi ptrace] wg %s: shader clock %.3f GHz\n", w ? "G/2" : "0", dc / dt * 1e-9);
         }
         fprintf(stderr, "[wmi ptrace] wg %s: step %.2f us; per phase (per layer) total / until input arrived:\n", w ? "G/2" : "0", tot / ns);
-        for (int k = 0; k < 11; ++k) {
-            const double d = k < 10 ? (double)ns * L : (double)ns;
+        for (int k = 0; k < 12; ++k) {
+            const double d = k < 11 ? (double)ns * L : (double)ns;
             fprintf(stderr, "[wmi ptrace]   %-9s %6.2f / %6.2f\n", nm[k], ph[k] / d, pw[k] / d);
         }
-        // sub-phase stamps (slots 26..31, when a build sets them): time after
+        // sub-phase stamps (slots 27..31, when a build sets them): time after
         // the latest poll-done stamp of the same layer
-        for (int k = 26; k < 32; ++k) {
+        for (int k = 27; k < 32; ++k) {
             double s = 0;
             int c = 0;
             for (int st = 1; st < steps; ++st)
                 for (int l = 0; l < L; ++l) {
                     const unsigned long long v = at(st, l, k, w);
                     unsigned long long pd = 0;
-                    for (int j = 16; j < 26; ++j) {
+                    for (int j = 16; j < 27; ++j) {
                         const unsigned long long p = at(st, l, j, w);
                         if (p && p <= v && p > pd) pd = p;
                     }
@@ -1757,10 +1757,31 @@ int run_ts_window(wmi_context *ctx, int clip, const std::vector<int32_t> &prompt
     const int total = np + max_tokens - 1;
     std::vector<TsRec> rec((size_t)max_tokens);
     int n_out = max_tokens;
+    const int G = persist_grid_for(ctx, 1);
+    if (G > 0) HIPCHK(ctx, hipMemsetAsync(ctx->d_xg, 0, ctx->xg_bytes, ctx->stream));
     for (int done = 0; done < total;) {
         const int chunk = std::min(16, total - done);
-        rc = run_dec_steps(ctx, clip, 1, np, np, 0, 1, done, chunk);
-        if (rc) return rc;
+        if (G > 0) {
+            // persistent decoder, one step per launch (logits stored, no token
+            // recorded), then the timestamp sampler picks the next token into
+            // dts_tok, which the next launch feeds (cur_tok)
+            for (int i = 0; i < chunk; ++i) {
+                PersistArgs pa = persist_args(ctx, clip, 1, G, np, np, 0, 1);
+                pa.n_steps = 1;
+                pa.out_stride = 0;
+                pa.logits_out = ctx->dlogits;
+                pa.cur_tok = ctx->dts_tok;
+                HIPCHK(ctx, launch_dec_persist(ctx->stream, pa, G));
+                TsArgs ta{};
+                ta.logits = ctx->dlogits; ta.V = hp.n_vocab; ta.beg = ctx->sp.beg; ta.eot = ctx->sp.eot;
+                ta.sot = ctx->sp.sot; ta.solm = ctx->sp.solm; ta.not_ = ctx->sp.not_; ta.feed_len = np;
+                ta.max_rec = hp.n_text_ctx; ta.st = ctx->dstate; ta.tok_out = ctx->dts_tok; ta.rec = ctx->dts_rec;
+                HIPCHK(ctx, launch_ts_sample(ctx->stream, ta));
+            }
+        } else {
+            rc = run_dec_steps(ctx, clip, 1, np, np, 0, 1, done, chunk);
+            if (rc) return rc;
+        }
         done += chunk;
         const int have = done - np + 1;  // records written so far
         if (have <= 0) continue;

@@ -315,7 +315,7 @@ __host__ __device__ inline XLayout persist_layout(int n, int H, int T) {
     L.xq = o; o += R * n / 2;
     L.oc = o; o += R * n / 2;
     L.h = o; o += R * 2 * n;
-    L.s = o; o += R * H * T;
+    L.s = o; o += 2 * PX_TASKS;     // per cross-attention task: its chunk's exp sum (double as lo, hi)
     L.m = o; o += PX_TASKS;
     L.p = o; o += R * H * ((T + 127) / 128) * 64;  // 128-key P.V partials
     L.a = o; o += R * PX_GMAX * 2;

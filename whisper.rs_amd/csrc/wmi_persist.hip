@@ -50,12 +50,14 @@ namespace {
 
 constexpr int PT = 256;                 // threads per workgroup
 constexpr uint32_t PSPIN = 1u << 19;    // polls before a seam is declared dead
-constexpr int NPH = 10;                 // phases per decoder layer
+constexpr int NPH = 11;                 // phases per decoder layer
 constexpr int PMAXB = 8;                // decoder rows
 constexpr int RNMAX = 16;               // rows of an n-row GEMV per workgroup
 constexpr int SCR_BYTES = 24 * 1024;    // attention / argmax scratch in LDS
 constexpr int NKP = 4;                  // 128-key passes per cross-attention chunk (cl <= 512)
 constexpr int EXPFB = 64;               // exp fallback list entries (exp_f16_fast)
+constexpr int XS_OFF = 1024;            // cross-attention task scores / p in the LDS scratch
+constexpr int XS_BYTES = 8192;          // (workgroup tasks x keys per task x 4 B)
 
 __device__ __forceinline__ uint64_t gld(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -673,7 +675,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                                                    (float)tv[2] + pv.z, (float)tv[3] + pv.w);
                     }
                 } else {
-                    const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l - 1, 9), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
+                    const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l - 1, 10), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 16)
                 }
@@ -684,7 +686,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 }
                 ln_rows<NS>(xf, lp, xs, B, w, lane);
                 __syncthreads();
-                PSTAMP(l * 32 + 26)
+                PSTAMP(l * 32 + 27)
                 if (act)
                     S.template dot<BT>(xs, NS, B, ra0, ra1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
                         const float vn = from_next_row(v), ebn = from_next_row(eb);
@@ -897,14 +899,17 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 
             PSTAMP(l * 32 + 3)
             // ---- E: cross scores per (row, head, key chunk) ----------------
+            // the scores stay in this workgroup's LDS (task slot k of the
+            // workgroup's tasks t = wg + k G); only the chunk max is published
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 4);
                 f16 *qh = (f16 *)scr;
                 const int ntask = B * H * nch;
-                for (int t = wg; t < ntask; t += G) {
+                for (int t = wg, k = 0; t < ntask; t += G, ++k) {
                     const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
+                    float *st = (float *)(scr + XS_OFF) + k * CL;
                     const f16 *Kb = (const f16 *)a.ck + ((int64_t)l * a.Bt + a.b0 + (a.beam ? 0 : b)) * T * NS + h * 64 + (tid & 1) * 32;
                     half8 kf[NKP][4];
                     const half8 z8 = {};
@@ -956,7 +961,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                             for (int i = 0; i < 4; ++i) s = dot8(kf[p][i], *(const half8 *)(qh + (tid & 1) * 32 + 8 * i), s);
                             s = xstep<XSum, 1>(s);
                             if (key < j1) {
-                                if ((tid & 1) == 0) gput(xg + oS + (int64_t)bh * T + key, tag, __float_as_uint(s));
+                                if ((tid & 1) == 0) st[key - j0] = s;
                                 m = fmaxf(m, s);
                             }
                         }
@@ -970,16 +975,62 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }
 
             PSTAMP(l * 32 + 4)
-            // ---- F: exact softmax + P16.V partial per chunk ----------------
+            // ---- F1: exp against the global max, chunk sums ----------------
+            // the row max over every chunk of (row, head); p = ggml exp table
+            // value of f16(s - max) replaces the task's scores in LDS; the
+            // chunk's double sum of p (f16 values in [0, 1]: exact in any
+            // order) is published as two granules
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 5);
-                float *cm = (float *)scr;          // [nch]  (nch <= 64)
-                float *Sv = cm + 64;               // [T]    scores, then p
+                float *cm = (float *)(scr + XS_OFF + XS_BYTES);  // [nch <= 64]
                 const int ntask = B * H * nch;
-                for (int t = wg; t < ntask; t += G) {
+                for (int t = wg, k = 0; t < ntask; t += G, ++k) {
+                    const int c = t % nch, bh = t / nch;
+                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
+                    float *st = (float *)(scr + XS_OFF) + k * CL;
+                    __syncthreads();
+                    const bool ok = gpoll(nch, ptag(pos, L, l, 4), [=](int i) { return xg + oM + (int64_t)bh * nch + i; },
+                                          (uint32_t *)cm, abortw, a.err);
+                    if (check(ok)) return;
+                PSTAMP(l * 32 + 21)
+                    // (LDS reads issued unconditionally from clamped addresses)
+                    const float m = wave_max(cm[lane < nch ? lane : 0]);
+                    double sum = 0.0;
+#pragma unroll
+                    for (int u = 0; u < NKP; ++u) {
+                        const int key = j0 + tid + 256 * u;
+                        if (256 * u < CL) {
+                            const float sv = st[(key < j1 ? key : j1 - 1) - j0];
+                            const float pj = exp_f16_fast(sv - m, sh.expfb);
+                            if (key < j1) {
+                                sum += (double)pj;
+                                st[key - j0] = pj;
+                            }
+                        }
+                    }
+                    sum = wave_sum(sum);
+                    if (lane == 0) sh.redd[w] = sum;
+                    __syncthreads();
+                    if (tid == 0) {
+                        const double cs = ((sh.redd[0] + sh.redd[1]) + sh.redd[2]) + sh.redd[3];
+                        gput(xg + oS + 2 * t, tag, lo32(cs));
+                        gput(xg + oS + 2 * t + 1, tag, hi32(cs));
+                    }
+                }
+            }
+
+            PSTAMP(l * 32 + 5)
+            // ---- F2: P16 = f16(p / sum) . V per 128-key sub-chunk -> partials
+            {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 6);
+                uint32_t *csu = (uint32_t *)(scr + XS_OFF + XS_BYTES + 256);  // [nch][2]
+                const int ntask = B * H * nch;
+                for (int t = wg, k = 0; t < ntask; t += G, ++k) {
                     const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
+                    const float *st = (const float *)(scr + XS_OFF) + k * CL;
                     const int doct = tid & 7, jg = tid >> 3;
                     const f16 *Vb = (const f16 *)a.cv + ((int64_t)l * a.Bt + a.b0 + (a.beam ? 0 : b)) * T * NS + h * 64 + doct * 8;
                     half8 vf[NKP][4];
@@ -994,43 +1045,14 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         }
                     PREFETCH_ISSUED
                     __syncthreads();
-                    const uint32_t tg = ptag(pos, L, l, 4);
-                    const bool ok = gpoll<8>(nch + T, tg,  // T <= 2048: one round
-                                          [=](int i) {
-                                              return i < nch ? xg + oM + (int64_t)bh * nch + i
-                                                             : xg + oS + (int64_t)bh * T + (i - nch);
-                                          },
-                                          (uint32_t *)cm, abortw, a.err);
-                    // (cm[0..nch) then the scores: Sv = cm + nch; moved below)
+                    const bool ok = gpoll(2 * nch, ptag(pos, L, l, 5), [=](int i) { return xg + oS + (int64_t)bh * nch * 2 + i; },
+                                          csu, abortw, a.err);
                     if (check(ok)) return;
-                PSTAMP(l * 32 + 21)
-                    float *Sx = cm + nch;
-                    // (LDS reads are issued unconditionally from clamped
-                    // addresses and selected afterwards: a read under a lane
-                    // guard is waited for on its own, one LDS latency each)
-                    const float m = wave_max(lane < nch ? cm[lane] : -INFINITY);
-                    // exp of every score against the global max; the double
-                    // sum of <= 2048 f16 values in [0, 1] is exact in any order
-                    float sv[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const int j = tid + 256 * u;
-                        sv[u] = Sx[j < T ? j : T - 1];
-                    }
-                    double sum = 0.0;
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const int j = tid + 256 * u;
-                        const float pj = exp_f16_fast(sv[u] - m, sh.expfb);
-                        if (j < T) {
-                            sum += (double)pj;
-                            Sx[j] = pj;
-                        }
-                    }
-                    sum = wave_sum(sum);
-                    if (lane == 0) sh.redd[w] = sum;
-                    __syncthreads();
-                    const float inv = (float)(1.0 / (((sh.redd[0] + sh.redd[1]) + sh.redd[2]) + sh.redd[3]));
+                PSTAMP(l * 32 + 22)
+                    // the row's sum over its chunks (exact: any order)
+                    double tot = 0.0;
+                    for (int i = 0; i < nch; ++i) tot += mk64(csu[2 * i + 1], csu[2 * i]);
+                    const float inv = (float)(1.0 / tot);
                     // one partial per 128-key sub-chunk: the grouping of a
                     // one-row run whatever the task's chunk (CL), so results
                     // do not depend on how many rows share the launch
@@ -1046,7 +1068,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #pragma unroll
                             for (int u = 0; u < 4; ++u) {
                                 const int key = j0 + 128 * p + jg * 4 + u;
-                                sp[u] = Sx[key < j1 ? key : j1 - 1];
+                                sp[u] = st[(key < j1 ? key : j1 - 1) - j0];
                             }
                             // keys past the chunk add pj = 0 (o + 0 == o: o is never -0)
 #pragma unroll
@@ -1073,23 +1095,22 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     if (tid < 64 * nsp)
                         gput(xg + oP + ((int64_t)bh * nsub + (j0 >> 7)) * 64 + tid, tag,
                              __float_as_uint(((sh.ored[0][tid] + sh.ored[1][tid]) + sh.ored[2][tid]) + sh.ored[3][tid]));
-                    (void)Sv;
                 }
             }
 
-            PSTAMP(l * 32 + 5)
+            PSTAMP(l * 32 + 6)
             // ---- G1: chunk partials summed in chunk order -> cross o ---------
             {
                 PHASE_IDS
-                const uint32_t tag = ptag(pos, L, l, 6);
+                const uint32_t tag = ptag(pos, L, l, 7);
                 float *pp = (float *)scr;  // [nsub][64]
                 for (int t = wg; t < B * H; t += G) {
                     const int b = t / H, h = t - b * H;
                     __syncthreads();
-                    const bool ok = gpoll(nsub * 64, ptag(pos, L, l, 5), ptr_u64(xg + oP + (int64_t)t * nsub * 64),
+                    const bool ok = gpoll(nsub * 64, ptag(pos, L, l, 6), ptr_u64(xg + oP + (int64_t)t * nsub * 64),
                                           (uint32_t *)pp, abortw, a.err);
                     if (check(ok)) return;
-                PSTAMP(l * 32 + 22)
+                PSTAMP(l * 32 + 23)
                     if (tid < 64) {  // in chunk order, 8 LDS reads in flight
                         float s = 0.0f;
                         for (int c0 = 0; c0 < nsub; c0 += 8) {
@@ -1108,19 +1129,19 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 }
             }
 
-            PSTAMP(l * 32 + 6)
+            PSTAMP(l * 32 + 7)
             // ---- G2: Wco rows + residual -> x'' -------------------------
             {
                 PHASE_IDS
-                const uint32_t tag = ptag(pos, L, l, 7);
+                const uint32_t tag = ptag(pos, L, l, 8);
                 GSet<KC, 1, KS_N, Q5> S;
                 const bool act = rn0 < rn1;
                 S.load(lmat<Q5>(P.wco, P.wco5, NS * NS), P.bco, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll<PUX>(B * NS / 2, ptag(pos, L, l, 6), ptr_u64(xg + oOC), (uint32_t *)xs, abortw, a.err);
+                const bool ok = gpoll<PUX>(B * NS / 2, ptag(pos, L, l, 7), ptr_u64(xg + oOC), (uint32_t *)xs, abortw, a.err);
                 if (check(ok)) return;
-            PSTAMP(l * 32 + 23)
+            PSTAMP(l * 32 + 24)
                 if (act)
                     S.template dot<BT>(xs, NS, B, rn0, rn1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
                         if (!valid) return;
@@ -1130,11 +1151,11 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     });
             }
 
-            PSTAMP(l * 32 + 7)
+            PSTAMP(l * 32 + 8)
             // ---- H: LN2(x'') + W0 rows + GELU -> hidden ---------------------
             {
                 PHASE_IDS
-                const uint32_t tag = ptag(pos, L, l, 8);
+                const uint32_t tag = ptag(pos, L, l, 9);
                 GSet<KC, 2, KS_H, Q5> S;
                 const bool act = rh0 < rh1;
                 S.load(lmat<Q5>(P.w0, P.w05, 4 * NS * NS), P.b0, NS, rh0, rh1, slot, l16);
@@ -1142,9 +1163,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 ln_params<NS>(P.ln2_w, P.ln2_b, lp, lane);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l, 7), ptr_u64(xg + oX3), (uint32_t *)xf, abortw, a.err);
+                const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l, 8), ptr_u64(xg + oX3), (uint32_t *)xf, abortw, a.err);
                 if (check(ok)) return;
-                PSTAMP(l * 32 + 24)
+                PSTAMP(l * 32 + 25)
                 ln_rows<NS>(xf, lp, xs, B, w, lane);
                 __syncthreads();
                 PSTAMP(l * 32 + 28)
@@ -1158,19 +1179,19 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     });
             }
 
-            PSTAMP(l * 32 + 8)
+            PSTAMP(l * 32 + 9)
             // ---- I: W1 rows + residual -> next layer's x --------------------
             {
                 PHASE_IDS
-                const uint32_t tag = ptag(pos, L, l, 9);
+                const uint32_t tag = ptag(pos, L, l, 10);
                 GSet<4 * KC, 1, KS_I, Q5> S;
                 const bool act = rn0 < rn1;
                 S.load(lmat<Q5>(P.w1, P.w15, 4 * NS * NS), P.b1, 4 * NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll<PUH>(B * 2 * NS, ptag(pos, L, l, 8), ptr_u64(xg + oH), (uint32_t *)xs, abortw, a.err);
+                const bool ok = gpoll<PUH>(B * 2 * NS, ptag(pos, L, l, 9), ptr_u64(xg + oH), (uint32_t *)xs, abortw, a.err);
                 if (check(ok)) return;
-                PSTAMP(l * 32 + 25)
+                PSTAMP(l * 32 + 26)
                 if (act)
                     S.template dot<BT>(xs, 4 * NS, B, rn0, rn1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
                         if (!valid) return;
@@ -1179,7 +1200,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         gput(xg + oX1 + b * NS + row, tag, __float_as_uint(x));
                     });
             }
-            PSTAMP(l * 32 + 9)
+            PSTAMP(l * 32 + 10)
         }
 
         // ---- logits: LN_final + vocabulary rows + per-WG argmax -------------
@@ -1195,7 +1216,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             ln_params<NS>(a.dln_w, a.dln_b, lp, lane);
             PREFETCH_ISSUED
             __syncthreads();
-            const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, L - 1, 9), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
+            const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, L - 1, 10), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
             if (check(ok)) return;
                 PSTAMP(L * 32 + 16)
             ln_rows<NS>(xf, lp, xs, B, w, lane);
@@ -1430,7 +1451,8 @@ int persist_grid(int device, int n, int B, int T, int V, int *nres) {
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G) {
     if (G < 1 || G > PX_GMAX || a.B < 1 || a.B > PMAXB || a.T > 2048 || a.nch < 1 || a.nch > 64 ||
         a.cl > 128 * NKP || (int64_t)a.nch * a.cl < a.T || (int64_t)a.B * (a.n / 64) * a.nch > PX_TASKS ||
-        a.tctx > 512 || a.cl % 128 || (a.beam && a.n_steps != 1) || (a.kv_src && a.kv_src_stride < a.tctx))
+        a.tctx > 512 || a.cl % 128 || (a.beam && a.n_steps != 1) || (a.kv_src && a.kv_src_stride < a.tctx) ||
+        ((int64_t)a.B * (a.n / 64) * a.nch + G - 1) / G * a.cl * 4 > XS_BYTES)  // task scores in LDS
         return hipErrorInvalidValue;
     switch (a.n) {
         case 128: return launch_ns<128>(s, a, G);
