@@ -56,6 +56,7 @@ constexpr int RNMAX = 16;               // rows of an n-row GEMV per workgroup
 constexpr int SCR_BYTES = 24 * 1024;    // attention / argmax scratch in LDS
 constexpr int NKP = 4;                  // 128-key passes per cross-attention chunk (cl <= 512)
 constexpr int EXPFB = 64;               // exp fallback list entries (exp_f16_fast)
+constexpr int GELUFB = 128;             // GELU fallback list entries (gelu_f16_fast)
 constexpr int XS_OFF = 1024;            // cross-attention task scores / p in the LDS scratch
 constexpr int XS_BYTES = 8192;          // (workgroup tasks x keys per task x 4 B)
 
@@ -107,6 +108,16 @@ __device__ __forceinline__ const WMI_AS(1) T *glb(const T *p) {
     return (const WMI_AS(1) T *)p;
 }
 typedef const WMI_AS(4) PersistLayer ConstLayer;
+// once-per-step streams (weight chunks, cross K/V): the non-temporal policy
+// in WMI_PNT builds (MI355X_MICROARCH.md nt-weights), else the default
+template <typename T>
+__device__ __forceinline__ T sld(const T *p) {
+#ifdef WMI_PNT
+    return __builtin_nontemporal_load(glb(p));
+#else
+    return *glb(p);
+#endif
+}
 
 struct PShared {
     float xres[PMAXB][RNMAX];   // this workgroup's rows of the residual stream
@@ -116,6 +127,7 @@ struct PShared {
     unsigned long long best[4][PMAXB];
     float ored[4][64 * 4];  // per wave: up to NKP 64-float partials
     __attribute__((aligned(16))) uint32_t expfb[EXPFB];  // exp fallback list (exp_f16_fast)
+    __attribute__((aligned(16))) uint32_t gelufb[GELUFB];  // GELU fallback list (gelu_f16_fast)
     float kpart[16 * PMAXB];  // split-K GEMV: per (row, k-slice) partials of every decoder row
     int abort_;
 };
@@ -207,10 +219,10 @@ __device__ __forceinline__ void wc_zero(WChunk<Q5> &c) {
 template <bool Q5>
 __device__ __forceinline__ void wc_load(WChunk<Q5> &c, const WMat &m, int64_t e) {
     if constexpr (Q5) {
-        c.n = *glb((const uint32_t *)(m.q + e / 2));
-        c.hd = *glb(m.qd + e / 32);
+        c.n = sld((const uint32_t *)(m.q + e / 2));
+        c.hd = sld(m.qd + e / 32);
     } else {
-        c.h = *glb((const half8 *)((const f16 *)m.w + e));
+        c.h = sld((const half8 *)((const f16 *)m.w + e));
     }
 }
 // sh = e % 32 (a lane's offset inside its block: (l16 & 3) * 8)
@@ -521,6 +533,40 @@ __device__ __forceinline__ float exp_f16_fast(float arg, const uint32_t *fb) {
     return hit != 0xffffffffu ? h2f_bits((uint16_t)hit) : hv;
 }
 
+// ggml's GELU table value f16(gelu_f32(f32 x)) (ggml_init, wmi_api.cpp
+// build_tables: the same f32 expression, no contraction) computed, as for
+// exp: the f32 result rounds to the table's f16 unless it lies within 4 f32
+// ulps of an f16 rounding midpoint (where the device tanhf may round
+// differently from glibc's); those inputs (~50 of 63488 finite ones) come
+// from a list found once per context (k_gelu_fallbacks) and kept in LDS, so
+// the H phase has no dependent global table load.  Non-finite inputs read the
+// table itself (never on a real decode).
+__device__ __forceinline__ bool gelu_f16_fast_ok(uint16_t hx, uint16_t &hr) {
+    const float f = h2f_bits(hx);
+    const float r = 0.5f * f * (1.0f + tanhf(0.79788456080286535587989211986876f * f * (1.0f + 0.044715f * f * f)));
+    hr = f2h_bits(r);
+    const float hv = h2f_bits(hr);
+    const float nb = h2f_bits(r >= hv ? (uint16_t)(hr + 1) : (uint16_t)(hr - 1));
+    const float mid = 0.5f * (hv + nb);
+    const float ulp = __uint_as_float(__float_as_uint(r) & 0x7f800000u) * 1.1920928955078125e-7f;
+    return fabsf(r - mid) > 4.0f * ulp;
+}
+__device__ __forceinline__ uint16_t gelu_f16_fast(uint16_t hx, const uint32_t *fb, const uint16_t *tab) {
+    uint16_t hr;
+    if (gelu_f16_fast_ok(hx, hr)) return hr;
+    if ((hx & 0x7c00u) == 0x7c00u) return tab[hx];  // inf / nan input
+    uint32_t hit = 0xffffffffu;
+#pragma unroll
+    for (int i = 0; i < GELUFB; i += 4) {
+        const uint4 e = *(const uint4 *)(fb + i);
+        hit = (e.x >> 16) == hx ? e.x : hit;
+        hit = (e.y >> 16) == hx ? e.y : hit;
+        hit = (e.z >> 16) == hx ? e.z : hit;
+        hit = (e.w >> 16) == hx ? e.w : hit;
+    }
+    return hit != 0xffffffffu ? (uint16_t)hit : hr;
+}
+
 // Every phase re-derives its lane indices from an opaque copy of threadIdx.x
 // behind a compiler memory barrier: __syncthreads() fences only LDS, so
 // without it the compiler hoists later phases' weight loads and lane
@@ -553,6 +599,12 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     constexpr int H = NS / 64;
     constexpr int NPL = KC <= 4 ? 2 : 1;  // logits passes per register set
     constexpr bool XQF = KC <= 6;         // cross q computed inside the score tasks (registers allow)
+    // cross-attention softmax: several rows (8 clips, beam slots) split it in
+    // two small hand-offs (chunk maxima, then chunk exp sums; each task's
+    // scores stay in LDS) instead of every task sweeping its row's T scores;
+    // one row keeps the single hand-off (one seam fewer: 140.8 vs 142.2 us
+    // per base step, profiles/r03/ptrace_fsplit.log)
+    constexpr bool FSPLIT = BT > 1;
     // split-K factors of the GEMV phases (quarter-waves per row), from the
     // rows a workgroup owns at the full grid
     constexpr int KS_N = split_of(KC, rows_full(NS)), KS_I = split_of(4 * KC, rows_full(NS));
@@ -605,6 +657,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     }
     if (tid == 0) sh.abort_ = 0;
     if (tid < EXPFB) sh.expfb[tid] = a.exp_fb[tid];
+    if (tid < GELUFB) sh.gelufb[tid] = a.gelu_fb[tid];
     __syncthreads();
     auto check = [&](bool ok) -> bool {  // workgroup-uniform abort after a poll
         if (!ok) sh.abort_ = 1;
@@ -919,7 +972,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         key = key < j1 ? key : j1 - 1;
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
-                            kf[p][i] = 128 * p < CL ? *(const half8 *)(Kb + (int64_t)key * NS + 8 * i) : z8;
+                            kf[p][i] = 128 * p < CL ? sld((const half8 *)(Kb + (int64_t)key * NS + 8 * i)) : z8;
                     }
                     if constexpr (XQF) {
                         // this head's cross q from x' directly: LNc(x'_b) and
@@ -961,7 +1014,10 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                             for (int i = 0; i < 4; ++i) s = dot8(kf[p][i], *(const half8 *)(qh + (tid & 1) * 32 + 8 * i), s);
                             s = xstep<XSum, 1>(s);
                             if (key < j1) {
-                                if ((tid & 1) == 0) st[key - j0] = s;
+                                if ((tid & 1) == 0) {
+                                    if constexpr (FSPLIT) st[key - j0] = s;
+                                    else gput(xg + oS + (int64_t)bh * T + key, tag, __float_as_uint(s));
+                                }
                                 m = fmaxf(m, s);
                             }
                         }
@@ -975,6 +1031,116 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }
 
             PSTAMP(l * 32 + 4)
+            if constexpr (!FSPLIT) {
+            PSTAMP(l * 32 + 5)
+            // ---- F: exact softmax + P16.V partial per chunk ----------------
+            {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 6);  // (G1 polls the F2 tag)
+                float *cm = (float *)scr;          // [nch]  (nch <= 64)
+                float *Sv = cm + 64;               // [T]    scores, then p
+                const int ntask = B * H * nch;
+                for (int t = wg; t < ntask; t += G) {
+                    const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
+                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
+                    const int doct = tid & 7, jg = tid >> 3;
+                    const f16 *Vb = (const f16 *)a.cv + ((int64_t)l * a.Bt + a.b0 + (a.beam ? 0 : b)) * T * NS + h * 64 + doct * 8;
+                    half8 vf[NKP][4];
+                    const half8 z8 = {};
+#pragma unroll
+                    for (int p = 0; p < NKP; ++p)
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            int key = j0 + 128 * p + jg * 4 + u;
+                            key = key < j1 ? key : j1 - 1;
+                            vf[p][u] = 128 * p < CL ? sld((const half8 *)(Vb + (int64_t)key * NS)) : z8;
+                        }
+                    PREFETCH_ISSUED
+                    __syncthreads();
+                    const uint32_t tg = ptag(pos, L, l, 4);
+                    const bool ok = gpoll<8>(nch + T, tg,  // T <= 2048: one round
+                                          [=](int i) {
+                                              return i < nch ? xg + oM + (int64_t)bh * nch + i
+                                                             : xg + oS + (int64_t)bh * T + (i - nch);
+                                          },
+                                          (uint32_t *)cm, abortw, a.err);
+                    // (cm[0..nch) then the scores: Sv = cm + nch; moved below)
+                    if (check(ok)) return;
+                PSTAMP(l * 32 + 22)
+                    float *Sx = cm + nch;
+                    // (LDS reads are issued unconditionally from clamped
+                    // addresses and selected afterwards: a read under a lane
+                    // guard is waited for on its own, one LDS latency each)
+                    const float m = wave_max(lane < nch ? cm[lane] : -INFINITY);
+                    // exp of every score against the global max; the double
+                    // sum of <= 2048 f16 values in [0, 1] is exact in any order
+                    float sv[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int j = tid + 256 * u;
+                        sv[u] = Sx[j < T ? j : T - 1];
+                    }
+                    double sum = 0.0;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int j = tid + 256 * u;
+                        const float pj = exp_f16_fast(sv[u] - m, sh.expfb);
+                        if (j < T) {
+                            sum += (double)pj;
+                            Sx[j] = pj;
+                        }
+                    }
+                    sum = wave_sum(sum);
+                    if (lane == 0) sh.redd[w] = sum;
+                    __syncthreads();
+                    const float inv = (float)(1.0 / (((sh.redd[0] + sh.redd[1]) + sh.redd[2]) + sh.redd[3]));
+                    // one partial per 128-key sub-chunk: the grouping of a
+                    // one-row run whatever the task's chunk (CL), so results
+                    // do not depend on how many rows share the launch
+                    float o[NKP][8];
+#pragma unroll
+                    for (int p = 0; p < NKP; ++p)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) o[p][e] = 0.0f;
+#pragma unroll
+                    for (int p = 0; p < NKP; ++p)
+                        if (j0 + 128 * p < j1) {  // workgroup-uniform
+                            float sp[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const int key = j0 + 128 * p + jg * 4 + u;
+                                sp[u] = Sx[key < j1 ? key : j1 - 1];
+                            }
+                            // keys past the chunk add pj = 0 (o + 0 == o: o is never -0)
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const int key = j0 + 128 * p + jg * 4 + u;
+                                const float pj = key < j1 ? h2f_bits(f2h_bits(sp[u] * inv)) : 0.0f;
+#pragma unroll
+                                for (int e = 0; e < 8; ++e) o[p][e] = o[p][e] + pj * (float)vf[p][u][e];
+                            }
+                        }
+#pragma unroll
+                    for (int p = 0; p < NKP; ++p)
+                        if (j0 + 128 * p < j1)
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) o[p][e] = red_8_16_32(o[p][e]);
+                    if (lane < 8)
+#pragma unroll
+                        for (int p = 0; p < NKP; ++p)
+                            if (j0 + 128 * p < j1)
+#pragma unroll
+                                for (int e = 0; e < 8; ++e) sh.ored[w][p * 64 + lane * 8 + e] = o[p][e];
+                    __syncthreads();
+                    const int nsp = (j1 - j0 + 127) >> 7;  // sub-chunks of this task
+                    if (tid < 64 * nsp)
+                        gput(xg + oP + ((int64_t)bh * nsub + (j0 >> 7)) * 64 + tid, tag,
+                             __float_as_uint(((sh.ored[0][tid] + sh.ored[1][tid]) + sh.ored[2][tid]) + sh.ored[3][tid]));
+                    (void)Sv;
+                }
+            }
+
+            } else {
             // ---- F1: exp against the global max, chunk sums ----------------
             // the row max over every chunk of (row, head); p = ggml exp table
             // value of f16(s - max) replaces the task's scores in LDS; the
@@ -1041,7 +1207,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         for (int u = 0; u < 4; ++u) {
                             int key = j0 + 128 * p + jg * 4 + u;
                             key = key < j1 ? key : j1 - 1;
-                            vf[p][u] = 128 * p < CL ? *(const half8 *)(Vb + (int64_t)key * NS) : z8;
+                            vf[p][u] = 128 * p < CL ? sld((const half8 *)(Vb + (int64_t)key * NS)) : z8;
                         }
                     PREFETCH_ISSUED
                     __syncthreads();
@@ -1097,6 +1263,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                              __float_as_uint(((sh.ored[0][tid] + sh.ored[1][tid]) + sh.ored[2][tid]) + sh.ored[3][tid]));
                 }
             }
+
+            }  // FSPLIT
 
             PSTAMP(l * 32 + 6)
             // ---- G1: chunk partials summed in chunk order -> cross o ---------
@@ -1174,7 +1342,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         const float vn = from_next_row(v), ebn = from_next_row(eb);
                         if (!valid || (q & 1)) return;
                         const uint16_t h0 = f2h_bits(v + eb), h1 = f2h_bits(vn + ebn);
-                        const uint16_t g0 = a.gelu_tab[h0], g1 = a.gelu_tab[h1];
+                        const uint16_t g0 = gelu_f16_fast(h0, sh.gelufb, a.gelu_tab);
+                        const uint16_t g1 = gelu_f16_fast(h1, sh.gelufb, a.gelu_tab);
                         gput(xg + oH + b * (2 * NS) + row / 2, tag, (uint32_t)g0 | ((uint32_t)g1 << 16));
                     });
             }
@@ -1389,6 +1558,24 @@ __global__ void k_exp_fallbacks(const uint16_t *tab, int n_exp, uint32_t *list, 
     if (k < (uint32_t)EXPFB) list[k] = ((uint32_t)j << 16) | (j < n_exp ? tab[j] : 0u);
 }
 
+// the GELU fallback list: every finite f16 input whose f32 GELU lies too
+// close to an f16 rounding midpoint, with its table value
+__global__ void k_gelu_fallbacks(const uint16_t *tab, uint32_t *list, uint32_t *n) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > 0xffff || (j & 0x7c00) == 0x7c00) return;
+    uint16_t hr;
+    if (gelu_f16_fast_ok((uint16_t)j, hr)) return;
+    const uint32_t k = atomicAdd(n, 1u);
+    if (k < (uint32_t)GELUFB) list[k] = ((uint32_t)j << 16) | tab[j];
+}
+
+// gelu_f16_fast (with the list) against the host-built ggml GELU table, every f16 input
+__global__ void k_gelu_selftest(const uint16_t *tab, const uint32_t *fb, uint32_t *mismatch) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > 0xffff || (j & 0x7c00) == 0x7c00) return;
+    if (gelu_f16_fast((uint16_t)j, fb, tab) != tab[j]) atomicAdd(mismatch, 1u);
+}
+
 // exp_f16_fast (with the list) against the host-built ggml exp table over
 // every non-positive f16 input
 __global__ void k_persist_selftest(const uint16_t *tab, int n_exp, const uint32_t *fb, uint32_t *mismatch) {
@@ -1431,6 +1618,16 @@ hipError_t launch_exp_fallbacks(hipStream_t s, const uint16_t *exp_tab, int n_ex
 hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, const uint32_t *fb,
                                    uint32_t *mismatch) {
     hipLaunchKernelGGL(k_persist_selftest, dim3((0x7c01 + 255) / 256), dim3(256), 0, s, exp_tab, n_exp, fb, mismatch);
+    return hipGetLastError();
+}
+
+hipError_t launch_gelu_fallbacks(hipStream_t s, const uint16_t *gelu_tab, uint32_t *list, uint32_t *n) {
+    hipLaunchKernelGGL(k_gelu_fallbacks, dim3(65536 / 256), dim3(256), 0, s, gelu_tab, list, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_gelu_selftest(hipStream_t s, const uint16_t *gelu_tab, const uint32_t *fb, uint32_t *mismatch) {
+    hipLaunchKernelGGL(k_gelu_selftest, dim3(65536 / 256), dim3(256), 0, s, gelu_tab, fb, mismatch);
     return hipGetLastError();
 }
 
