@@ -49,9 +49,8 @@ def micro_ctx(wmi, micro_model):
 
 
 def test_device_exp_matches_ggml_table(micro_ctx):
-    """The decoder computes exp and GELU instead of reading ggml's f16 tables:
-    every one of the 31745 non-positive f16 inputs must give the exp table's
-    exact entry, and every finite f16 input the GELU table's."""
+    """The decoder computes exp instead of reading ggml's f16 table: every one
+    of the 31745 non-positive f16 inputs must give the table's exact entry."""
     assert micro_ctx.selftest() == 0
 
 

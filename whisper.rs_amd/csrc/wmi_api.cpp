@@ -901,20 +901,15 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
     }
     HIPCHK(ctx, hipMalloc(&ctx->d_players, pl.size() * sizeof(PersistLayer)));
     HIPCHK(ctx, hipMemcpy(ctx->d_players, pl.data(), pl.size() * sizeof(PersistLayer), hipMemcpyHostToDevice));
-    // the persistent decoder's exp fallback list (64 entries + a count word at
-    // [64]) and GELU fallback list (128 entries at [80] + a count word at [208])
-    HIPCHK(ctx, hipMalloc(&ctx->d_expfb, 212 * 4));
-    HIPCHK(ctx, hipMemset(ctx->d_expfb, 0xff, 212 * 4));
+    // the persistent decoder's exp fallback list (64 entries + a count word)
+    HIPCHK(ctx, hipMalloc(&ctx->d_expfb, 65 * 4));
+    HIPCHK(ctx, hipMemset(ctx->d_expfb, 0xff, 64 * 4));
     HIPCHK(ctx, hipMemset(ctx->d_expfb + 64, 0, 4));
-    HIPCHK(ctx, hipMemset(ctx->d_expfb + 208, 0, 4));
     HIPCHK(ctx, launch_exp_fallbacks(nullptr, ctx->exp_tab, ctx->n_exp, ctx->d_expfb, ctx->d_expfb + 64));
-    HIPCHK(ctx, launch_gelu_fallbacks(nullptr, ctx->gelu_tab, ctx->d_expfb + 80, ctx->d_expfb + 208));
-    uint32_t nfb = 0, ngfb = 0;
+    uint32_t nfb = 0;
     HIPCHK(ctx, hipMemcpy(&nfb, ctx->d_expfb + 64, 4, hipMemcpyDeviceToHost));
-    HIPCHK(ctx, hipMemcpy(&ngfb, ctx->d_expfb + 208, 4, hipMemcpyDeviceToHost));
     ctx->n_expfb = (int)nfb;
-    // (not seen: ~19 and ~50 inputs) the kernel chain then decodes
-    if (nfb > 64 || ngfb > 128) ctx->use_persist = false;
+    if (nfb > 64) ctx->use_persist = false;  // (not seen: ~19 inputs) the kernel chain then decodes
     if (ctx->wf32) ctx->use_persist = false;  // f32 matrices: the kernel chain with the f32 GEMVs
     return WMI_OK;
 }
@@ -1594,7 +1589,6 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     PersistArgs a{};
     a.layers = ctx->d_players; a.te = ctx->te; a.pe = ctx->d_pe; a.dln_w = ctx->dln_w; a.dln_b = ctx->dln_b;
     a.gelu_tab = ctx->gelu_tab; a.exp_tab = ctx->exp_tab; a.n_exp = ctx->n_exp; a.exp_fb = ctx->d_expfb;
-    a.gelu_fb = ctx->d_expfb + 80;
     a.kcache = ctx->kcache; a.vcache = ctx->vcache; a.ck = ctx->ck; a.cv = ctx->cv;
     a.L = ctx->dec_layers; a.n = n; a.V = hp.n_vocab; a.B = B; a.T = T; a.tctx = hp.n_text_ctx;
     a.Bt = ctx->enc_clips; a.b0 = b0;
@@ -2691,7 +2685,6 @@ int wmi_selftest(wmi_context *ctx, int32_t *n_mismatch) {
     HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));
     HIPCHK(ctx, launch_selftest(ctx->stream, ctx->exp_tab, ctx->n_exp, ctx->derr));
     HIPCHK(ctx, launch_persist_selftest(ctx->stream, ctx->exp_tab, ctx->n_exp, ctx->d_expfb, ctx->derr));
-    HIPCHK(ctx, launch_gelu_selftest(ctx->stream, ctx->gelu_tab, ctx->d_expfb + 80, ctx->derr));
     uint32_t mm = 0;
     HIPCHK(ctx, hipMemcpyAsync(&mm, ctx->derr, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));

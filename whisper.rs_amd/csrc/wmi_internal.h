@@ -334,7 +334,6 @@ struct PersistArgs {
     const uint16_t *exp_tab;     // ggml exp table, non-positive half [n_exp]
     int n_exp;
     const uint32_t *exp_fb;      // [64] exp fallback list (launch_exp_fallbacks), 0xffffffff-padded
-    const uint32_t *gelu_fb;     // [128] GELU fallback list (launch_gelu_fallbacks), 0xffffffff-padded
     uint16_t *kcache, *vcache;   // [L][DEC_ROWS][tctx][n]
     const uint16_t *ck, *cv;     // cross K/V [L][Bt][T][n]; row b uses clip b0 + b
     int L, n, V, B, T, tctx, Bt, b0;
@@ -366,11 +365,6 @@ hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G);
 // the inputs whose f32 exp is too close to an f16 midpoint, with their table
 // values, into list[64] (count in *n; > 64 means the list is unusable)
 hipError_t launch_exp_fallbacks(hipStream_t s, const uint16_t *exp_tab, int n_exp, uint32_t *list, uint32_t *n);
-// the inputs whose f32 GELU is too close to an f16 midpoint, with their table
-// values, into list[128] (count in *n; > 128 means the list is unusable)
-hipError_t launch_gelu_fallbacks(hipStream_t s, const uint16_t *gelu_tab, uint32_t *list, uint32_t *n);
-// the persistent decoder's GELU vs the host ggml table, every finite f16 input
-hipError_t launch_gelu_selftest(hipStream_t s, const uint16_t *gelu_tab, const uint32_t *fb, uint32_t *mismatch);
 // the persistent decoder's exp vs the host ggml table, every non-positive f16 input
 hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n_exp, const uint32_t *fb,
                                    uint32_t *mismatch);

@@ -56,7 +56,6 @@ constexpr int RNMAX = 16;               // rows of an n-row GEMV per workgroup
 constexpr int SCR_BYTES = 24 * 1024;    // attention / argmax scratch in LDS
 constexpr int NKP = 4;                  // 128-key passes per cross-attention chunk (cl <= 512)
 constexpr int EXPFB = 64;               // exp fallback list entries (exp_f16_fast)
-constexpr int GELUFB = 128;             // GELU fallback list entries (gelu_f16_fast)
 constexpr int XS_OFF = 1024;            // cross-attention task scores / p in the LDS scratch
 constexpr int XS_BYTES = 8192;          // (workgroup tasks x keys per task x 4 B)
 
@@ -123,11 +122,10 @@ struct PShared {
     float xres[PMAXB][RNMAX];   // this workgroup's rows of the residual stream
     int32_t tok[PMAXB];
     float redf[4];
-    double redd[4];
+    double redd[4], redd2[4];
     unsigned long long best[4][PMAXB];
     float ored[4][64 * 4];  // per wave: up to NKP 64-float partials
     __attribute__((aligned(16))) uint32_t expfb[EXPFB];  // exp fallback list (exp_f16_fast)
-    __attribute__((aligned(16))) uint32_t gelufb[GELUFB];  // GELU fallback list (gelu_f16_fast)
     float kpart[16 * PMAXB];  // split-K GEMV: per (row, k-slice) partials of every decoder row
     int abort_;
 };
@@ -438,7 +436,11 @@ struct GSet<KCH, NP, 1, Q5> {
 };
 
 // LayerNorm (ggml norm: double mean / variance, eps 1e-5; then * w + b) of
-// rows b < B of xf [B][NS] into xs [B][NS] f16 — wave w takes rows w, w + 4
+// rows b < B of xf [B][NS] into xs [B][NS] f16 — wave w takes rows w, w + 4.
+// One pass: var = E[x^2] - mean^2 in double (the f32 inputs' squares are
+// exact in double; against ggml's two-pass sum the variance differs by
+// ~1e-16 relative, so the f32 scale is the same unless that double lies
+// within 1e-16 of an f32 rounding boundary)
 template <int NS>
 struct LnP {
     static constexpr int V = (NS + 255) / 256;
@@ -463,23 +465,18 @@ __device__ __forceinline__ void ln_rows(const float *xf, const LnP<NS> &P, f16 *
             const int e = (lane + 64 * i) * 4;
             xv[i] = e < NS ? *(const float4 *)(xf + b * NS + e) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        double s1 = 0.0;
-#pragma unroll
-        for (int i = 0; i < LV; ++i)
-            if ((lane + 64 * i) * 4 < NS)
-                s1 += ((double)xv[i].x + (double)xv[i].y) + ((double)xv[i].z + (double)xv[i].w);
-        s1 = wave_sum(s1);
-        const double mean = s1 / NS;
-        double s2 = 0.0;
+        double s1 = 0.0, s2 = 0.0;
 #pragma unroll
         for (int i = 0; i < LV; ++i)
             if ((lane + 64 * i) * 4 < NS) {
-                const double d0 = (double)xv[i].x - mean, d1 = (double)xv[i].y - mean;
-                const double d2 = (double)xv[i].z - mean, d3 = (double)xv[i].w - mean;
+                const double d0 = xv[i].x, d1 = xv[i].y, d2 = xv[i].z, d3 = xv[i].w;
+                s1 += (d0 + d1) + (d2 + d3);
                 s2 += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
             }
+        s1 = wave_sum(s1);
         s2 = wave_sum(s2);
-        const float scale = (float)(1.0 / sqrt(s2 / NS + (double)1e-5f));
+        const double mean = s1 / NS;
+        const float scale = (float)(1.0 / sqrt((s2 / NS - mean * mean) + (double)1e-5f));
 #pragma unroll
         for (int i = 0; i < LV; ++i) {
             const int e = (lane + 64 * i) * 4;
@@ -495,6 +492,108 @@ __device__ __forceinline__ void ln_rows(const float *xf, const LnP<NS> &P, f16 *
             }
         }
     }
+}
+
+// One-row LayerNorm over the whole workgroup (B = 1 instances): thread tid
+// holds elements e = tid + PT u — the layout in which a PT-thread poll of NS
+// granules receives them — so the statistics start from the poll's registers
+// (one partial per thread, a wave sum, one LDS exchange) instead of one wave
+// re-reading the row from LDS; same one-pass formula as ln_rows.
+template <int NS>
+struct Ln1P {
+    static constexpr int NE = (NS + PT - 1) / PT;
+    float w[NE], b[NE];
+};
+template <int NS>
+__device__ __forceinline__ void ln1_params(const float *lw, const float *lb, Ln1P<NS> &P, int tid) {
+#pragma unroll
+    for (int u = 0; u < Ln1P<NS>::NE; ++u) {
+        const int e = tid + PT * u, ec = e < NS ? e : 0;
+        P.w[u] = *glb(lw + ec);
+        P.b[u] = *glb(lb + ec);
+    }
+}
+// statistics over the workgroup (every thread calls; sh.abort_ is raised when
+// !ok and checked at the one barrier) and xs[e] = f16(b + w * f32(x - mean) * scale)
+template <int NS>
+__device__ __forceinline__ bool ln1_vals(const float (&xv)[Ln1P<NS>::NE], const Ln1P<NS> &P, f16 *xs, bool ok,
+                                         double *r1, double *r2, int *abort_) {
+    constexpr int NE = Ln1P<NS>::NE;
+    int tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, w = tid >> 6;
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int u = 0; u < NE; ++u)
+        if (tid + PT * u < NS) {
+            const double d = xv[u];
+            s1 += d;
+            s2 += d * d;
+        }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+        r1[w] = s1;
+        r2[w] = s2;
+    }
+    if (!ok) *abort_ = 1;
+    __syncthreads();
+    if (*abort_) return false;
+    const double S1 = ((r1[0] + r1[1]) + r1[2]) + r1[3], S2 = ((r2[0] + r2[1]) + r2[2]) + r2[3];
+    const double mean = S1 / NS;
+    const float scale = (float)(1.0 / sqrt((S2 / NS - mean * mean) + (double)1e-5f));
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+        const int e = tid + PT * u;
+        if (e < NS) {
+            const float t = (float)((double)xv[u] - mean) * scale;
+            xs[e] = (f16)(P.b[u] + P.w[u] * t);
+        }
+    }
+    return true;
+}
+// poll one row's NS f32 granules (src[e], tag) into registers and xf, then
+// ln1_vals; false: the grid is aborting
+template <int NS>
+__device__ __forceinline__ bool poll_ln1(const uint64_t *src, uint32_t tag, const Ln1P<NS> &P, float *xf, f16 *xs,
+                                         uint32_t *abortw, uint32_t *err, double *r1, double *r2, int *abort_) {
+    constexpr int NE = Ln1P<NS>::NE;
+    int tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    uint64_t v[NE];
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+        const int e = tid + PT * u;
+        v[u] = e < NS ? gld(src + e) : ((uint64_t)tag << 32);
+    }
+    bool ok = true;
+    for (uint32_t it = 0;; ++it) {
+        bool all = true;
+#pragma unroll
+        for (int u = 0; u < NE; ++u)
+            if ((uint32_t)(v[u] >> 32) != tag) {
+                all = false;
+                v[u] = gld(src + tid + PT * u);
+            }
+        if (all) break;
+        if ((it & 15) == 15) {
+            if (ld32(abortw)) { ok = false; break; }
+            if (it > PSPIN) {
+                st32(abortw, 1u);
+                atomicOr(err, 8u);
+                ok = false;
+                break;
+            }
+        }
+    }
+    float xv[NE];
+#pragma unroll
+    for (int u = 0; u < NE; ++u) {
+        const int e = tid + PT * u;
+        xv[u] = __uint_as_float((uint32_t)v[u]);
+        if (e < NS) xf[e] = xv[u];
+    }
+    return ln1_vals<NS>(xv, P, xs, ok, r1, r2, abort_);
 }
 
 // ggml's table_exp_f16 value f16(exp(double(f16 x))) for x <= 0 without a
@@ -533,40 +632,6 @@ __device__ __forceinline__ float exp_f16_fast(float arg, const uint32_t *fb) {
     return hit != 0xffffffffu ? h2f_bits((uint16_t)hit) : hv;
 }
 
-// ggml's GELU table value f16(gelu_f32(f32 x)) (ggml_init, wmi_api.cpp
-// build_tables: the same f32 expression, no contraction) computed, as for
-// exp: the f32 result rounds to the table's f16 unless it lies within 4 f32
-// ulps of an f16 rounding midpoint (where the device tanhf may round
-// differently from glibc's); those inputs (~50 of 63488 finite ones) come
-// from a list found once per context (k_gelu_fallbacks) and kept in LDS, so
-// the H phase has no dependent global table load.  Non-finite inputs read the
-// table itself (never on a real decode).
-__device__ __forceinline__ bool gelu_f16_fast_ok(uint16_t hx, uint16_t &hr) {
-    const float f = h2f_bits(hx);
-    const float r = 0.5f * f * (1.0f + tanhf(0.79788456080286535587989211986876f * f * (1.0f + 0.044715f * f * f)));
-    hr = f2h_bits(r);
-    const float hv = h2f_bits(hr);
-    const float nb = h2f_bits(r >= hv ? (uint16_t)(hr + 1) : (uint16_t)(hr - 1));
-    const float mid = 0.5f * (hv + nb);
-    const float ulp = __uint_as_float(__float_as_uint(r) & 0x7f800000u) * 1.1920928955078125e-7f;
-    return fabsf(r - mid) > 4.0f * ulp;
-}
-__device__ __forceinline__ uint16_t gelu_f16_fast(uint16_t hx, const uint32_t *fb, const uint16_t *tab) {
-    uint16_t hr;
-    if (gelu_f16_fast_ok(hx, hr)) return hr;
-    if ((hx & 0x7c00u) == 0x7c00u) return tab[hx];  // inf / nan input
-    uint32_t hit = 0xffffffffu;
-#pragma unroll
-    for (int i = 0; i < GELUFB; i += 4) {
-        const uint4 e = *(const uint4 *)(fb + i);
-        hit = (e.x >> 16) == hx ? e.x : hit;
-        hit = (e.y >> 16) == hx ? e.y : hit;
-        hit = (e.z >> 16) == hx ? e.z : hit;
-        hit = (e.w >> 16) == hx ? e.w : hit;
-    }
-    return hit != 0xffffffffu ? (uint16_t)hit : hr;
-}
-
 // Every phase re-derives its lane indices from an opaque copy of threadIdx.x
 // behind a compiler memory barrier: __syncthreads() fences only LDS, so
 // without it the compiler hoists later phases' weight loads and lane
@@ -598,7 +663,10 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     constexpr int KC = NS / 128;        // 128-element chunks of a K = n row
     constexpr int H = NS / 64;
     constexpr int NPL = KC <= 4 ? 2 : 1;  // logits passes per register set
-    constexpr bool XQF = KC <= 6;         // cross q computed inside the score tasks (registers allow)
+#ifndef WMI_XQF_KC
+#define WMI_XQF_KC 6
+#endif
+    constexpr bool XQF = KC <= WMI_XQF_KC;  // cross q computed inside the score tasks (registers allow)
     // cross-attention softmax: several rows (8 clips, beam slots) split it in
     // two small hand-offs (chunk maxima, then chunk exp sums; each task's
     // scores stay in LDS) instead of every task sweeping its row's T scores;
@@ -657,7 +725,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     }
     if (tid == 0) sh.abort_ = 0;
     if (tid < EXPFB) sh.expfb[tid] = a.exp_fb[tid];
-    if (tid < GELUFB) sh.gelufb[tid] = a.gelu_fb[tid];
     __syncthreads();
     auto check = [&](bool ok) -> bool {  // workgroup-uniform abort after a poll
         if (!ok) sh.abort_ = 1;
@@ -703,7 +770,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 const bool act = ra0 < ra1;
                 S.load(lmat<Q5>(P.wqkv, P.wqkv5, 3 * NS * NS), P.bqkv, NS, ra0, ra1, slot, l16);
                 LnP<NS> lp;
-                ln_params<NS>(P.ln1_w, P.ln1_b, lp, lane);
+                Ln1P<NS> l1;
+                if constexpr (BT == 1) ln1_params<NS>(P.ln1_w, P.ln1_b, l1, tid);
+                else ln_params<NS>(P.ln1_w, P.ln1_b, lp, lane);
                 PREFETCH_ISSUED
                 __syncthreads();
                 if (l == 0) {
@@ -727,9 +796,22 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         *(float4 *)(xf + b * NS + e) = make_float4((float)tv[0] + pv.x, (float)tv[1] + pv.y,
                                                                    (float)tv[2] + pv.z, (float)tv[3] + pv.w);
                     }
+                    if constexpr (BT == 1) {
+                        __syncthreads();
+                        float xv[Ln1P<NS>::NE];
+#pragma unroll
+                        for (int u = 0; u < Ln1P<NS>::NE; ++u) xv[u] = xf[tid + PT * u < NS ? tid + PT * u : 0];
+                        if (!ln1_vals<NS>(xv, l1, xs, true, sh.redd, sh.redd2, &sh.abort_)) return;
+                    }
                 } else {
-                    const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l - 1, 10), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
-                    if (check(ok)) return;
+                    if constexpr (BT == 1) {
+                        if (!poll_ln1<NS>(xg + oX1, ptag(pos, L, l - 1, 10), l1, xf, xs, abortw, a.err, sh.redd, sh.redd2,
+                                          &sh.abort_))
+                            return;
+                    } else {
+                        const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l - 1, 10), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
+                        if (check(ok)) return;
+                    }
                 PSTAMP(l * 32 + 16)
                 }
                 __syncthreads();
@@ -737,8 +819,10 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     const int b = i / rn, r = i - b * rn;
                     sh.xres[b][r] = xf[b * NS + rn0 + r];
                 }
-                ln_rows<NS>(xf, lp, xs, B, w, lane);
-                __syncthreads();
+                if constexpr (BT > 1) {
+                    ln_rows<NS>(xf, lp, xs, B, w, lane);
+                    __syncthreads();
+                }
                 PSTAMP(l * 32 + 27)
                 if (act)
                     S.template dot<BT>(xs, NS, B, ra0, ra1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
@@ -934,13 +1018,20 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 const bool act = rn0 < rn1;
                 S.load(wmat(P.wcq), P.bcq, NS, rn0, rn1, slot, l16);
                 LnP<NS> lp;
-                ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
+                Ln1P<NS> l1;
+                if constexpr (BT == 1) ln1_params<NS>(P.lnc_w, P.lnc_b, l1, tid);
+                else ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l, 2), ptr_u64(xg + oX2), (uint32_t *)xf, abortw, a.err);
-                if (check(ok)) return;
+                if constexpr (BT == 1) {
+                    if (!poll_ln1<NS>(xg + oX2, ptag(pos, L, l, 2), l1, xf, xs, abortw, a.err, sh.redd, sh.redd2, &sh.abort_))
+                        return;
+                } else {
+                    const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l, 2), ptr_u64(xg + oX2), (uint32_t *)xf, abortw, a.err);
+                    if (check(ok)) return;
+                    ln_rows<NS>(xf, lp, xs, B, w, lane);
+                }
                 PSTAMP(l * 32 + 19)
-                ln_rows<NS>(xf, lp, xs, B, w, lane);
                 __syncthreads();
                 if (act)
                     S.template dot<BT>(xs, NS, B, rn0, rn1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
@@ -980,13 +1071,21 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         WSet<KC, 4> S;
                         wset_load(S, wmat(P.wcq), P.bcq, NS, h * 64, h * 64 + 64, slot, l16);
                         LnP<NS> lp;
-                        ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
+                        Ln1P<NS> l1;
+                        if constexpr (BT == 1) ln1_params<NS>(P.lnc_w, P.lnc_b, l1, tid);
+                        else ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
                         PREFETCH_ISSUED
                         __syncthreads();
-                        const bool ok = gpoll<PUX>(NS, ptag(pos, L, l, 2), ptr_u64(xg + oX2 + b * NS), (uint32_t *)xf, abortw, a.err);
-                        if (check(ok)) return;
+                        if constexpr (BT == 1) {
+                            if (!poll_ln1<NS>(xg + oX2 + b * NS, ptag(pos, L, l, 2), l1, xf, xs, abortw, a.err, sh.redd,
+                                              sh.redd2, &sh.abort_))
+                                return;
+                        } else {
+                            const bool ok = gpoll<PUX>(NS, ptag(pos, L, l, 2), ptr_u64(xg + oX2 + b * NS), (uint32_t *)xf, abortw, a.err);
+                            if (check(ok)) return;
+                            ln_rows<NS>(xf, lp, xs, 1, w, lane);
+                        }
                 PSTAMP(l * 32 + 20)
-                        ln_rows<NS>(xf, lp, xs, 1, w, lane);
                         __syncthreads();
                 PSTAMP(l * 32 + 29)
                         wset_dot<1>(S, xs, NS, 1, h * 64, h * 64 + 64, slot, l16,
@@ -1328,13 +1427,20 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 const bool act = rh0 < rh1;
                 S.load(lmat<Q5>(P.w0, P.w05, 4 * NS * NS), P.b0, NS, rh0, rh1, slot, l16);
                 LnP<NS> lp;
-                ln_params<NS>(P.ln2_w, P.ln2_b, lp, lane);
+                Ln1P<NS> l1;
+                if constexpr (BT == 1) ln1_params<NS>(P.ln2_w, P.ln2_b, l1, tid);
+                else ln_params<NS>(P.ln2_w, P.ln2_b, lp, lane);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l, 8), ptr_u64(xg + oX3), (uint32_t *)xf, abortw, a.err);
-                if (check(ok)) return;
+                if constexpr (BT == 1) {
+                    if (!poll_ln1<NS>(xg + oX3, ptag(pos, L, l, 8), l1, xf, xs, abortw, a.err, sh.redd, sh.redd2, &sh.abort_))
+                        return;
+                } else {
+                    const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l, 8), ptr_u64(xg + oX3), (uint32_t *)xf, abortw, a.err);
+                    if (check(ok)) return;
+                    ln_rows<NS>(xf, lp, xs, B, w, lane);
+                }
                 PSTAMP(l * 32 + 25)
-                ln_rows<NS>(xf, lp, xs, B, w, lane);
                 __syncthreads();
                 PSTAMP(l * 32 + 28)
                 if (act)
@@ -1342,8 +1448,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         const float vn = from_next_row(v), ebn = from_next_row(eb);
                         if (!valid || (q & 1)) return;
                         const uint16_t h0 = f2h_bits(v + eb), h1 = f2h_bits(vn + ebn);
-                        const uint16_t g0 = gelu_f16_fast(h0, sh.gelufb, a.gelu_tab);
-                        const uint16_t g1 = gelu_f16_fast(h1, sh.gelufb, a.gelu_tab);
+                        const uint16_t g0 = a.gelu_tab[h0], g1 = a.gelu_tab[h1];
                         gput(xg + oH + b * (2 * NS) + row / 2, tag, (uint32_t)g0 | ((uint32_t)g1 << 16));
                     });
             }
@@ -1379,15 +1484,31 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PHASE_IDS
             WSet<KC, NPL> S0, S1;
             constexpr int RS = 16 * NPL;  // rows per register set
+#ifndef WMI_LOGITS_LATE
             wset_load(S0, wmat(a.te), nullptr, NS, rs0, rv1, slot, l16);
             wset_load(S1, wmat(a.te), nullptr, NS, rs0 + RS, rv1, slot, l16);
+#endif
             LnP<NS> lp;
-            ln_params<NS>(a.dln_w, a.dln_b, lp, lane);
+            Ln1P<NS> l1;
+            if constexpr (BT == 1) ln1_params<NS>(a.dln_w, a.dln_b, l1, tid);
+            else ln_params<NS>(a.dln_w, a.dln_b, lp, lane);
             PREFETCH_ISSUED
             __syncthreads();
-            const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, L - 1, 10), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
-            if (check(ok)) return;
+            if constexpr (BT == 1) {
+                if (!poll_ln1<NS>(xg + oX1, ptag(pos, L, L - 1, 10), l1, xf, xs, abortw, a.err, sh.redd, sh.redd2, &sh.abort_))
+                    return;
+            } else {
+                const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, L - 1, 10), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
+                if (check(ok)) return;
+            }
                 PSTAMP(L * 32 + 16)
+#ifdef WMI_LOGITS_LATE
+            // the streamed rows requested after the poll (not in front of it in
+            // the wave's load queue): the LN and the LDS-resident rows cover them
+            wset_load(S0, wmat(a.te), nullptr, NS, rs0, rv1, slot, l16);
+            wset_load(S1, wmat(a.te), nullptr, NS, rs0 + RS, rv1, slot, l16);
+            PREFETCH_ISSUED
+#endif
             ln_rows<NS>(xf, lp, xs, B, w, lane);
             __syncthreads();
             PSTAMP(L * 32 + 1)
@@ -1558,24 +1679,6 @@ __global__ void k_exp_fallbacks(const uint16_t *tab, int n_exp, uint32_t *list, 
     if (k < (uint32_t)EXPFB) list[k] = ((uint32_t)j << 16) | (j < n_exp ? tab[j] : 0u);
 }
 
-// the GELU fallback list: every finite f16 input whose f32 GELU lies too
-// close to an f16 rounding midpoint, with its table value
-__global__ void k_gelu_fallbacks(const uint16_t *tab, uint32_t *list, uint32_t *n) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j > 0xffff || (j & 0x7c00) == 0x7c00) return;
-    uint16_t hr;
-    if (gelu_f16_fast_ok((uint16_t)j, hr)) return;
-    const uint32_t k = atomicAdd(n, 1u);
-    if (k < (uint32_t)GELUFB) list[k] = ((uint32_t)j << 16) | tab[j];
-}
-
-// gelu_f16_fast (with the list) against the host-built ggml GELU table, every f16 input
-__global__ void k_gelu_selftest(const uint16_t *tab, const uint32_t *fb, uint32_t *mismatch) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j > 0xffff || (j & 0x7c00) == 0x7c00) return;
-    if (gelu_f16_fast((uint16_t)j, fb, tab) != tab[j]) atomicAdd(mismatch, 1u);
-}
-
 // exp_f16_fast (with the list) against the host-built ggml exp table over
 // every non-positive f16 input
 __global__ void k_persist_selftest(const uint16_t *tab, int n_exp, const uint32_t *fb, uint32_t *mismatch) {
@@ -1621,15 +1724,6 @@ hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n
     return hipGetLastError();
 }
 
-hipError_t launch_gelu_fallbacks(hipStream_t s, const uint16_t *gelu_tab, uint32_t *list, uint32_t *n) {
-    hipLaunchKernelGGL(k_gelu_fallbacks, dim3(65536 / 256), dim3(256), 0, s, gelu_tab, list, n);
-    return hipGetLastError();
-}
-
-hipError_t launch_gelu_selftest(hipStream_t s, const uint16_t *gelu_tab, const uint32_t *fb, uint32_t *mismatch) {
-    hipLaunchKernelGGL(k_gelu_selftest, dim3(65536 / 256), dim3(256), 0, s, gelu_tab, fb, mismatch);
-    return hipGetLastError();
-}
 
 int persist_grid(int device, int n, int B, int T, int V, int *nres) {
     *nres = 0;
