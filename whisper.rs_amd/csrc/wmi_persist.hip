@@ -1509,7 +1509,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             wset_load(S1, wmat(a.te), nullptr, NS, rs0 + RS, rv1, slot, l16);
             PREFETCH_ISSUED
 #endif
-            ln_rows<NS>(xf, lp, xs, B, w, lane);
+            if constexpr (BT > 1) ln_rows<NS>(xf, lp, xs, B, w, lane);
             __syncthreads();
             PSTAMP(L * 32 + 1)
             unsigned long long best = 0ull;
