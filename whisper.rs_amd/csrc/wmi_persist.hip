@@ -632,6 +632,30 @@ __device__ __forceinline__ float exp_f16_fast(float arg, const uint32_t *fb) {
     return hit != 0xffffffffu ? h2f_bits((uint16_t)hit) : hv;
 }
 
+// Cross-attention task of workgroup slot s (a workgroup takes slots wg,
+// wg + G, ...; -1: no task).  When they fit in one round of the grid, the
+// nch chunk tasks of one (row, head) take slots of one residue mod 8 — one
+// XCD under the observed round-robin placement (speed only, never
+// correctness) — so the nch workgroups that each read the head's 64 cross-q
+// weight rows (E, XQF) share one L2; otherwise task = slot.
+__device__ __forceinline__ int xtask(int s, int nch, int BH, int G) {
+#ifdef WMI_NO_XCDMAP
+    return s < BH * nch ? s : -1;
+#endif
+    const int S = 8 * nch * ((BH + 7) >> 3);
+    if (S > G) return s < BH * nch ? s : -1;
+    const int x = s & 7, k = s >> 3, kq = k / nch;
+    const int g = x + 8 * kq;
+    return s < S && g < BH ? g * nch + (k - kq * nch) : -1;
+}
+__device__ __forceinline__ int xslots(int nch, int BH, int G) {
+#ifdef WMI_NO_XCDMAP
+    return BH * nch;
+#endif
+    const int S = 8 * nch * ((BH + 7) >> 3);
+    return S > G ? BH * nch : S;
+}
+
 // Every phase re-derives its lane indices from an opaque copy of threadIdx.x
 // behind a compiler memory barrier: __syncthreads() fences only LDS, so
 // without it the compiler hoists later phases' weight loads and lane
@@ -883,15 +907,25 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     for (int r = 0; r < 2; ++r) {
                         const int j = tid + 256 * r;
                         const uint32_t off = (uint32_t)((((int64_t)srk[r] * tctx + j) * NS + h * 64) * 2);
+#ifdef WMI_EXP_NOKV  // timing diagnostic only: no cache reads (wrong results)
+                        (void)off;
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) kv[r][i] = z8;
+#else
 #pragma unroll
                         for (int i = 0; i < 8; ++i) kv[r][i] = j < pos ? bload_sc1(rk, off + 16 * i) : z8;
+#endif
                     }
                     // value rows j < pos, in flight across the poll as well
                     half8 vv[16];
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
                         const int j = jg + 32 * i;
+#ifdef WMI_EXP_NOKV
+                        vv[i] = z8;
+#else
                         vv[i] = j < pos ? bload_sc1(rv, (uint32_t)((((int64_t)srv[i] * tctx + j) * NS + h * 64 + doct * 8) * 2)) : z8;
+#endif
                     }
                     PREFETCH_ISSUED
                     __syncthreads();
@@ -1049,11 +1083,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 4);
                 f16 *qh = (f16 *)scr;
-                const int ntask = B * H * nch;
-                for (int t = wg, k = 0; t < ntask; t += G, ++k) {
+                const int nslot = xslots(nch, B * H, G);
+                for (int s = wg, k = 0; s < nslot; s += G) {
+                    const int t = xtask(s, nch, B * H, G);
+                    if (t < 0) continue;  // (workgroup-uniform)
                     const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
-                    float *st = (float *)(scr + XS_OFF) + k * CL;
+                    float *st = (float *)(scr + XS_OFF) + (k++) * CL;
                     const f16 *Kb = (const f16 *)a.ck + ((int64_t)l * a.Bt + a.b0 + (a.beam ? 0 : b)) * T * NS + h * 64 + (tid & 1) * 32;
                     half8 kf[NKP][4];
                     const half8 z8 = {};
@@ -1138,8 +1174,10 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 const uint32_t tag = ptag(pos, L, l, 6);  // (G1 polls the F2 tag)
                 float *cm = (float *)scr;          // [nch]  (nch <= 64)
                 float *Sv = cm + 64;               // [T]    scores, then p
-                const int ntask = B * H * nch;
-                for (int t = wg; t < ntask; t += G) {
+                const int nslot = xslots(nch, B * H, G);
+                for (int s = wg; s < nslot; s += G) {
+                    const int t = xtask(s, nch, B * H, G);
+                    if (t < 0) continue;
                     const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
                     const int doct = tid & 7, jg = tid >> 3;
@@ -1249,11 +1287,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 5);
                 float *cm = (float *)(scr + XS_OFF + XS_BYTES);  // [nch <= 64]
-                const int ntask = B * H * nch;
-                for (int t = wg, k = 0; t < ntask; t += G, ++k) {
+                const int nslot = xslots(nch, B * H, G);
+                for (int s = wg, k = 0; s < nslot; s += G) {
+                    const int t = xtask(s, nch, B * H, G);
+                    if (t < 0) continue;
                     const int c = t % nch, bh = t / nch;
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
-                    float *st = (float *)(scr + XS_OFF) + k * CL;
+                    float *st = (float *)(scr + XS_OFF) + (k++) * CL;
                     __syncthreads();
                     const bool ok = gpoll(nch, ptag(pos, L, l, 4), [=](int i) { return xg + oM + (int64_t)bh * nch + i; },
                                           (uint32_t *)cm, abortw, a.err);
@@ -1291,11 +1331,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 6);
                 uint32_t *csu = (uint32_t *)(scr + XS_OFF + XS_BYTES + 256);  // [nch][2]
-                const int ntask = B * H * nch;
-                for (int t = wg, k = 0; t < ntask; t += G, ++k) {
+                const int nslot = xslots(nch, B * H, G);
+                for (int s = wg, k = 0; s < nslot; s += G) {
+                    const int t = xtask(s, nch, B * H, G);
+                    if (t < 0) continue;
                     const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
-                    const float *st = (const float *)(scr + XS_OFF) + k * CL;
+                    const float *st = (const float *)(scr + XS_OFF) + (k++) * CL;
                     const int doct = tid & 7, jg = tid >> 3;
                     const f16 *Vb = (const f16 *)a.cv + ((int64_t)l * a.Bt + a.b0 + (a.beam ? 0 : b)) * T * NS + h * 64 + doct * 8;
                     half8 vf[NKP][4];
@@ -1484,10 +1526,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PHASE_IDS
             WSet<KC, NPL> S0, S1;
             constexpr int RS = 16 * NPL;  // rows per register set
-#ifndef WMI_LOGITS_LATE
-            wset_load(S0, wmat(a.te), nullptr, NS, rs0, rv1, slot, l16);
-            wset_load(S1, wmat(a.te), nullptr, NS, rs0 + RS, rv1, slot, l16);
-#endif
             LnP<NS> lp;
             Ln1P<NS> l1;
             if constexpr (BT == 1) ln1_params<NS>(a.dln_w, a.dln_b, l1, tid);
@@ -1502,13 +1540,12 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 if (check(ok)) return;
             }
                 PSTAMP(L * 32 + 16)
-#ifdef WMI_LOGITS_LATE
-            // the streamed rows requested after the poll (not in front of it in
-            // the wave's load queue): the LN and the LDS-resident rows cover them
+            // the streamed rows are requested after the poll, not in front of
+            // it in the wave's load queue: the LDS-resident rows cover their
+            // latency (logits 6.9 -> 5.8 us a step, profiles/r03/ab_r03c.txt)
             wset_load(S0, wmat(a.te), nullptr, NS, rs0, rv1, slot, l16);
             wset_load(S1, wmat(a.te), nullptr, NS, rs0 + RS, rv1, slot, l16);
             PREFETCH_ISSUED
-#endif
             if constexpr (BT > 1) ln_rows<NS>(xf, lp, xs, B, w, lane);
             __syncthreads();
             PSTAMP(L * 32 + 1)
