@@ -285,6 +285,7 @@ struct wmi_context {
     bool persist_logits = false;      // WMI_PERSIST_LOGITS=1: also store every step's logits (dlogits)
     int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
     int fault_inject = 0;             // WMI_FAULT_INJECT=1 (test): mark the first persistent block as timed out
+    bool use_kvl = true;              // WMI_KVL=0: one-row launches read self-attention K / V from memory
     int n_fallbacks = 0;              // decodes re-run on the kernel chain after a persistent exchange timeout
     PersistLayer *d_players = nullptr;
     uint32_t *d_expfb = nullptr;       // exp fallback list of the persistent decoder [64] + count
@@ -1616,6 +1617,22 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     return a;
 }
 
+// LDS-resident self-attention K / V for a one-row launch ending before
+// position pos_end (PersistArgs::kvl): every (layer, head) gets a workgroup of
+// its own, whose LDS (the vocabulary-row region) holds the head's rows; that
+// workgroup streams vkv vocabulary rows, chosen so its stream matches the
+// others' (resident nres + streamed rest)
+void set_kvl(wmi_context *ctx, PersistArgs &pa, int G, int pos_end) {
+    const int H = ctx->hp.n_text_head, L = ctx->dec_layers, n = ctx->hp.n_text_state, V = ctx->hp.n_vocab;
+    const int nk = L * H, cap = (pos_end + 31) / 32 * 32;
+    if (!ctx->use_kvl || pa.B != 1 || pa.beam || nk >= G || cap > 512 || (int64_t)cap * 256 > (int64_t)pa.nres * n * 2)
+        return;
+    pa.kvl = 1;
+    pa.kvcap = cap;
+    const int64_t vk = ((int64_t)V - (int64_t)pa.nres * (G - nk) + G - 1) / G;
+    pa.vkv = (int)(vk > 0 ? vk : 0);
+}
+
 // greedy decode of every encoded clip; tokens stay in ctx->dtokens
 // ([enc_clips][n_gen]); returns after enqueueing (no sync) unless early stop.
 int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, std::vector<int32_t> *host_tokens,
@@ -1651,6 +1668,7 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
             if (G > 0) {  // persistent decoder: the chunk's steps in one launch
                 PersistArgs pa = persist_args(ctx, b0, B, G, np, np, suppress_eot, n_gen);
                 pa.n_steps = chunk;
+                if (chunk >= 8) set_kvl(ctx, pa, G, done_steps + chunk);
                 if (ctx->d_ptrace && done_steps == 0 && b0 == 0) pa.ptrace = ctx->d_ptrace;
                 HIPCHK(ctx, launch_dec_persist(ctx->stream, pa, G));
                 if (ctx->fault_inject && b0 == 0 && done_steps == 0)  // as a stranded grid reports it
@@ -2086,6 +2104,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (const char *e = getenv("WMI_PERSIST_Q5")) ctx->persist_q5 = atoi(e) ? 1 : 0;
     if (const char *c = getenv("WMI_CHECKSUMS")) ctx->checksums = atoi(c) != 0;
     if (const char *c = getenv("WMI_FAULT_INJECT")) ctx->fault_inject = atoi(c);
+    if (const char *c = getenv("WMI_KVL")) ctx->use_kvl = atoi(c) != 0;
     ctx->dec_layers = ctx->hp.n_text_layer;
     if (const char *c = getenv("WMI_DEC_LAYERS")) ctx->dec_layers = std::max(1, std::min(atoi(c), ctx->hp.n_text_layer));
     if (getenv("WMI_PTRACE")) {

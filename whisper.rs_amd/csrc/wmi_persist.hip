@@ -632,30 +632,6 @@ __device__ __forceinline__ float exp_f16_fast(float arg, const uint32_t *fb) {
     return hit != 0xffffffffu ? h2f_bits((uint16_t)hit) : hv;
 }
 
-// Cross-attention task of workgroup slot s (a workgroup takes slots wg,
-// wg + G, ...; -1: no task).  When they fit in one round of the grid, the
-// nch chunk tasks of one (row, head) take slots of one residue mod 8 — one
-// XCD under the observed round-robin placement (speed only, never
-// correctness) — so the nch workgroups that each read the head's 64 cross-q
-// weight rows (E, XQF) share one L2; otherwise task = slot.
-__device__ __forceinline__ int xtask(int s, int nch, int BH, int G) {
-#ifdef WMI_NO_XCDMAP
-    return s < BH * nch ? s : -1;
-#endif
-    const int S = 8 * nch * ((BH + 7) >> 3);
-    if (S > G) return s < BH * nch ? s : -1;
-    const int x = s & 7, k = s >> 3, kq = k / nch;
-    const int g = x + 8 * kq;
-    return s < S && g < BH ? g * nch + (k - kq * nch) : -1;
-}
-__device__ __forceinline__ int xslots(int nch, int BH, int G) {
-#ifdef WMI_NO_XCDMAP
-    return BH * nch;
-#endif
-    const int S = 8 * nch * ((BH + 7) >> 3);
-    return S > G ? BH * nch : S;
-}
-
 // Every phase re-derives its lane indices from an opaque copy of threadIdx.x
 // behind a compiler memory barrier: __syncthreads() fences only LDS, so
 // without it the compiler hoists later phases' weight loads and lane
@@ -738,11 +714,38 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     part(NS, true, rn0, rn1);      // Wo / Wcq / Wco / W1 rows = this WG's residual rows
     part(3 * NS, true, ra0, ra1);  // Wqkv rows
     part(4 * NS, true, rh0, rh1);  // W0 rows
-    part(a.V, false, rv0, rv1);    // vocabulary rows
+    // LDS-resident self-attention K / V (PersistArgs::kvl): workgroups
+    // [0, L H) own one (layer, head) each
+    const bool kvl = BT == 1 && a.kvl;
+    const int nkw = kvl ? L * H : 0;
+    const bool kvw = wg < nkw;
+    f16 *Kl = vres, *Vl = vres + (size_t)a.kvcap * 64;  // [kvcap][64] each (K chunks swizzled)
+    if (kvl) {  // vocabulary rows: vkv for each K / V owner, the rest spread over the others
+        const int ro = (a.V - nkw * a.vkv + (G - nkw) - 1) / (G - nkw);
+        rv0 = kvw ? wg * a.vkv : nkw * a.vkv + (wg - nkw) * ro;
+        rv0 = rv0 < a.V ? rv0 : a.V;
+        rv1 = rv0 + (kvw ? a.vkv : ro);
+        rv1 = rv1 < a.V ? rv1 : a.V;
+    } else {
+        part(a.V, false, rv0, rv1);
+    }
     const int rn = rn1 - rn0;
     // this workgroup's first vocabulary rows stay in LDS for the whole launch
-    const int rs0 = rv0 + a.nres < rv1 ? rv0 + a.nres : rv1;
-    {
+    // (a K / V owner keeps its head's rows there instead)
+    const int rs0 = kvw ? rv0 : rv0 + a.nres < rv1 ? rv0 + a.nres : rv1;
+    if (kvw) {
+        // rows [0, pos) of head h, layer l from the cache (written by earlier
+        // launches: plain loads); K chunk c of row j at slot c ^ (j & 7), so the
+        // score loop's row-per-lane reads hit distinct banks
+        const int l0 = wg / H, h0 = wg - l0 * H, p0 = a.st->pos;
+        const f16 *kcs = (const f16 *)a.kcache + (size_t)l0 * DEC_ROWS * tctx * NS + h0 * 64;
+        const f16 *vcs = (const f16 *)a.vcache + (size_t)l0 * DEC_ROWS * tctx * NS + h0 * 64;
+        for (int i = tid; i < p0 * 8; i += PT) {
+            const int j = i >> 3, c = i & 7;
+            *(half8 *)(Kl + j * 64 + ((c ^ (j & 7)) * 8)) = *(const half8 *)(kcs + (int64_t)j * NS + c * 8);
+            *(half8 *)(Vl + j * 64 + c * 8) = *(const half8 *)(vcs + (int64_t)j * NS + c * 8);
+        }
+    } else {
         const uint4 *src = (const uint4 *)((const f16 *)a.te + (int64_t)rv0 * NS);
         uint4 *dst = (uint4 *)vres;
         for (int i = tid; i < (rs0 - rv0) * NS / 8; i += PT) dst[i] = src[i];
@@ -874,7 +877,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 const __amdgpu_buffer_rsrc_t rv = rsrc_of(vc, (uint32_t)(DEC_ROWS * tctx * NS * 2));
                 f16 *qn = (f16 *)scr, *kn = qn + 64, *vn = qn + 128;  // this step's q, k, v of the head
                 uint16_t *P16 = (uint16_t *)(scr + 512);                 // [512]
-                for (int t = wg; t < B * H; t += G) {
+                // (K / V owners: workgroup l H + h takes head h of layer l)
+                for (int t = kvl ? wg - l * H : wg; t >= 0 && t < B * H; t += G) {
                     const int b = t / H, h = t - b * H;
                     const int doct = tid & 7, jg = tid >> 3;
                     // cache rows j < pos (this step's row comes from the granules)
@@ -912,8 +916,17 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #pragma unroll
                         for (int i = 0; i < 8; ++i) kv[r][i] = z8;
 #else
+                        if (kvl) {  // from LDS (clamped row, selected after)
+                            const int jr = j < a.kvcap ? j : a.kvcap - 1;
 #pragma unroll
-                        for (int i = 0; i < 8; ++i) kv[r][i] = j < pos ? bload_sc1(rk, off + 16 * i) : z8;
+                            for (int i = 0; i < 8; ++i) {
+                                const half8 kl = *(const half8 *)(Kl + jr * 64 + ((i ^ (jr & 7)) * 8));
+                                kv[r][i] = j < pos ? kl : z8;
+                            }
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < 8; ++i) kv[r][i] = j < pos ? bload_sc1(rk, off + 16 * i) : z8;
+                        }
 #endif
                     }
                     // value rows j < pos, in flight across the poll as well
@@ -924,7 +937,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #ifdef WMI_EXP_NOKV
                         vv[i] = z8;
 #else
-                        vv[i] = j < pos ? bload_sc1(rv, (uint32_t)((((int64_t)srv[i] * tctx + j) * NS + h * 64 + doct * 8) * 2)) : z8;
+                        if (kvl) {
+                            const int jr = j < a.kvcap ? j : a.kvcap - 1;
+                            const half8 vl = *(const half8 *)(Vl + jr * 64 + doct * 8);
+                            vv[i] = j < pos ? vl : z8;
+                        } else {
+                            vv[i] = j < pos ? bload_sc1(rv, (uint32_t)((((int64_t)srv[i] * tctx + j) * NS + h * 64 + doct * 8) * 2)) : z8;
+                        }
 #endif
                     }
                     PREFETCH_ISSUED
@@ -935,6 +954,10 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                           (uint32_t *)qn, abortw, a.err);
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 17)
+                    if (kvl && tid < 16 && pos < a.kvcap) {  // this step's row joins the LDS copy
+                        if (tid < 8) *(half8 *)(Kl + pos * 64 + ((tid ^ (pos & 7)) * 8)) = *(const half8 *)(kn + tid * 8);
+                        else *(half8 *)(Vl + pos * 64 + (tid - 8) * 8) = *(const half8 *)(vn + (tid - 8) * 8);
+                    }
                     // scores: cache rows from registers, this step's row (same
                     // value in every lane) from the granules; no lane guards
                     half8 q8[8];
@@ -1083,10 +1106,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 4);
                 f16 *qh = (f16 *)scr;
-                const int nslot = xslots(nch, B * H, G);
-                for (int s = wg, k = 0; s < nslot; s += G) {
-                    const int t = xtask(s, nch, B * H, G);
-                    if (t < 0) continue;  // (workgroup-uniform)
+                const int ntask = B * H * nch;
+                for (int t = wg, k = 0; t < ntask; t += G) {
                     const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
                     float *st = (float *)(scr + XS_OFF) + (k++) * CL;
@@ -1174,10 +1195,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 const uint32_t tag = ptag(pos, L, l, 6);  // (G1 polls the F2 tag)
                 float *cm = (float *)scr;          // [nch]  (nch <= 64)
                 float *Sv = cm + 64;               // [T]    scores, then p
-                const int nslot = xslots(nch, B * H, G);
-                for (int s = wg; s < nslot; s += G) {
-                    const int t = xtask(s, nch, B * H, G);
-                    if (t < 0) continue;
+                const int ntask = B * H * nch;
+                for (int t = wg; t < ntask; t += G) {
                     const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
                     const int doct = tid & 7, jg = tid >> 3;
@@ -1287,10 +1306,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 5);
                 float *cm = (float *)(scr + XS_OFF + XS_BYTES);  // [nch <= 64]
-                const int nslot = xslots(nch, B * H, G);
-                for (int s = wg, k = 0; s < nslot; s += G) {
-                    const int t = xtask(s, nch, B * H, G);
-                    if (t < 0) continue;
+                const int ntask = B * H * nch;
+                for (int t = wg, k = 0; t < ntask; t += G) {
                     const int c = t % nch, bh = t / nch;
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
                     float *st = (float *)(scr + XS_OFF) + (k++) * CL;
@@ -1331,10 +1348,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 6);
                 uint32_t *csu = (uint32_t *)(scr + XS_OFF + XS_BYTES + 256);  // [nch][2]
-                const int nslot = xslots(nch, B * H, G);
-                for (int s = wg, k = 0; s < nslot; s += G) {
-                    const int t = xtask(s, nch, B * H, G);
-                    if (t < 0) continue;
+                const int ntask = B * H * nch;
+                for (int t = wg, k = 0; t < ntask; t += G) {
                     const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
                     const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
                     const float *st = (const float *)(scr + XS_OFF) + (k++) * CL;
@@ -1780,7 +1795,9 @@ hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G) {
     if (G < 1 || G > PX_GMAX || a.B < 1 || a.B > PMAXB || a.T > 2048 || a.nch < 1 || a.nch > 64 ||
         a.cl > 128 * NKP || (int64_t)a.nch * a.cl < a.T || (int64_t)a.B * (a.n / 64) * a.nch > PX_TASKS ||
         a.tctx > 512 || a.cl % 128 || (a.beam && a.n_steps != 1) || (a.kv_src && a.kv_src_stride < a.tctx) ||
-        ((int64_t)a.B * (a.n / 64) * a.nch + G - 1) / G * a.cl * 4 > XS_BYTES)  // task scores in LDS
+        ((int64_t)a.B * (a.n / 64) * a.nch + G - 1) / G * a.cl * 4 > XS_BYTES ||  // task scores in LDS
+        (a.kvl && (a.B != 1 || a.beam || a.L * (a.n / 64) >= G || a.kvcap < 32 || a.kvcap > 512 ||
+                   (int64_t)a.kvcap * 256 > (int64_t)a.nres * a.n * 2 || a.vkv < 0)))
         return hipErrorInvalidValue;
     switch (a.n) {
         case 128: return launch_ns<128>(s, a, G);
