@@ -476,6 +476,32 @@ def test_persistent_q5_equals_f16(wmi, model_cache, model, n_clips):
             ctx.close()
 
 
+@pytest.mark.parametrize("model,n_ctx,n_tok", [("micro", 64, 150), ("tiny.en", 1500, 300), ("base", 1500, 40)])
+def test_lds_kv_equals_memory_kv(wmi, model_cache, model, n_ctx, n_tok):
+    """One-row launches keep each (layer, head)'s self-attention K / V in the
+    LDS of a workgroup of its own and run the attention inside each wave
+    (PersistArgs::kvl); the same arithmetic in the same order as the path that
+    reads the cache through memory (WMI_KVL=0): bitwise the same ids and last
+    step logits (tiny.en: 300 steps, past the 256 keys of a lane's first
+    slots)."""
+    path = synth.model_path(model, model_cache)
+    clip = [synth.synth_pcm_f32(30.0 if n_ctx == 1500 else 2.0, 90)]
+    out = []
+    for env in ({"WMI_PERSIST_LOGITS": "1"}, {"WMI_PERSIST_LOGITS": "1", "WMI_KVL": "0"}):
+        ctx = _ctx_with_env(wmi, path, env)
+        try:
+            ctx.set_audio_ctx(n_ctx)
+            ctx.pcm_to_mel_batch(clip)
+            ctx.encode(1, 0)
+            toks = ctx.decode_greedy(n_tok, suppress_eot=True)[0]
+            V = ctx.hparams["n_vocab"]
+            out.append((toks, np.frombuffer(ctx.debug_read(2, V * 4), np.float32).copy()))
+        finally:
+            ctx.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
 @pytest.mark.parametrize("model,n_clips,n_ctx", [("micro", 1, 64), ("micro", 3, 64), ("micro", 2, 1500),
                                                  ("tiny.en", 1, 1500), ("base", 2, 1500)])
 def test_persistent_matches_chain(wmi, model_cache, model, n_clips, n_ctx):

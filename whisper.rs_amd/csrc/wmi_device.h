@@ -51,6 +51,9 @@ __device__ __forceinline__ uint32_t dpp_xor2(uint32_t x) {
 __device__ __forceinline__ uint32_t dpp_xor1(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xb1, 0xf, 0xf, false);
 }
+__device__ __forceinline__ uint32_t dpp_xor3(uint32_t x) {  // quad_perm [3,2,1,0]
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x1b, 0xf, 0xf, false);
+}
 // {own, partner} in some order for lane ^ 16 / lane ^ 32
 __device__ __forceinline__ void swap16(uint32_t x, uint32_t &a, uint32_t &b) {
     const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);

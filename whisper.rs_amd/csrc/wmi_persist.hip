@@ -735,15 +735,16 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     const int rs0 = kvw ? rv0 : rv0 + a.nres < rv1 ? rv0 + a.nres : rv1;
     if (kvw) {
         // rows [0, pos) of head h, layer l from the cache (written by earlier
-        // launches: plain loads); K chunk c of row j at slot c ^ (j & 7), so the
-        // score loop's row-per-lane reads hit distinct banks
+        // launches: plain loads); K chunk c of row j at slot c ^ (j & 7) and V
+        // chunk c at slot c ^ ((j >> 3) & 7), so the row-per-lane reads of the
+        // score loop and of P.V hit distinct banks
         const int l0 = wg / H, h0 = wg - l0 * H, p0 = a.st->pos;
         const f16 *kcs = (const f16 *)a.kcache + (size_t)l0 * DEC_ROWS * tctx * NS + h0 * 64;
         const f16 *vcs = (const f16 *)a.vcache + (size_t)l0 * DEC_ROWS * tctx * NS + h0 * 64;
         for (int i = tid; i < p0 * 8; i += PT) {
             const int j = i >> 3, c = i & 7;
             *(half8 *)(Kl + j * 64 + ((c ^ (j & 7)) * 8)) = *(const half8 *)(kcs + (int64_t)j * NS + c * 8);
-            *(half8 *)(Vl + j * 64 + c * 8) = *(const half8 *)(vcs + (int64_t)j * NS + c * 8);
+            *(half8 *)(Vl + j * 64 + ((c ^ ((j >> 3) & 7)) * 8)) = *(const half8 *)(vcs + (int64_t)j * NS + c * 8);
         }
     } else {
         const uint4 *src = (const uint4 *)((const f16 *)a.te + (int64_t)rv0 * NS);
@@ -880,6 +881,106 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 // (K / V owners: workgroup l H + h takes head h of layer l)
                 for (int t = kvl ? wg - l * H : wg; t >= 0 && t < B * H; t += G) {
                     const int b = t / H, h = t - b * H;
+                    if (kvl) {
+                        // K / V from this workgroup's LDS copy and no exchange
+                        // between its waves: every wave computes all M = pos + 1
+                        // scores and the softmax (the max, and the double sum
+                        // of f16 values, are exact in any order: the same P16
+                        // in every wave), then P.V for its 16 output dims.  Each
+                        // P.V lane sums its keys kg + 32 i in i order and the
+                        // key groups combine in the memory path's order (xor 8,
+                        // 16, 32, then groups 0..3 in sequence), so the outputs
+                        // are bitwise those of the memory path.
+                        __syncthreads();
+                        const int64_t hq = b * (NS / 2) + h * 32;
+                        const bool ok = gpoll(96, ptag(pos, L, l, 0),
+                                              [=](int i) { return xg + oQ + (i >> 5) * (4 * NS) + hq + (i & 31); },
+                                              (uint32_t *)qn, abortw, a.err);
+                        if (check(ok)) return;
+                PSTAMP(l * 32 + 17)
+                        const int M = pos + 1;
+                        if (tid < 16 && pos < a.kvcap) {  // this step's row joins the LDS copy
+                            if (tid < 8) *(half8 *)(Kl + pos * 64 + ((tid ^ (pos & 7)) * 8)) = *(const half8 *)(kn + tid * 8);
+                            else *(half8 *)(Vl + pos * 64 + (((tid - 8) ^ ((pos >> 3) & 7)) * 8)) = *(const half8 *)(vn + (tid - 8) * 8);
+                        }
+                        half8 q8[8];
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) q8[i] = *(const half8 *)(qn + 8 * i);
+                        constexpr int KPL = 8;  // keys per lane (512 / 64)
+                        float sc[KPL];
+                        float mx = -INFINITY;
+#pragma unroll
+                        for (int k = 0; k < KPL; ++k) {
+                            const int j = lane + 64 * k;
+                            float s = 0.0f;
+                            if (64 * k < M) {  // wave-uniform
+                                const int jr = j < pos ? j : j == pos ? 0 : 0;
+                                half8 kr[8];
+#pragma unroll
+                                for (int i = 0; i < 8; ++i) kr[i] = *(const half8 *)(Kl + jr * 64 + ((i ^ (jr & 7)) * 8));
+                                if (j == pos) {
+#pragma unroll
+                                    for (int i = 0; i < 8; ++i) kr[i] = *(const half8 *)(kn + 8 * i);
+                                }
+#pragma unroll
+                                for (int i = 0; i < 8; ++i) s = dot8(kr[i], q8[i], s);
+                                if (j < M) mx = fmaxf(mx, s);
+                            }
+                            sc[k] = s;
+                        }
+                        mx = wave_max(mx);
+                        double sum = 0.0;
+                        float pk[KPL];
+#pragma unroll
+                        for (int k = 0; k < KPL; ++k) {
+                            pk[k] = 0.0f;
+                            if (64 * k < M && lane + 64 * k < M) {
+                                pk[k] = exp_f16_fast(sc[k] - mx, sh.expfb);
+                                sum += (double)pk[k];
+                            }
+                        }
+                        sum = wave_sum(sum);
+                        const float inv = (float)(1.0 / sum);
+                        uint16_t *P16w = (uint16_t *)(scr + 2048) + w * 512;  // this wave's P16 [512]
+#pragma unroll
+                        for (int k = 0; k < KPL; ++k)
+                            if (64 * k < M && lane + 64 * k < M) P16w[lane + 64 * k] = f2h_bits(pk[k] * inv);
+                        wave_sync();
+                        // P.V: lane -> key group kg (bits 0-2 from lane bits 3-5, bits
+                        // 3-4 from lane bits 0-1), dim octet 2 w + lane bit 2
+                        const int kg = ((lane >> 3) & 7) | ((lane & 3) << 3), dct = 2 * w + ((lane >> 2) & 1);
+                        float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            if (32 * i >= pos) break;  // wave-uniform: the rest add zeros
+                            const int j = kg + 32 * i;
+                            const int jr = j < pos ? j : 0;
+                            const half8 vr = *(const half8 *)(Vl + jr * 64 + ((dct ^ ((jr >> 3) & 7)) * 8));
+                            const float pj = j < pos ? h2f_bits(P16w[jr]) : 0.0f;
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vr[e];
+                        }
+                        if (kg == (pos & 31)) {
+                            const float pj = h2f_bits(P16w[pos]);
+                            const half8 vr = *(const half8 *)(vn + dct * 8);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vr[e];
+                        }
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            float v = red_8_16_32(o[e]);
+                            // key groups 0..3 (lane bits 0-1) in sequence: ((g0 + g1) + g2) + g3
+                            const float g1 = __uint_as_float(dpp_xor1(__float_as_uint(v)));
+                            const float g2 = __uint_as_float(dpp_xor2(__float_as_uint(v)));
+                            const float g3 = __uint_as_float(dpp_xor3(__float_as_uint(v)));
+                            o[e] = ((v + g1) + g2) + g3;
+                        }
+                        if ((lane & ~4) == 0)  // lanes 0 and 4: dims dct * 8 .. + 7
+#pragma unroll
+                            for (int e = 0; e < 8; e += 2)
+                                gput(xg + oO + b * (NS / 2) + h * 32 + dct * 4 + e / 2, ptag(pos, L, l, 1), pack2(o[e], o[e + 1]));
+                        continue;
+                    }
                     const int doct = tid & 7, jg = tid >> 3;
                     // cache rows j < pos (this step's row comes from the granules)
                     half8 kv[2][8];
@@ -916,17 +1017,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #pragma unroll
                         for (int i = 0; i < 8; ++i) kv[r][i] = z8;
 #else
-                        if (kvl) {  // from LDS (clamped row, selected after)
-                            const int jr = j < a.kvcap ? j : a.kvcap - 1;
 #pragma unroll
-                            for (int i = 0; i < 8; ++i) {
-                                const half8 kl = *(const half8 *)(Kl + jr * 64 + ((i ^ (jr & 7)) * 8));
-                                kv[r][i] = j < pos ? kl : z8;
-                            }
-                        } else {
-#pragma unroll
-                            for (int i = 0; i < 8; ++i) kv[r][i] = j < pos ? bload_sc1(rk, off + 16 * i) : z8;
-                        }
+                        for (int i = 0; i < 8; ++i) kv[r][i] = j < pos ? bload_sc1(rk, off + 16 * i) : z8;
 #endif
                     }
                     // value rows j < pos, in flight across the poll as well
@@ -937,13 +1029,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #ifdef WMI_EXP_NOKV
                         vv[i] = z8;
 #else
-                        if (kvl) {
-                            const int jr = j < a.kvcap ? j : a.kvcap - 1;
-                            const half8 vl = *(const half8 *)(Vl + jr * 64 + doct * 8);
-                            vv[i] = j < pos ? vl : z8;
-                        } else {
-                            vv[i] = j < pos ? bload_sc1(rv, (uint32_t)((((int64_t)srv[i] * tctx + j) * NS + h * 64 + doct * 8) * 2)) : z8;
-                        }
+                        vv[i] = j < pos ? bload_sc1(rv, (uint32_t)((((int64_t)srv[i] * tctx + j) * NS + h * 64 + doct * 8) * 2)) : z8;
 #endif
                     }
                     PREFETCH_ISSUED
@@ -954,10 +1040,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                           (uint32_t *)qn, abortw, a.err);
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 17)
-                    if (kvl && tid < 16 && pos < a.kvcap) {  // this step's row joins the LDS copy
-                        if (tid < 8) *(half8 *)(Kl + pos * 64 + ((tid ^ (pos & 7)) * 8)) = *(const half8 *)(kn + tid * 8);
-                        else *(half8 *)(Vl + pos * 64 + (tid - 8) * 8) = *(const half8 *)(vn + (tid - 8) * 8);
-                    }
                     // scores: cache rows from registers, this step's row (same
                     // value in every lane) from the granules; no lane guards
                     half8 q8[8];
