@@ -903,56 +903,52 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                             if (tid < 8) *(half8 *)(Kl + pos * 64 + ((tid ^ (pos & 7)) * 8)) = *(const half8 *)(kn + tid * 8);
                             else *(half8 *)(Vl + pos * 64 + (((tid - 8) ^ ((pos >> 3) & 7)) * 8)) = *(const half8 *)(vn + (tid - 8) * 8);
                         }
-                        half8 q8[8];
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) q8[i] = *(const half8 *)(qn + 8 * i);
-                        constexpr int KPL = 8;  // keys per lane (512 / 64)
-                        float sc[KPL];
+                        // (loops over a lane's key slots are not unrolled: the
+                        // scores and p live in this wave's LDS, not in registers)
+                        float *sP = (float *)(scr + 2048) + w * 512;                 // this wave's scores, then p [512]
+                        uint16_t *P16w = (uint16_t *)(scr + 2048 + 4 * 2048) + w * 512;  // this wave's P16 [512]
+                        const int nk = (M + 63) >> 6;
                         float mx = -INFINITY;
-#pragma unroll
-                        for (int k = 0; k < KPL; ++k) {
+#pragma unroll 1
+                        for (int k = 0; k < nk; ++k) {
                             const int j = lane + 64 * k;
+                            const int jr = j < pos ? j : 0;
                             float s = 0.0f;
-                            if (64 * k < M) {  // wave-uniform
-                                const int jr = j < pos ? j : j == pos ? 0 : 0;
-                                half8 kr[8];
 #pragma unroll
-                                for (int i = 0; i < 8; ++i) kr[i] = *(const half8 *)(Kl + jr * 64 + ((i ^ (jr & 7)) * 8));
-                                if (j == pos) {
-#pragma unroll
-                                    for (int i = 0; i < 8; ++i) kr[i] = *(const half8 *)(kn + 8 * i);
-                                }
-#pragma unroll
-                                for (int i = 0; i < 8; ++i) s = dot8(kr[i], q8[i], s);
-                                if (j < M) mx = fmaxf(mx, s);
+                            for (int i = 0; i < 8; ++i) {
+                                const half8 q = *(const half8 *)(qn + 8 * i);
+                                const half8 kl = *(const half8 *)(Kl + jr * 64 + ((i ^ (jr & 7)) * 8));
+                                const half8 kp = *(const half8 *)(kn + 8 * i);
+                                s = dot8(j == pos ? kp : kl, q, s);
                             }
-                            sc[k] = s;
+                            sP[j] = s;
+                            if (j < M) mx = fmaxf(mx, s);
                         }
                         mx = wave_max(mx);
                         double sum = 0.0;
-                        float pk[KPL];
-#pragma unroll
-                        for (int k = 0; k < KPL; ++k) {
-                            pk[k] = 0.0f;
-                            if (64 * k < M && lane + 64 * k < M) {
-                                pk[k] = exp_f16_fast(sc[k] - mx, sh.expfb);
-                                sum += (double)pk[k];
+#pragma unroll 1
+                        for (int k = 0; k < nk; ++k) {
+                            const int j = lane + 64 * k;
+                            const float pj = exp_f16_fast(sP[j] - mx, sh.expfb);
+                            if (j < M) {
+                                sum += (double)pj;
+                                sP[j] = pj;
                             }
                         }
                         sum = wave_sum(sum);
                         const float inv = (float)(1.0 / sum);
-                        uint16_t *P16w = (uint16_t *)(scr + 2048) + w * 512;  // this wave's P16 [512]
-#pragma unroll
-                        for (int k = 0; k < KPL; ++k)
-                            if (64 * k < M && lane + 64 * k < M) P16w[lane + 64 * k] = f2h_bits(pk[k] * inv);
+#pragma unroll 1
+                        for (int k = 0; k < nk; ++k) {
+                            const int j = lane + 64 * k;
+                            if (j < M) P16w[j] = f2h_bits(sP[j] * inv);
+                        }
                         wave_sync();
                         // P.V: lane -> key group kg (bits 0-2 from lane bits 3-5, bits
                         // 3-4 from lane bits 0-1), dim octet 2 w + lane bit 2
                         const int kg = ((lane >> 3) & 7) | ((lane & 3) << 3), dct = 2 * w + ((lane >> 2) & 1);
                         float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            if (32 * i >= pos) break;  // wave-uniform: the rest add zeros
+#pragma unroll 1
+                        for (int i = 0; 32 * i < pos; ++i) {  // (the rest add zeros)
                             const int j = kg + 32 * i;
                             const int jr = j < pos ? j : 0;
                             const half8 vr = *(const half8 *)(Vl + jr * 64 + ((dct ^ ((jr >> 3) & 7)) * 8));
