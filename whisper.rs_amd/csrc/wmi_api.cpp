@@ -284,6 +284,7 @@ struct wmi_context {
     int persist_q5 = -1;              // WMI_PERSIST_Q5: 1 always, 0 never, default when B > 1
     bool persist_logits = false;      // WMI_PERSIST_LOGITS=1: also store every step's logits (dlogits)
     int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
+    int enc_layers = 0;               // WMI_ENC_LAYERS (debug): run only the first encoder layers
     int fault_inject = 0;             // WMI_FAULT_INJECT=1 (test): mark the first persistent block as timed out
     bool use_kvl = true;              // WMI_KVL=0: one-row launches read self-attention K / V from memory
     int n_fallbacks = 0;              // decodes re-run on the kernel chain after a persistent exchange timeout
@@ -1157,7 +1158,7 @@ int run_encode(wmi_context *ctx, int mel_offset) {
     g.out32 = ctx->h; g.ldo = n; g.gelu_tab = ctx->gelu_tab; g.pe = ctx->e_pe; g.T = T;
     HIPCHK(ctx, launch_gemm(s, EPI_CONV2PE, g));
     const int M = B * T;
-    for (int l = 0; l < hp.n_audio_layer; ++l) {
+    for (int l = 0; l < ctx->enc_layers; ++l) {
         const EncLayerDev &e = ctx->enc[l];
         HIPCHK(ctx, launch_layernorm(s, ctx->h, M, n, e.ln1_w, e.ln1_b, f32 ? nullptr : ctx->xln, ctx->xln32));
         g = GemmArgs{};
@@ -2107,6 +2108,8 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (const char *c = getenv("WMI_KVL")) ctx->use_kvl = atoi(c) != 0;
     ctx->dec_layers = ctx->hp.n_text_layer;
     if (const char *c = getenv("WMI_DEC_LAYERS")) ctx->dec_layers = std::max(1, std::min(atoi(c), ctx->hp.n_text_layer));
+    ctx->enc_layers = ctx->hp.n_audio_layer;
+    if (const char *c = getenv("WMI_ENC_LAYERS")) ctx->enc_layers = std::max(0, std::min(atoi(c), ctx->hp.n_audio_layer));
     if (getenv("WMI_PTRACE")) {
         const size_t nb = (size_t)hp_ptrace_slots(ctx->hp) * 8;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_ptrace, nb));
@@ -2687,6 +2690,7 @@ int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes) {
             memcpy(out, v, std::min(sizeof v, bytes));
             return WMI_OK;
         }
+        case 12: src = ctx->h; have = (size_t)ctx->enc_clips * ctx->enc_T * ctx->hp.n_audio_state * 4; break;  // encoder residual stream
         case 11: {  // host: decodes re-run on the kernel chain after a persistent exchange timeout
             const int32_t v = ctx->n_fallbacks;
             memcpy(out, &v, std::min(sizeof v, bytes));
