@@ -286,7 +286,10 @@ struct wmi_context {
     int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
     int enc_layers = 0;               // WMI_ENC_LAYERS (debug): run only the first encoder layers
     int fault_inject = 0;             // WMI_FAULT_INJECT=1 (test): mark the first persistent block as timed out
-    bool use_kvl = true;              // WMI_KVL=0: one-row launches read self-attention K / V from memory
+    // WMI_KVL=1: one-row launches hold self-attention K / V in LDS with the
+    // wave-local attention (bitwise equal to the memory path, but 149.5 vs
+    // 141.2 us a base step on one box, profiles/r03/ab_r03g_*): off by default
+    bool use_kvl = false;
     int n_fallbacks = 0;              // decodes re-run on the kernel chain after a persistent exchange timeout
     PersistLayer *d_players = nullptr;
     uint32_t *d_expfb = nullptr;       // exp fallback list of the persistent decoder [64] + count
