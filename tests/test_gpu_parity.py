@@ -395,13 +395,33 @@ def test_large_v3(wmi, model_cache):
     try:
         assert ctx.hparams["n_mels"] == 128 and ctx.hparams["n_vocab"] == 51866
         _greedy_case(ctx, om, range(1234, 1237), 12, 1500, 30.0, min_len=9)
-        ref, score, got, got_score = _beam_case(ctx, om, range(1234, 1238), 5, 6, True, n_ctx=1500, secs=30.0,
+        ref, score, got, got_score = _beam_case(ctx, om, range(1234, 1238), 5, 12, True, n_ctx=1500, secs=30.0,
                                                 fail=True)
         np.testing.assert_array_equal(got, ref)
         assert abs(got_score - score) < 2e-2
     finally:
         ctx.close()
         om.close()
+
+
+@pytest.mark.slow
+def test_beam_shared_cross_equals_per_row(wmi, model_cache):
+    """C5's beam rows read their clip's cross K / V through one task per (head,
+    key chunk) (PersistArgs::xshare): bitwise the tokens and scores of the
+    per-row tasks (WMI_XSHARE=0), whose arithmetic it repeats row by row."""
+    path = synth.model_path("large-v3", model_cache)
+    pcm = [synth.synth_pcm_f32(30.0, 1236)]
+    out = []
+    for env in ({}, {"WMI_XSHARE": "0"}):
+        ctx = _ctx_with_env(wmi, path, env)
+        try:
+            ctx.pcm_to_mel_batch(pcm)
+            ctx.encode(1, 0)
+            out.append(ctx.decode_beam(5, 16, suppress_eot=True)[0])
+        finally:
+            ctx.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
 
 
 # --- ggml quantised weights (config C3; semantics in tests/test_quant.py) ----

@@ -290,6 +290,7 @@ struct wmi_context {
     // wave-local attention (bitwise equal to the memory path, but 149.5 vs
     // 141.2 us a base step on one box, profiles/r03/ab_r03g_*): off by default
     bool use_kvl = false;
+    bool use_xshare = true;           // WMI_XSHARE=0: beam rows read the cross K / V per row
     int n_fallbacks = 0;              // decodes re-run on the kernel chain after a persistent exchange timeout
     PersistLayer *d_players = nullptr;
     uint32_t *d_expfb = nullptr;       // exp fallback list of the persistent decoder [64] + count
@@ -1601,11 +1602,15 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     // tasks would need more than one round of the grid (several rows) —
     // the smallest multiple of 128 (<= 512) that fits them in one round;
     // always within the exchange block's task table
+    // beam launches of n > 768 (cross q from the D phase) share one task per
+    // (head, chunk) among the rows (PersistArgs::xshare): only H * nch tasks
+    const int rows_t = ctx->beam_k > 0 && n > 768 && ctx->use_xshare ? 1 : B;
     int cl = 128;
-    while (cl < 512 && ((int64_t)B * H * ((T + cl - 1) / cl) > G || (int64_t)B * H * ((T + cl - 1) / cl) > PX_TASKS))
+    while (cl < 512 && ((int64_t)rows_t * H * ((T + cl - 1) / cl) > G || (int64_t)B * H * ((T + cl - 1) / cl) > PX_TASKS))
         cl += 128;
     a.cl = cl;
     a.nch = (T + cl - 1) / cl;
+    a.xshare = rows_t == 1 && B > 1 ? 1 : 0;
     a.qscale = powf((float)n / (float)H, -0.25f);
     a.st = ctx->dstate; a.feed = ctx->dfeed; a.feed_len = feed_len; a.feed_stride = feed_stride;
     a.tokens_out = ctx->dtokens + (size_t)b0 * out_stride; a.out_stride = out_stride;
@@ -2109,6 +2114,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (const char *c = getenv("WMI_CHECKSUMS")) ctx->checksums = atoi(c) != 0;
     if (const char *c = getenv("WMI_FAULT_INJECT")) ctx->fault_inject = atoi(c);
     if (const char *c = getenv("WMI_KVL")) ctx->use_kvl = atoi(c) != 0;
+    if (const char *c = getenv("WMI_XSHARE")) ctx->use_xshare = atoi(c) != 0;
     ctx->dec_layers = ctx->hp.n_text_layer;
     if (const char *c = getenv("WMI_DEC_LAYERS")) ctx->dec_layers = std::max(1, std::min(atoi(c), ctx->hp.n_text_layer));
     ctx->enc_layers = ctx->hp.n_audio_layer;

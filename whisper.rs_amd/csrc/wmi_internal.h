@@ -299,7 +299,7 @@ struct PersistLayer {          // decoder layer weights (device pointers)
 struct XLayout {
     int x1, x2, x3, q, k, v, o, xq, oc, h, s, m, p, a, ctl, total;
 };
-constexpr int PX_TASKS = 1024;   // cross-attention (row, head, chunk) tasks
+constexpr int PX_TASKS = 2048;   // cross-attention (row, head, chunk) tasks
 constexpr int PX_GMAX = 256;     // workgroups
 __host__ __device__ inline XLayout persist_layout(int n, int H, int T) {
     XLayout L{};
@@ -366,6 +366,10 @@ struct PersistArgs {
     // row itself, so no step reads the cache through memory; its LDS holds
     // no vocabulary rows, and it takes vkv vocabulary rows (all streamed)
     int kvl, kvcap, vkv;
+    // beam launches (rows = hypotheses of one clip, n > 768): one cross-
+    // attention task per (head, key chunk) covers every row (PersistArgs::nch
+    // then counts the chunks of one head: H * nch tasks)
+    int xshare;
 };
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G);
 // the inputs whose f32 exp is too close to an f16 midpoint, with their table

@@ -123,6 +123,8 @@ struct PShared {
     int32_t tok[PMAXB];
     float redf[4];
     double redd[4], redd2[4];
+    float redfb[PMAXB][4];   // beam-shared cross tasks: per-row wave maxima
+    double reddb[PMAXB][4];  // and per-row wave sums
     unsigned long long best[4][PMAXB];
     float ored[4][64 * 4];  // per wave: up to NKP 64-float partials
     __attribute__((aligned(16))) uint32_t expfb[EXPFB];  // exp fallback list (exp_f16_fast)
@@ -673,6 +675,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     // one row keeps the single hand-off (one seam fewer: 140.8 vs 142.2 us
     // per base step, profiles/r03/ptrace_fsplit.log)
     constexpr bool FSPLIT = BT > 1;
+    // beam rows share one clip's cross K / V tasks (PersistArgs::xshare)
+    const bool xsh = BEAM && !XQF && a.xshare;
     // split-K factors of the GEMV phases (quarter-waves per row), from the
     // rows a workgroup owns at the full grid
     constexpr int KS_N = split_of(KC, rows_full(NS)), KS_I = split_of(4 * KC, rows_full(NS));
@@ -1177,6 +1181,63 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }
 
             PSTAMP(l * 32 + 3)
+            // beam search (rows = hypotheses of one clip, cross q from D): one
+            // task per (head, key chunk) covers every row, so each K / V chunk
+            // is read once a step (the per-row tasks read it once per row); a
+            // row's arithmetic is the per-row task's, in the same order
+            if (xsh) {
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 4);
+                f16 *qb = (f16 *)scr;  // [B][64] this head's cross q of every row
+                const int ntask = H * nch;
+                for (int t = wg, k = 0; t < ntask; t += G) {
+                    const int c = t % nch, h = t / nch;
+                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
+                    float *st = (float *)(scr + XS_OFF) + (k++) * (B * CL);  // [B][CL]
+                    const f16 *Kb = (const f16 *)a.ck + ((int64_t)l * a.Bt + a.b0) * T * NS + h * 64 + (tid & 1) * 32;
+                    half8 kf[NKP][4];
+                    const half8 z8 = {};
+#pragma unroll
+                    for (int p = 0; p < NKP; ++p) {
+                        int key = j0 + 128 * p + (tid >> 1);
+                        key = key < j1 ? key : j1 - 1;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            kf[p][i] = 128 * p < CL ? sld((const half8 *)(Kb + (int64_t)key * NS + 8 * i)) : z8;
+                    }
+                    PREFETCH_ISSUED
+                    __syncthreads();
+                    const bool ok = gpoll(B * 32, ptag(pos, L, l, 3),
+                                          [=](int i) { return xg + oXQ + (i >> 5) * (NS / 2) + h * 32 + (i & 31); },
+                                          (uint32_t *)qb, abortw, a.err);
+                    if (check(ok)) return;
+                PSTAMP(l * 32 + 20)
+                    for (int b = 0; b < B; ++b) {
+                        float m = -INFINITY;
+#pragma unroll
+                        for (int p = 0; p < NKP; ++p)
+                            if (j0 + 128 * p < j1) {
+                                const int key = j0 + 128 * p + (tid >> 1);
+                                float sv = 0.0f;
+#pragma unroll
+                                for (int i = 0; i < 4; ++i)
+                                    sv = dot8(kf[p][i], *(const half8 *)(qb + b * 64 + (tid & 1) * 32 + 8 * i), sv);
+                                sv = xstep<XSum, 1>(sv);
+                                if (key < j1) {
+                                    if ((tid & 1) == 0) st[b * CL + key - j0] = sv;
+                                    m = fmaxf(m, sv);
+                                }
+                            }
+                        m = wave_max(m);
+                        if (lane == 0) sh.redfb[b][w] = m;
+                    }
+                    __syncthreads();
+                    if (tid < B)
+                        gput(xg + oM + ((int64_t)tid * H + h) * nch + c, tag,
+                             __float_as_uint(fmaxf(fmaxf(sh.redfb[tid][0], sh.redfb[tid][1]),
+                                                   fmaxf(sh.redfb[tid][2], sh.redfb[tid][3]))));
+                }
+            } else
             // ---- E: cross scores per (row, head, key chunk) ----------------
             // the scores stay in this workgroup's LDS (task slot k of the
             // workgroup's tasks t = wg + k G); only the chunk max is published
@@ -1375,6 +1436,48 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }
 
             } else {
+            if (xsh) {  // beam rows sharing one clip (see E)
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 5);
+                float *cmb = (float *)(scr + XS_OFF + XS_BYTES);  // [B][nch]
+                const int ntask = H * nch;
+                for (int t = wg, k = 0; t < ntask; t += G) {
+                    const int c = t % nch, h = t / nch;
+                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
+                    float *st = (float *)(scr + XS_OFF) + (k++) * (B * CL);
+                    __syncthreads();
+                    const bool ok = gpoll(B * nch, ptag(pos, L, l, 4),
+                                          [=](int i) { return xg + oM + ((int64_t)(i / nch) * H + h) * nch + (i % nch); },
+                                          (uint32_t *)cmb, abortw, a.err);
+                    if (check(ok)) return;
+                PSTAMP(l * 32 + 21)
+                    for (int b = 0; b < B; ++b) {
+                        const float m = wave_max(cmb[b * nch + (lane < nch ? lane : 0)]);
+                        double sum = 0.0;
+#pragma unroll
+                        for (int u = 0; u < NKP; ++u) {
+                            const int key = j0 + tid + 256 * u;
+                            if (256 * u < CL) {
+                                const float sv = st[b * CL + (key < j1 ? key : j1 - 1) - j0];
+                                const float pj = exp_f16_fast(sv - m, sh.expfb);
+                                if (key < j1) {
+                                    sum += (double)pj;
+                                    st[b * CL + key - j0] = pj;
+                                }
+                            }
+                        }
+                        sum = wave_sum(sum);
+                        if (lane == 0) sh.reddb[b][w] = sum;
+                    }
+                    __syncthreads();
+                    if (tid < B) {
+                        const double cs = ((sh.reddb[tid][0] + sh.reddb[tid][1]) + sh.reddb[tid][2]) + sh.reddb[tid][3];
+                        const int64_t tb = ((int64_t)tid * H + h) * nch + c;
+                        gput(xg + oS + 2 * tb, tag, lo32(cs));
+                        gput(xg + oS + 2 * tb + 1, tag, hi32(cs));
+                    }
+                }
+            } else
             // ---- F1: exp against the global max, chunk sums ----------------
             // the row max over every chunk of (row, head); p = ggml exp table
             // value of f16(s - max) replaces the task's scores in LDS; the
@@ -1421,6 +1524,83 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }
 
             PSTAMP(l * 32 + 5)
+            if (xsh) {  // beam rows sharing one clip (see E): V chunk read once, P.V per row
+                PHASE_IDS
+                const uint32_t tag = ptag(pos, L, l, 6);
+                uint32_t *csub = (uint32_t *)(scr + XS_OFF + XS_BYTES + 2048);  // [B][nch][2]
+                const int ntask = H * nch;
+                for (int t = wg, k = 0; t < ntask; t += G) {
+                    const int c = t % nch, h = t / nch;
+                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
+                    const float *st = (const float *)(scr + XS_OFF) + (k++) * (B * CL);
+                    const int doct = tid & 7, jg = tid >> 3;
+                    const f16 *Vb = (const f16 *)a.cv + ((int64_t)l * a.Bt + a.b0) * T * NS + h * 64 + doct * 8;
+                    half8 vf[NKP][4];
+                    const half8 z8 = {};
+#pragma unroll
+                    for (int p = 0; p < NKP; ++p)
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            int key = j0 + 128 * p + jg * 4 + u;
+                            key = key < j1 ? key : j1 - 1;
+                            vf[p][u] = 128 * p < CL ? sld((const half8 *)(Vb + (int64_t)key * NS)) : z8;
+                        }
+                    PREFETCH_ISSUED
+                    __syncthreads();
+                    const bool ok = gpoll(B * 2 * nch, ptag(pos, L, l, 5),
+                                          [=](int i) {
+                                              const int b = i / (2 * nch), r = i - b * 2 * nch;
+                                              return xg + oS + 2 * (((int64_t)b * H + h) * nch) + r;
+                                          },
+                                          csub, abortw, a.err);
+                    if (check(ok)) return;
+                PSTAMP(l * 32 + 22)
+                    const int nsp = (j1 - j0 + 127) >> 7;
+                    for (int b = 0; b < B; ++b) {
+                        double tot = 0.0;
+                        for (int i = 0; i < nch; ++i) tot += mk64(csub[(b * nch + i) * 2 + 1], csub[(b * nch + i) * 2]);
+                        const float inv = (float)(1.0 / tot);
+                        float o[NKP][8];
+#pragma unroll
+                        for (int p = 0; p < NKP; ++p)
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) o[p][e] = 0.0f;
+#pragma unroll
+                        for (int p = 0; p < NKP; ++p)
+                            if (j0 + 128 * p < j1) {
+                                float sp[4];
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    const int key = j0 + 128 * p + jg * 4 + u;
+                                    sp[u] = st[b * CL + (key < j1 ? key : j1 - 1) - j0];
+                                }
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    const int key = j0 + 128 * p + jg * 4 + u;
+                                    const float pj = key < j1 ? h2f_bits(f2h_bits(sp[u] * inv)) : 0.0f;
+#pragma unroll
+                                    for (int e = 0; e < 8; ++e) o[p][e] = o[p][e] + pj * (float)vf[p][u][e];
+                                }
+                            }
+#pragma unroll
+                        for (int p = 0; p < NKP; ++p)
+                            if (j0 + 128 * p < j1)
+#pragma unroll
+                                for (int e = 0; e < 8; ++e) o[p][e] = red_8_16_32(o[p][e]);
+                        if (lane < 8)
+#pragma unroll
+                            for (int p = 0; p < NKP; ++p)
+                                if (j0 + 128 * p < j1)
+#pragma unroll
+                                    for (int e = 0; e < 8; ++e) sh.ored[w][p * 64 + lane * 8 + e] = o[p][e];
+                        __syncthreads();
+                        if (tid < 64 * nsp)
+                            gput(xg + oP + (((int64_t)b * H + h) * nsub + (j0 >> 7)) * 64 + tid, tag,
+                                 __float_as_uint(((sh.ored[0][tid] + sh.ored[1][tid]) + sh.ored[2][tid]) + sh.ored[3][tid]));
+                        __syncthreads();
+                    }
+                }
+            } else
             // ---- F2: P16 = f16(p / sum) . V per 128-key sub-chunk -> partials
             {
                 PHASE_IDS
@@ -1874,6 +2054,8 @@ hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G) {
         a.cl > 128 * NKP || (int64_t)a.nch * a.cl < a.T || (int64_t)a.B * (a.n / 64) * a.nch > PX_TASKS ||
         a.tctx > 512 || a.cl % 128 || (a.beam && a.n_steps != 1) || (a.kv_src && a.kv_src_stride < a.tctx) ||
         ((int64_t)a.B * (a.n / 64) * a.nch + G - 1) / G * a.cl * 4 > XS_BYTES ||  // task scores in LDS
+        (a.xshare && (!a.beam || a.n <= 768 || ((int64_t)(a.n / 64) * a.nch + G - 1) / G * a.B * a.cl * 4 > XS_BYTES ||
+                      a.B * a.nch * 4 > 2048 || a.B * a.nch * 8 > 4096)) ||
         (a.kvl && (a.B != 1 || a.beam || a.L * (a.n / 64) >= G || a.kvcap < 32 || a.kvcap > 512 ||
                    (int64_t)a.kvcap * 256 > (int64_t)a.nres * a.n * 2 || a.vkv < 0)))
         return hipErrorInvalidValue;
