@@ -204,19 +204,7 @@ def test_greedy_tokens_micro(micro_ctx, oracle_micro):
     _greedy_case(micro_ctx, oracle_micro, range(99, 129), 24, 64, 2.0, min_len=18)
 
 
-def test_batch_equals_single(wmi, micro_model):
-    """A clip's results do not depend on its batch (bitwise).  One-row launches
-    default to the fused decoder (PersistArgs::fuse), whose Wo / Wco products
-    are summed per head, so the single-clip runs here use WMI_FUSE=0 — the
-    batched instances' arithmetic; test_fused_matches_unfused bounds the rest."""
-    micro_ctx = _ctx_with_env(wmi, micro_model, {"WMI_FUSE": "0"}, max_clips=3)
-    try:
-        _batch_equals_single(micro_ctx)
-    finally:
-        micro_ctx.close()
-
-
-def _batch_equals_single(micro_ctx):
+def test_batch_equals_single(micro_ctx):
     clips = [synth.synth_pcm_f32(2.0, s) for s in (1, 2, 3)]
     micro_ctx.set_audio_ctx(64)
     micro_ctx.pcm_to_mel_batch(clips)
@@ -378,9 +366,8 @@ def test_beam_search_finishing(wmi, eot_twin_model):
 def test_base_batch_of_8_equals_single(wmi, model_cache):
     """C4's per-GPU shard: 8 x 30 s clips through the batched encoder (M =
     12000 rows per GEMM) and the 8-row persistent decoder give bitwise the
-    single-clip results (which the full-size test pins to the oracle); the
-    single-clip runs without the fused one-row decoder (see test_batch_equals_single)."""
-    ctx = _ctx_with_env(wmi, synth.model_path("base", model_cache), {"WMI_FUSE": "0"}, max_clips=8)
+    single-clip results (which the full-size test pins to the oracle)."""
+    ctx = wmi.WhisperContext.new(synth.model_path("base", model_cache), 0, max_clips=8)
     try:
         clips = [synth.synth_pcm_f32(30.0, 1234 + i) for i in range(8)]
         ctx.pcm_to_mel_batch(clips)
@@ -558,25 +545,9 @@ def test_persistent_matches_chain(wmi, model_cache, model, n_clips, n_ctx):
     last-bit difference may legitimately flip (base seed 41: one at step 10,
     margin 4.9e-4 in the oracle)."""
     path = synth.model_path(model, model_cache)
-    _decoders_agree(wmi, path, n_clips, n_ctx, ({"WMI_PERSIST": "1"}, {"WMI_PERSIST": "0", "WMI_NO_FUSE": "1"}))
-
-
-@pytest.mark.parametrize("model,n_ctx", [("micro", 64), ("micro", 1500), ("tiny.en", 1500), ("base", 1500),
-                                         ("small", 1500)])
-def test_fused_matches_unfused(wmi, model_cache, model, n_ctx):
-    """The fused one-row persistent decoder (self-attention tasks apply their
-    head's Wo column block, cross-attention reducers their head's Wco block;
-    consumers add the per-head partials in head order) against the unfused
-    instance (C and G2 phases, WMI_FUSE=0): the same arithmetic except the
-    order of the Wo / Wco sums, so the teacher-forced logits agree within 2e-3
-    and the greedy ids up to a near-tie (top-2 margin < 2e-3)."""
-    path = synth.model_path(model, model_cache)
-    _decoders_agree(wmi, path, 1, n_ctx, ({"WMI_FUSE": "1"}, {"WMI_FUSE": "0"}))
-
-
-def _decoders_agree(wmi, path, n_clips, n_ctx, envs):
     clips = [synth.synth_pcm_f32(30.0 if n_ctx == 1500 else 2.0, 40 + i) for i in range(n_clips)]
-    ctxs = [_ctx_with_env(wmi, path, env, max_clips=n_clips) for env in envs]
+    ctxs = [_ctx_with_env(wmi, path, env, max_clips=n_clips)
+            for env in ({"WMI_PERSIST": "1"}, {"WMI_PERSIST": "0", "WMI_NO_FUSE": "1"})]
     try:
         out = []
         for ctx in ctxs:

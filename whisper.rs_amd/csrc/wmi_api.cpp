@@ -291,7 +291,6 @@ struct wmi_context {
     // 141.2 us a base step on one box, profiles/r03/ab_r03g_*): off by default
     bool use_kvl = false;
     bool use_xshare = true;           // WMI_XSHARE=0: beam rows read the cross K / V per row
-    bool use_fuse = false;            // WMI_FUSE=1: fused one-row launches (measured slower)
     int n_fallbacks = 0;              // decodes re-run on the kernel chain after a persistent exchange timeout
     PersistLayer *d_players = nullptr;
     uint32_t *d_expfb = nullptr;       // exp fallback list of the persistent decoder [64] + count
@@ -1172,7 +1171,7 @@ int run_encode(wmi_context *ctx, int mel_offset) {
         g.q = ctx->q; g.k = ctx->k; g.vt = ctx->vt; g.T = T; g.Tp = Tp; g.n_state = n;
         HIPCHK(ctx, launch_gemm(s, EPI_QKV, g));
         AttnArgs at{}; at.tune = &ctx->tune;
-        at.q = ctx->q; at.k = ctx->k; at.vt = ctx->vt; at.exp_fb = ctx->d_expfb; at.out = ctx->att; at.out32 = ctx->att32; at.exp_tab = ctx->exp_tab;
+        at.q = ctx->q; at.k = ctx->k; at.vt = ctx->vt; at.out = ctx->att; at.out32 = ctx->att32; at.exp_tab = ctx->exp_tab;
         at.n_exp = ctx->n_exp; at.T = T; at.Tp = Tp; at.H = H; at.n_state = n; at.n_clips = B;
         at.scale = (float)(1.0 / sqrt(64.0));
         HIPCHK(ctx, launch_attn_enc(s, at));
@@ -1624,9 +1623,6 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     // less at eight (845 vs 918 us/step), so by default only when B > 1
     const bool have5 = ctx->use_q5 && !ctx->dec.empty() && ctx->dec[0].wqkv5;
     a.q5 = have5 && (ctx->persist_q5 > 0 || (ctx->persist_q5 < 0 && B > 1)) ? 1 : 0;
-    // fused one-row launches (PersistArgs::fuse): every cross task must run in
-    // the grid's first round (each publishes a slice of x')
-    a.fuse = ctx->use_fuse && B == 1 && !a.q5 && n <= 768 && (int64_t)H * a.nch <= G && H * ((n + 255) / 256) <= G ? 1 : 0;
     return a;
 }
 
@@ -1641,7 +1637,6 @@ void set_kvl(wmi_context *ctx, PersistArgs &pa, int G, int pos_end) {
     if (!ctx->use_kvl || pa.B != 1 || pa.beam || nk >= G || cap > 512 || (int64_t)cap * 256 > (int64_t)pa.nres * n * 2)
         return;
     pa.kvl = 1;
-    pa.fuse = 0;
     pa.kvcap = cap;
     const int64_t vk = ((int64_t)V - (int64_t)pa.nres * (G - nk) + G - 1) / G;
     pa.vkv = (int)(vk > 0 ? vk : 0);
@@ -1958,7 +1953,6 @@ int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_st
                     PersistArgs pa = persist_args(ctx, clip, K, G, np, np, suppress_eot, 1);
                     pa.n_steps = 1;
                     pa.beam = 1;
-                    pa.fuse = 0;
                     pa.cur_tok = ctx->dbstate->tok;
                     pa.kv_src = ctx->dkvsrc;
                     pa.kv_src_stride = hp.n_text_ctx;
@@ -2121,7 +2115,6 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (const char *c = getenv("WMI_FAULT_INJECT")) ctx->fault_inject = atoi(c);
     if (const char *c = getenv("WMI_KVL")) ctx->use_kvl = atoi(c) != 0;
     if (const char *c = getenv("WMI_XSHARE")) ctx->use_xshare = atoi(c) != 0;
-    if (const char *c = getenv("WMI_FUSE")) ctx->use_fuse = atoi(c) != 0;
     ctx->dec_layers = ctx->hp.n_text_layer;
     if (const char *c = getenv("WMI_DEC_LAYERS")) ctx->dec_layers = std::max(1, std::min(atoi(c), ctx->hp.n_text_layer));
     ctx->enc_layers = ctx->hp.n_audio_layer;
@@ -2599,7 +2592,7 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
             HIPCHK(ctx, launch_gemm(s, EPI_GELU16, g));
         } else if (which == 2) {
             AttnArgs at{}; at.tune = &ctx->tune;
-            at.q = ctx->q; at.k = ctx->k; at.vt = ctx->vt; at.exp_fb = ctx->d_expfb; at.out = ctx->att; at.exp_tab = ctx->exp_tab;
+            at.q = ctx->q; at.k = ctx->k; at.vt = ctx->vt; at.out = ctx->att; at.exp_tab = ctx->exp_tab;
             at.n_exp = ctx->n_exp; at.T = T; at.Tp = (int)up(T, 64); at.H = hp.n_audio_head; at.n_state = n;
             at.n_clips = B; at.scale = 0.125f;
             HIPCHK(ctx, launch_attn_enc(s, at));

@@ -216,42 +216,4 @@ __device__ __forceinline__ float dot8(const half8 w, const half8 x, float acc) {
     return acc;
 }
 
-constexpr int EXPFB = 64;  // exp fallback list entries (exp_f16_fast)
-
-// ggml's table_exp_f16 value f16(exp(double(f16 x))) for x <= 0 without a
-// double exp (whose polynomial constants the compiler would keep live in
-// registers across the whole persistent loop): the f32 exp rounds to the same
-// f16 unless it lies within 4 f32 ulps of an f16 rounding midpoint.  Those
-// inputs (~19 of the 31744 non-positive ones) are found once per context on
-// the device (k_exp_fallbacks) and their table values kept in a 64-entry
-// list {j << 16 | value} (0xffffffff-padded) that the kernel holds in LDS:
-// the rare lane reads it with 16 independent LDS loads instead of waiting
-// for a global table load.
-__device__ __forceinline__ bool exp_f16_fast_ok(float arg, f16 &hx, float &hv) {
-    hx = (f16)arg;
-    const float r = expf((float)hx);
-    const uint16_t hr = f2h_bits(r);
-    hv = h2f_bits(hr);
-    const float nb = h2f_bits(r >= hv ? (uint16_t)(hr + 1) : (uint16_t)(hr - 1));
-    const float mid = 0.5f * (hv + nb);
-    const float ulp = __uint_as_float(__float_as_uint(r) & 0x7f800000u) * 1.1920928955078125e-7f;
-    return fabsf(r - mid) > 4.0f * ulp;
-}
-__device__ __forceinline__ float exp_f16_fast(float arg, const uint32_t *fb) {
-    f16 hx;
-    float hv;
-    if (exp_f16_fast_ok(arg, hx, hv)) return hv;
-    const uint32_t j = __builtin_bit_cast(uint16_t, hx) & 0x7fff;
-    uint32_t hit = 0xffffffffu;
-#pragma unroll
-    for (int i = 0; i < EXPFB; i += 4) {
-        const uint4 e = *(const uint4 *)(fb + i);
-        hit = (e.x >> 16) == j ? e.x : hit;
-        hit = (e.y >> 16) == j ? e.y : hit;
-        hit = (e.z >> 16) == j ? e.z : hit;
-        hit = (e.w >> 16) == j ? e.w : hit;
-    }
-    return hit != 0xffffffffu ? h2f_bits((uint16_t)hit) : hv;
-}
-
 }  // namespace wmi

@@ -107,7 +107,6 @@ struct AttnArgs {
     float *out32;                // or f32 output (f32 models: Wo takes it unrounded)
     const uint16_t *exp_tab;     // f16 exp table, negative half
     int n_exp;                   // entries in exp_tab
-    const uint32_t *exp_fb;      // [64] exp fallback list (exp_f16_fast), for the computed-exp build
     int T, Tp, H, n_state, n_clips;
     float scale;
 };
@@ -298,7 +297,7 @@ struct PersistLayer {          // decoder layer weights (device pointers)
 
 // exchange block layout in granules (host and device agree)
 struct XLayout {
-    int x1, x2, x3, q, k, v, o, xq, oc, h, s, m, p, a, wp, wc, xp, ctl, total;
+    int x1, x2, x3, q, k, v, o, xq, oc, h, s, m, p, a, ctl, total;
 };
 constexpr int PX_TASKS = 2048;   // cross-attention (row, head, chunk) tasks
 constexpr int PX_GMAX = 256;     // workgroups
@@ -321,12 +320,7 @@ __host__ __device__ inline XLayout persist_layout(int n, int H, int T) {
     L.m = o; o += PX_TASKS;
     L.p = o; o += R * H * ((T + 127) / 128) * 64;  // 128-key P.V partials
     L.a = o; o += R * PX_GMAX * 2;
-    // fused one-row launches (PersistArgs::fuse): per-head partial products of
-    // Wo and Wco ([H][n] f32 each) and x' published in slices by the cross tasks
-    L.wp = o; o += H * n;
-    L.wc = o; o += H * n;
-    L.xp = o; o += n;
-    L.ctl = o; o += 16;            // ctl[0] low word: abort flag
+    L.ctl = o; o += 16;             // ctl[0] low word: abort flag
     L.total = (o + 15) / 16 * 16;   // whole 128-byte lines (memset size a multiple of 16 B)
     return L;
 }
@@ -376,12 +370,6 @@ struct PersistArgs {
     // attention task per (head, key chunk) covers every row (PersistArgs::nch
     // then counts the chunks of one head: H * nch tasks)
     int xshare;
-    // one-row greedy launches with n <= 768 (f16 weights): the self-attention
-    // task of head h also multiplies its output by Wo's column block h, and
-    // the cross-attention reducer of head h by Wco's: the C and G2 all-to-all
-    // phases disappear (7 hand-offs a layer instead of 9); consumers add the
-    // H partials in head order (wmi_persist.hip, phases B', R, E', H')
-    int fuse;
 };
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G);
 // the inputs whose f32 exp is too close to an f16 midpoint, with their table

@@ -568,20 +568,12 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     const int key = key0 + kb * 32 + ((r + u) & 3) + 8 * ((r + u) >> 2) + 4 * lh;
-#ifdef WMI_ATTN_CEXP
-                    // computed table value (exp_f16_fast: f32 exp, fallback
-                    // list in LDS at tab for the near-midpoint inputs)
-                    (void)n_exp;
-                    float e = exp_f16_fast(v[u], (const uint32_t *)tab);
-                    if (TAIL) e = key < T ? e : 0.0f;
-#else
                     // f16(|v|) = the magnitude bits of f16(v) (v <= 0): the abs is a
                     // free source modifier of the conversion
                     uint32_t i = f2h_bits(fabsf(v[u]));
                     i = i < n_exp ? i : n_exp;  // v_min: index n_exp holds 0
                     if (TAIL) i = key < T ? i : n_exp;
                     const float e = h2f_bits(tab[i]);  // unguarded read (a guarded one branches per element)
-#endif
                     if constexpr (PASS == 1) sum += (double)e;
                     else pa[(r + u) >> 3][(r + u) & 7] = (f16)(e * inv);
                 }
@@ -676,11 +668,7 @@ template <int NW>
 __global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
     uint16_t *tab = (uint16_t *)smraw;
-#ifdef WMI_ATTN_CEXP
-    const int tab_bytes = EXPFB * 4;  // the exp fallback list only
-#else
     const int tab_bytes = (((a.n_exp + 1) * 2 + 15) / 16) * 16;
-#endif
     f16 *Ks = (f16 *)(smraw + tab_bytes);      // [2][64 keys][AT4_LD]
     f16 *Vs = Ks + 2 * AT4_KT * AT4_LD;        // [2][64 dims][AT4_LD] (V^T tile)
     const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
@@ -699,15 +687,11 @@ __global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) qf[s] = *(const half8 *)(Q + (int64_t)qrow * 64 + 16 * s + 8 * lh);
     }
-#ifdef WMI_ATTN_CEXP
-    if (tid < EXPFB) ((uint32_t *)tab)[tid] = a.exp_fb[tid];
-#else
     {
         const int nch = (a.n_exp + 1 + 7) / 8;  // through the 0 at index n_exp
         const uint4 *tsrc = (const uint4 *)a.exp_tab;
         for (int i = tid; i < nch; i += 128 * NW) ((uint4 *)tab)[i] = tsrc[i];
     }
-#endif
     // exchange slots for the key-half partner (the V buffers: unused until sweep 2)
     float *xm = (float *)Vs;                    // [2 NW][64]
     double *xd = (double *)(xm + 2 * NW * 64);  // [2 NW][64]
@@ -768,11 +752,7 @@ __global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
 
 template <int NW>
 static hipError_t attn_enc4_launch(hipStream_t s, const AttnArgs &a) {
-#ifdef WMI_ATTN_CEXP
-    const size_t tabb = EXPFB * 4;
-#else
     const size_t tabb = (((a.n_exp + 1) * 2 + 15) / 16) * 16;
-#endif
     const size_t lds = tabb + (size_t)4 * AT4_KT * AT4_LD * 2;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     hipError_t e = allow_lds(k_attn_enc4<NW>, lds);

@@ -55,6 +55,7 @@ constexpr int PMAXB = 8;                // decoder rows
 constexpr int RNMAX = 16;               // rows of an n-row GEMV per workgroup
 constexpr int SCR_BYTES = 24 * 1024;    // attention / argmax scratch in LDS
 constexpr int NKP = 4;                  // 128-key passes per cross-attention chunk (cl <= 512)
+constexpr int EXPFB = 64;               // exp fallback list entries (exp_f16_fast)
 constexpr int XS_OFF = 1024;            // cross-attention task scores / p in the LDS scratch
 constexpr int XS_BYTES = 8192;          // (workgroup tasks x keys per task x 4 B)
 
@@ -131,14 +132,6 @@ struct PShared {
     int abort_;
 };
 
-// WMI_POLL_SLEEP (build option): s_sleep between re-polls of unmatched
-// granules (units of 64 clocks), easing the sc1 load traffic of a waiting grid
-__device__ __forceinline__ void poll_backoff() {
-#ifdef WMI_POLL_SLEEP
-    __builtin_amdgcn_s_sleep(WMI_POLL_SLEEP);
-#endif
-}
-
 // Poll cnt granules (granule i at addr(i)) until every tag equals `tag`,
 // storing the values to dst[i] (LDS).  Bounded: a dead seam sets the abort
 // word (every poller checks it) and err bit 3, so the grid always drains.
@@ -163,7 +156,6 @@ __device__ __forceinline__ bool gpoll(int cnt, uint32_t tag, F addr, uint32_t *d
                     v[u] = gld(addr(base + PT * u));
                 }
             if (all) break;
-            poll_backoff();
             if ((it & 15) == 15) {
                 if (ld32(abortw)) { ok = false; break; }
                 if (it > PSPIN) {
@@ -586,7 +578,6 @@ __device__ __forceinline__ bool poll_ln1(const uint64_t *src, uint32_t tag, cons
                 v[u] = gld(src + tid + PT * u);
             }
         if (all) break;
-        poll_backoff();
         if ((it & 15) == 15) {
             if (ld32(abortw)) { ok = false; break; }
             if (it > PSPIN) {
@@ -607,75 +598,41 @@ __device__ __forceinline__ bool poll_ln1(const uint64_t *src, uint32_t tag, cons
     return ln1_vals<NS>(xv, P, xs, ok, r1, r2, abort_);
 }
 
-// Fused one-row launches: a residual sum handed off as NH per-head partial
-// products (parts[h][e], tag ptg) instead of the finished vector.  Thread tid
-// polls elements e = tid + PT u of every head, then
-//   x[e] = (((p_0 + p_1) + ... + p_{NH-1}) + bias[e]) + base[e]
-// (the unfused phase's (dot + bias) + residual, with the dot split by head),
-// where base is this workgroup's LDS copy xf (GBASE false) or granules gbase
-// (tag btg, polled with the partials); x goes to xf and through ln1_vals
-template <int NS, int NH, bool GBASE>
-__device__ __forceinline__ bool poll_wsum_ln1(const uint64_t *parts, uint32_t ptg, const float *bias,
-                                              const uint64_t *gbase, uint32_t btg, const Ln1P<NS> &P, float *xf,
-                                              f16 *xs, uint32_t *abortw, uint32_t *err, double *r1, double *r2,
-                                              int *abort_) {
-    constexpr int NE = Ln1P<NS>::NE, NG = NH + (GBASE ? 1 : 0);
-    int tid = (int)threadIdx.x;
-    asm volatile("" : "+v"(tid));
-    float bv[NE];
-    uint64_t v[NE][NG];
-#pragma unroll
-    for (int u = 0; u < NE; ++u) {
-        const int e = tid + PT * u, ec = e < NS ? e : 0;
-        bv[u] = *glb(bias + ec);
-#pragma unroll
-        for (int h = 0; h < NG; ++h) {
-            const uint32_t tg = h < NH ? ptg : btg;
-            v[u][h] = e < NS ? gld(h < NH ? parts + h * NS + e : gbase + e) : ((uint64_t)tg << 32);
-        }
-    }
-    asm volatile("" : : : "memory");  // the bias loads stay ahead of the poll
-    bool ok = true;
-    for (uint32_t it = 0;; ++it) {
-        bool all = true;
-#pragma unroll
-        for (int u = 0; u < NE; ++u)
-#pragma unroll
-            for (int h = 0; h < NG; ++h) {
-                const uint32_t tg = h < NH ? ptg : btg;
-                if ((uint32_t)(v[u][h] >> 32) != tg) {
-                    all = false;
-                    const int e = tid + PT * u;
-                    v[u][h] = gld(h < NH ? parts + h * NS + e : gbase + e);
-                }
-            }
-        if (all) break;
-        poll_backoff();
-        if ((it & 15) == 15) {
-            if (ld32(abortw)) { ok = false; break; }
-            if (it > PSPIN) {
-                st32(abortw, 1u);
-                atomicOr(err, 8u);
-                ok = false;
-                break;
-            }
-        }
-    }
-    float xv[NE];
-#pragma unroll
-    for (int u = 0; u < NE; ++u) {
-        const int e = tid + PT * u, ec = e < NS ? e : 0;
-        float s = __uint_as_float((uint32_t)v[u][0]);
-#pragma unroll
-        for (int h = 1; h < NH; ++h) s = s + __uint_as_float((uint32_t)v[u][h]);
-        const float base = GBASE ? __uint_as_float((uint32_t)v[u][NG - 1]) : xf[ec];
-        xv[u] = (s + bv[u]) + base;
-        if (e < NS) xf[e] = xv[u];
-    }
-    return ln1_vals<NS>(xv, P, xs, ok, r1, r2, abort_);
+// ggml's table_exp_f16 value f16(exp(double(f16 x))) for x <= 0 without a
+// double exp (whose polynomial constants the compiler would keep live in
+// registers across the whole persistent loop): the f32 exp rounds to the same
+// f16 unless it lies within 4 f32 ulps of an f16 rounding midpoint.  Those
+// inputs (~19 of the 31744 non-positive ones) are found once per context on
+// the device (k_exp_fallbacks) and their table values kept in a 64-entry
+// list {j << 16 | value} (0xffffffff-padded) that the kernel holds in LDS:
+// the rare lane reads it with 16 independent LDS loads instead of waiting
+// for a global table load.
+__device__ __forceinline__ bool exp_f16_fast_ok(float arg, f16 &hx, float &hv) {
+    hx = (f16)arg;
+    const float r = expf((float)hx);
+    const uint16_t hr = f2h_bits(r);
+    hv = h2f_bits(hr);
+    const float nb = h2f_bits(r >= hv ? (uint16_t)(hr + 1) : (uint16_t)(hr - 1));
+    const float mid = 0.5f * (hv + nb);
+    const float ulp = __uint_as_float(__float_as_uint(r) & 0x7f800000u) * 1.1920928955078125e-7f;
+    return fabsf(r - mid) > 4.0f * ulp;
 }
-
-// (exp_f16_fast, the f32 exp with the fallback list: wmi_device.h)
+__device__ __forceinline__ float exp_f16_fast(float arg, const uint32_t *fb) {
+    f16 hx;
+    float hv;
+    if (exp_f16_fast_ok(arg, hx, hv)) return hv;
+    const uint32_t j = __builtin_bit_cast(uint16_t, hx) & 0x7fff;
+    uint32_t hit = 0xffffffffu;
+#pragma unroll
+    for (int i = 0; i < EXPFB; i += 4) {
+        const uint4 e = *(const uint4 *)(fb + i);
+        hit = (e.x >> 16) == j ? e.x : hit;
+        hit = (e.y >> 16) == j ? e.y : hit;
+        hit = (e.z >> 16) == j ? e.z : hit;
+        hit = (e.w >> 16) == j ? e.w : hit;
+    }
+    return hit != 0xffffffffu ? h2f_bits((uint16_t)hit) : hv;
+}
 
 // Every phase re-derives its lane indices from an opaque copy of threadIdx.x
 // behind a compiler memory barrier: __syncthreads() fences only LDS, so
@@ -703,8 +660,7 @@ __device__ __forceinline__ bool poll_wsum_ln1(const uint64_t *parts, uint32_t pt
 // BT: rows at compile time (1) or at most (8, runtime B); BEAM: beam-search
 // launches (self-attention history through kv_src; its index registers stay
 // out of the greedy instances)
-// FU: fused one-row launches (PersistArgs::fuse; BT 1, f16, XQF)
-template <int NS, int BT, bool BEAM, bool Q5, bool FU>
+template <int NS, int BT, bool BEAM, bool Q5>
 __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     constexpr int KC = NS / 128;        // 128-element chunks of a K = n row
     constexpr int H = NS / 64;
@@ -713,10 +669,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #define WMI_XQF_KC 6
 #endif
     constexpr bool XQF = KC <= WMI_XQF_KC;  // cross q computed inside the score tasks (registers allow)
-    static_assert(!FU || (BT == 1 && !BEAM && !Q5 && XQF), "fused launches: one row, f16, n <= 768");
-    // fused launches: Wo / Wco column blocks of a head split into RSO row
-    // ranges of PT rows (one output row per thread)
-    constexpr int RSO = (NS + PT - 1) / PT;
     // cross-attention softmax: several rows (8 clips, beam slots) split it in
     // two small hand-offs (chunk maxima, then chunk exp sums; each task's
     // scores stay in LDS) instead of every task sweeping its row's T scores;
@@ -746,11 +698,11 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     f16 *vres = (f16 *)(scr + SCR_BYTES);                                  // [nres][NS] resident vocabulary rows
     // exchange offsets as plain scalars (a struct captured by the lambdas
     // below would be kept in scratch memory)
-    int oX1, oX2, oX3, oQ, oK, oV, oO, oXQ, oOC, oH, oS, oM, oP, oA, oWP, oWC, oXP;
+    int oX1, oX2, oX3, oQ, oK, oV, oO, oXQ, oOC, oH, oS, oM, oP, oA;
     {
         const XLayout X = persist_layout(NS, H, T);
         oX1 = X.x1; oX2 = X.x2; oX3 = X.x3; oQ = X.q; oK = X.k; oV = X.v; oO = X.o; oXQ = X.xq;
-        oOC = X.oc; oH = X.h; oS = X.s; oM = X.m; oP = X.p; oA = X.a; oWP = X.wp; oWC = X.wc; oXP = X.xp;
+        oOC = X.oc; oH = X.h; oS = X.s; oM = X.m; oP = X.p; oA = X.a;
     }
     uint64_t *xg = a.xg;
     uint32_t *abortw = (uint32_t *)(xg + persist_layout(NS, H, T).ctl);
@@ -768,7 +720,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     part(4 * NS, true, rh0, rh1);  // W0 rows
     // LDS-resident self-attention K / V (PersistArgs::kvl): workgroups
     // [0, L H) own one (layer, head) each
-    const bool kvl = BT == 1 && !FU && a.kvl;
+    const bool kvl = BT == 1 && a.kvl;
     const int nkw = kvl ? L * H : 0;
     const bool kvw = wg < nkw;
     f16 *Kl = vres, *Vl = vres + (size_t)a.kvcap * 64;  // [kvcap][64] each (K chunks swizzled)
@@ -914,6 +866,14 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         else if (which == 1) pk = pack2(v * qs, vn * qs);
                         else pk = pack2(eb + v, ebn + vn);
                         const int64_t gi = (which == 0 ? oQ : which == 1 ? oK : oV) + b * (NS / 2) + c / 2;
+                        // KV-cache row pos: an sc1 (write-through) store with no
+                        // tag.  It is read from step pos + 1 on, by loads issued
+                        // after that step's q/k/v poll; every hand-off between
+                        // this store and that poll passes through a poll of this
+                        // wave (its s_waitcnt vmcnt(0) on gfx9 also drains the
+                        // store), so the row is in L2/memory before any granule
+                        // that transitively signals it (documented,
+                        // no fence — an agent release costs ~1.7 us per phase)
                         if (which > 0)
                             st32((uint32_t *)((which == 1 ? kc : vc) + ((int64_t)b * tctx + pos) * NS + c), pk);
                         gput(xg + gi, tag, pk);
@@ -931,9 +891,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 f16 *qn = (f16 *)scr, *kn = qn + 64, *vn = qn + 128;  // this step's q, k, v of the head
                 uint16_t *P16 = (uint16_t *)(scr + 512);                 // [512]
                 // (K / V owners: workgroup l H + h takes head h of layer l)
-                // (fused launches: task t = head h, Wo row range s)
-                for (int t = kvl ? wg - l * H : wg; t >= 0 && t < (FU ? H * RSO : B * H); t += G) {
-                    const int b = FU ? 0 : t / H, h = FU ? t / RSO : t - b * H;
+                for (int t = kvl ? wg - l * H : wg; t >= 0 && t < B * H; t += G) {
+                    const int b = t / H, h = t - b * H;
                     if (kvl) {
                         // K / V from this workgroup's LDS copy and no exchange
                         // between its waves: every wave computes all M = pos + 1
@@ -1081,16 +1040,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         vv[i] = j < pos ? bload_sc1(rv, (uint32_t)((((int64_t)srv[i] * tctx + j) * NS + h * 64 + doct * 8) * 2)) : z8;
 #endif
                     }
-                    // fused: this thread's Wo row (row range s), column block h
-                    const int wrow = FU ? (t - h * RSO) * PT + tid : 0;
-                    half8 wo8[FU ? 8 : 1];
-                    if constexpr (FU) {
-                        const f16 *wr = (const f16 *)P.wo + (int64_t)(wrow < NS ? wrow : NS - 1) * NS + h * 64;
-#pragma unroll
-                        for (int c = 0; c < 8; ++c) wo8[c] = sld((const half8 *)(wr + 8 * c));
-                    } else {
-                        wo8[0] = z8;
-                    }
                     PREFETCH_ISSUED
                     __syncthreads();
                     const int64_t hq = b * (NS / 2) + h * 32;  // q, k, v granule blocks lie 4 NS apart
@@ -1175,30 +1124,18 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #pragma unroll
                         for (int e = 0; e < 8; ++e) sh.ored[w][lane * 8 + e] = o[e];
                     __syncthreads();
-                    f16 *o16 = (f16 *)(scr + 1536);  // fused: the head's output, f16 (the f16 pairs of o)
                     if (tid < 32) {
                         const int d = 2 * tid;
                         const float o0 = ((sh.ored[0][d] + sh.ored[1][d]) + sh.ored[2][d]) + sh.ored[3][d];
                         const float o1 = ((sh.ored[0][d + 1] + sh.ored[1][d + 1]) + sh.ored[2][d + 1]) + sh.ored[3][d + 1];
-                        if constexpr (FU) *(uint32_t *)(o16 + d) = pack2(o0, o1);
-                        else gput(xg + oO + b * (NS / 2) + h * 32 + tid, tag, pack2(o0, o1));
-                    }
-                    if constexpr (FU) {
-                        // Wo[row][h 64 .. h 64 + 63] . o_h, in d order -> head h's partial
-                        __syncthreads();
-                        float acc = 0.0f;
-#pragma unroll
-                        for (int c = 0; c < 8; ++c) acc = dot8(wo8[c], *(const half8 *)(o16 + 8 * c), acc);
-                        if (wrow < NS) gput(xg + oWP + h * NS + wrow, tag, __float_as_uint(acc));
-                        __syncthreads();  // o16 / ored of a next task
+                        gput(xg + oO + b * (NS / 2) + h * 32 + tid, tag, pack2(o0, o1));
                     }
                 }
             }
 
             PSTAMP(l * 32 + 1)
             // ---- C: Wo rows + residual -> x' ---------------------------
-            // (fused launches: B' published the per-head Wo partials)
-            if constexpr (!FU) {
+            {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 2);
                 GSet<KC, 1, KS_N, Q5> S;
@@ -1343,19 +1280,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         else ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
                         PREFETCH_ISSUED
                         __syncthreads();
-                        if constexpr (FU) {
-                            // x' = (sum of the H Wo partials + bo) + x (x: this
-                            // workgroup's copy from phase A), then LNc
-                            if (k == 1) {  // (the first task of the workgroup; later ones reuse xs)
-                                if (!poll_wsum_ln1<NS, H, false>(xg + oWP, ptag(pos, L, l, 1), P.bo, nullptr, 0u, l1, xf, xs,
-                                                                 abortw, a.err, sh.redd, sh.redd2, &sh.abort_))
-                                    return;
-                                // x' for phase H', published in slices by the cross tasks
-                                const int per = (NS + ntask - 1) / ntask;
-                                if (tid < per && t * per + tid < NS)
-                                    gput(xg + oXP + t * per + tid, ptag(pos, L, l, 3), __float_as_uint(xf[t * per + tid]));
-                            }
-                        } else if constexpr (BT == 1) {
+                        if constexpr (BT == 1) {
                             if (!poll_ln1<NS>(xg + oX2 + b * NS, ptag(pos, L, l, 2), l1, xf, xs, abortw, a.err, sh.redd,
                                               sh.redd2, &sh.abort_))
                                 return;
@@ -1764,47 +1689,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }  // FSPLIT
 
             PSTAMP(l * 32 + 6)
-            // ---- R (fused launches): per (head h, Wco row range s) the G1 sum
-            // of the head's 128-key partials -> cross o_h (f16, as G1 rounds
-            // it), then Wco[row][h 64 .. h 64 + 63] . o_h -> head h's partial
-            if constexpr (FU) {
-                PHASE_IDS
-                const uint32_t tag = ptag(pos, L, l, 8);
-                float *pp = (float *)scr;                      // [nsub][64]
-                f16 *o16 = (f16 *)(scr + SCR_BYTES - 256);     // [64]
-                for (int t = wg; t < H * RSO; t += G) {
-                    const int h = t / RSO, wrow = (t - h * RSO) * PT + tid;
-                    half8 wc8[8];
-                    const f16 *wr = (const f16 *)P.wco + (int64_t)(wrow < NS ? wrow : NS - 1) * NS + h * 64;
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) wc8[c] = sld((const half8 *)(wr + 8 * c));
-                    PREFETCH_ISSUED
-                    __syncthreads();
-                    const bool ok = gpoll(nsub * 64, ptag(pos, L, l, 6), ptr_u64(xg + oP + (int64_t)h * nsub * 64),
-                                          (uint32_t *)pp, abortw, a.err);
-                    if (check(ok)) return;
-                PSTAMP(l * 32 + 23)
-                    if (tid < 64) {  // in chunk order (G1's sum)
-                        float sv = 0.0f;
-                        for (int c0 = 0; c0 < nsub; c0 += 8) {
-                            float v[8];
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) v[u] = pp[(c0 + u < nsub ? c0 + u : nsub - 1) * 64 + tid];
-#pragma unroll
-                            for (int u = 0; u < 8; ++u)
-                                if (c0 + u < nsub) sv = c0 + u == 0 ? v[u] : sv + v[u];
-                        }
-                        o16[tid] = (f16)sv;
-                    }
-                    __syncthreads();
-                    float acc = 0.0f;
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) acc = dot8(wc8[c], *(const half8 *)(o16 + 8 * c), acc);
-                    if (wrow < NS) gput(xg + oWC + h * NS + wrow, tag, __float_as_uint(acc));
-                }
-            }
             // ---- G1: chunk partials summed in chunk order -> cross o ---------
-            if constexpr (!FU) {
+            {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 7);
                 float *pp = (float *)scr;  // [nsub][64]
@@ -1835,7 +1721,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 
             PSTAMP(l * 32 + 7)
             // ---- G2: Wco rows + residual -> x'' -------------------------
-            if constexpr (!FU) {
+            {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 8);
                 GSet<KC, 1, KS_N, Q5> S;
@@ -1869,14 +1755,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 else ln_params<NS>(P.ln2_w, P.ln2_b, lp, lane);
                 PREFETCH_ISSUED
                 __syncthreads();
-                if constexpr (FU) {
-                    // x'' = (sum of the H Wco partials + bco) + x' (x' from the
-                    // cross tasks' slices); this workgroup's residual rows for I
-                    if (!poll_wsum_ln1<NS, H, true>(xg + oWC, ptag(pos, L, l, 8), P.bco, xg + oXP, ptag(pos, L, l, 3), l1, xf,
-                                                    xs, abortw, a.err, sh.redd, sh.redd2, &sh.abort_))
-                        return;
-                    for (int i = tid; i < rn; i += PT) sh.xres[0][i] = xf[rn0 + i];
-                } else if constexpr (BT == 1) {
+                if constexpr (BT == 1) {
                     if (!poll_ln1<NS>(xg + oX3, ptag(pos, L, l, 8), l1, xf, xs, abortw, a.err, sh.redd, sh.redd2, &sh.abort_))
                         return;
                 } else {
@@ -2056,13 +1935,13 @@ size_t persist_lds(int B) {
 }
 constexpr size_t LDS_CU = 160 * 1024;
 
-template <int NS, int BT, bool BEAM, bool Q5, bool FU = false>
+template <int NS, int BT, bool BEAM, bool Q5>
 hipError_t launch_nsb(hipStream_t s, const PersistArgs &a, int G) {
     const size_t lds = persist_lds<NS>(a.B) + (size_t)a.nres * NS * 2;
-    hipError_t e = hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM, Q5, FU>,
+    hipError_t e = hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM, Q5>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_dec_persist<NS, BT, BEAM, Q5, FU>), dim3(G), dim3(PT), lds, s, a);
+    hipLaunchKernelGGL((k_dec_persist<NS, BT, BEAM, Q5>), dim3(G), dim3(PT), lds, s, a);
     return hipGetLastError();
 }
 #ifndef WMI_PERSIST_Q5_TU
@@ -2072,16 +1951,14 @@ template <int NS>
 hipError_t launch_ns(hipStream_t s, const PersistArgs &a, int G) {
     if (a.beam) return launch_nsb<NS, PMAXB, true, false>(s, a, G);
     if (a.q5) return launch_persist_q5(s, a, G);
-    if constexpr (NS <= 768)
-        if (a.fuse) return launch_nsb<NS, 1, false, false, true>(s, a, G);
     return a.B == 1 ? launch_nsb<NS, 1, false, false>(s, a, G) : launch_nsb<NS, PMAXB, false, false>(s, a, G);
 }
 #endif
 
-template <int NS, int BT, bool BEAM, bool Q5, bool FU = false>
+template <int NS, int BT, bool BEAM, bool Q5>
 int grid_nsb(int device, int B, int V, int *nres) {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, (const void *)k_dec_persist<NS, BT, BEAM, Q5, FU>) != hipSuccess) return 0;
+    if (hipFuncGetAttributes(&fa, (const void *)k_dec_persist<NS, BT, BEAM, Q5>) != hipSuccess) return 0;
     const size_t base = persist_lds<NS>(B), avail = LDS_CU - fa.sharedSizeBytes - 1024;
     if (base > avail) return 0;
     // resident vocabulary rows: as many of a workgroup's rows as the LDS holds
@@ -2089,11 +1966,11 @@ int grid_nsb(int device, int B, int V, int *nres) {
     int nr = (int)((avail - base) / (NS * 2));
     *nres = nr < rpw ? nr : rpw;
     const size_t lds = base + (size_t)*nres * NS * 2;
-    if (hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM, Q5, FU>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM, Q5>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess)
         return 0;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dec_persist<NS, BT, BEAM, Q5, FU>, PT, lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dec_persist<NS, BT, BEAM, Q5>, PT, lds) != hipSuccess ||
         per_cu < 1)
         return 0;
     hipDeviceProp_t prop;
@@ -2142,7 +2019,6 @@ int grid_ns(int device, int B, int V, int *nres) {
     };
     if (B == 1) {
         take(grid_nsb<NS, 1, false, false>(device, B, V, &ni));
-        if constexpr (NS <= 768) take(grid_nsb<NS, 1, false, false, true>(device, B, V, &ni));
     } else {
         take(grid_nsb<NS, PMAXB, false, false>(device, B, V, &ni));
         take(grid_nsb<NS, PMAXB, true, false>(device, B, V, &ni));
@@ -2189,9 +2065,7 @@ hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G) {
         (a.xshare && (!a.beam || a.n <= 768 || ((int64_t)(a.n / 64) * a.nch + G - 1) / G * a.B * a.cl * 4 > XS_BYTES ||
                       a.B * a.nch * 4 > 2048 || a.B * a.nch * 8 > 4096)) ||
         (a.kvl && (a.B != 1 || a.beam || a.L * (a.n / 64) >= G || a.kvcap < 32 || a.kvcap > 512 ||
-                   (int64_t)a.kvcap * 256 > (int64_t)a.nres * a.n * 2 || a.vkv < 0)) ||
-        (a.fuse && (a.B != 1 || a.beam || a.q5 || a.kvl || a.n > 768 || (int64_t)(a.n / 64) * a.nch > G ||
-                    (a.n / 64) * ((a.n + PT - 1) / PT) > G)))
+                   (int64_t)a.kvcap * 256 > (int64_t)a.nres * a.n * 2 || a.vkv < 0)))
         return hipErrorInvalidValue;
     switch (a.n) {
         case 128: return launch_ns<128>(s, a, G);
