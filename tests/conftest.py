@@ -19,6 +19,7 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def model_cache(tmp_path_factory):
     d = os.environ.get("WMI_MODEL_CACHE") or str(tmp_path_factory.mktemp("models"))
+    os.makedirs(d, exist_ok=True)
     os.environ["WMI_MODEL_CACHE"] = d
     return d
 

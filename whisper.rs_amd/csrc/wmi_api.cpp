@@ -281,7 +281,7 @@ struct wmi_context {
     bool checksums = false;           // WMI_CHECKSUMS=1: the reference's stage sums (debug prints)
     float cks[5] = {0, 0, 0, 0, 0};   // _hann, samples, filters, mel before normalisation, mel window
     bool use_persist = true;          // WMI_PERSIST=0: kernel chain instead
-    int persist_q5 = -1;              // WMI_PERSIST_Q5: 1 always, 0 never, default when B > 1
+    int persist_q5 = -1;              // WMI_PERSIST_Q5: 0 = decoder GEMVs on the f16 copies (default: q5_1 blocks)
     bool persist_logits = false;      // WMI_PERSIST_LOGITS=1: also store every step's logits (dlogits)
     int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
     int enc_layers = 0;               // WMI_ENC_LAYERS (debug): run only the first encoder layers
@@ -1618,11 +1618,14 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     a.xg = ctx->d_xg; a.err = ctx->derr;
     a.nres = ctx->persist_nres[B];
     a.logits_out = ctx->persist_logits ? ctx->dlogits : nullptr;
-    // q5_1 blocks in the persistent GEMVs: the dequantisation VALU costs more
-    // than the smaller stream saves at one row (small: 357 vs 329 us/step) and
-    // less at eight (845 vs 918 us/step), so by default only when B > 1
+    // q5_1 blocks in the persistent GEMVs (the ggml dequant x activation
+    // product of a q5_1 file), dequantised inside each phase's poll so the
+    // VALU overlaps the seam: small q5_1, one clip 43.1 ms decode vs 42.0 ms
+    // on the f16 copies (a one-row step is latency-bound: the 2.7x smaller
+    // stream buys nothing there), eight clips 111.6 vs 112.4 ms
+    // (profiles/r03/q5_ab.txt); WMI_PERSIST_Q5=0 selects the f16 copies
     const bool have5 = ctx->use_q5 && !ctx->dec.empty() && ctx->dec[0].wqkv5;
-    a.q5 = have5 && (ctx->persist_q5 > 0 || (ctx->persist_q5 < 0 && B > 1)) ? 1 : 0;
+    a.q5 = have5 && ctx->persist_q5 != 0 ? 1 : 0;
     return a;
 }
 
@@ -2653,7 +2656,11 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
         const double L = hp.n_text_layer, Tx = T;
         int32_t prompt[8];
         const int np = prompt_tokens(ctx, prompt), steps = np + ctx->staged_n_decode - 1;
-        const double w_step = L * (28.0 * nt * nt + 68.0 * nt) + V * nt * 2 + 2 * nt * 4;
+        // (q5_1 GEMVs: Wqkv, Wo, Wco, W0, W1 = 13 n^2 weights at 24 bytes a
+        // 32-weight block; Wcq stays f16)
+        const bool dq5 = ctx->use_q5 && !ctx->dec.empty() && ctx->dec[0].wqkv5 && ctx->persist_q5 != 0;
+        const double w_mat = dq5 ? 13.0 * nt * nt * 0.75 + 2.0 * nt * nt : 28.0 * nt * nt;
+        const double w_step = L * (w_mat + 68.0 * nt) + V * nt * 2 + 2 * nt * 4;
         double bytes = 0, flops = 0;
         for (int b0 = 0; b0 < B; b0 += 8) {
             const double rows = B - b0 < 8 ? B - b0 : 8;
@@ -2666,7 +2673,8 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
         }
         out->alg_bytes = bytes;
         out->alg_flops = flops;
-        snprintf(out->name, sizeof out->name, "k_dec_persist<%d,%d> (%d steps)", (int)nt, B == 1 ? 1 : 8, steps);
+        snprintf(out->name, sizeof out->name, "k_dec_persist<%d,%d%s> (%d steps)", (int)nt, B == 1 ? 1 : 8,
+                 dq5 ? ",Q5" : "", steps);
     } else {
         const double N = hp.n_text_layer * 2.0 * nt;
         out->alg_flops = 2.0 * M * N * n;

@@ -132,12 +132,19 @@ struct PShared {
     int abort_;
 };
 
+struct NoPre {
+    __device__ void operator()() const {}
+};
 // Poll cnt granules (granule i at addr(i)) until every tag equals `tag`,
 // storing the values to dst[i] (LDS).  Bounded: a dead seam sets the abort
 // word (every poller checks it) and err bit 3, so the grid always drains.
-template <int PU = 4, typename F>  // PU: granules in flight per thread
-__device__ __forceinline__ bool gpoll(int cnt, uint32_t tag, F addr, uint32_t *dst, uint32_t *abortw, uint32_t *err) {
-    bool ok = true;
+// pre() runs once in every thread while its first round of loads is in
+// flight (the q5_1 phases dequantise their prefetched weights there, so the
+// VALU work overlaps the seam instead of following it).
+template <int PU = 4, typename F, typename Pre = NoPre>  // PU: granules in flight per thread
+__device__ __forceinline__ bool gpoll(int cnt, uint32_t tag, F addr, uint32_t *dst, uint32_t *abortw, uint32_t *err,
+                                      Pre pre = Pre{}) {
+    bool ok = true, pre_done = false;
     int tid = (int)threadIdx.x;
     asm volatile("" : "+v"(tid));
     for (int base = tid; base < cnt && ok; base += PT * PU) {
@@ -146,6 +153,10 @@ __device__ __forceinline__ bool gpoll(int cnt, uint32_t tag, F addr, uint32_t *d
         for (int u = 0; u < PU; ++u) {
             const int i = base + PT * u;
             v[u] = i < cnt ? gld(addr(i)) : ((uint64_t)tag << 32);
+        }
+        if (!pre_done) {
+            pre();
+            pre_done = true;
         }
         for (uint32_t it = 0;; ++it) {
             bool all = true;
@@ -172,6 +183,7 @@ __device__ __forceinline__ bool gpoll(int cnt, uint32_t tag, F addr, uint32_t *d
             if (i < cnt) dst[i] = (uint32_t)v[u];
         }
     }
+    if (!pre_done) pre();
     return ok;
 }
 
@@ -205,12 +217,14 @@ template <>
 struct WChunk<true> {
     uint32_t n;
     u32x2v hd;
+    half8 h;  // the dequantised weights (wc_pre), read by wc_h8
 };
 template <bool Q5>
 __device__ __forceinline__ void wc_zero(WChunk<Q5> &c) {
     if constexpr (Q5) {
         c.n = 0u;
         c.hd = u32x2v{0u, 0u};  // d = m = 0: dequantises to +0
+        c.h = half8{};
     } else {
         c.h = half8{};
     }
@@ -225,11 +239,19 @@ __device__ __forceinline__ void wc_load(WChunk<Q5> &c, const WMat &m, int64_t e)
         c.h = sld((const half8 *)((const f16 *)m.w + e));
     }
 }
-// sh = e % 32 (a lane's offset inside its block: (l16 & 3) * 8)
+// sh = e % 32 (a lane's offset inside its block: (l16 & 3) * 8).  q5_1
+// chunks are dequantised once by wc_pre (called inside the phase's poll,
+// gpoll / poll_ln1 `pre`), to exactly the loader's f16 copy
 template <bool Q5>
-__device__ __forceinline__ half8 wc_h8(const WChunk<Q5> &c, int sh) {
-    if constexpr (Q5) return q5_half8(c.n, c.hd[0], c.hd[1], sh);
-    else return c.h;
+__device__ __forceinline__ void wc_pre(WChunk<Q5> &c, int sh) {
+    if constexpr (Q5) {
+        c.h = q5_half8(c.n, c.hd[0], c.hd[1], sh);
+        asm volatile("" : "+v"(c.h));  // computed here, not sunk to the first use
+    }
+}
+template <bool Q5>
+__device__ __forceinline__ half8 wc_h8(const WChunk<Q5> &c, int) {
+    return c.h;
 }
 
 // ---- GEMV over this workgroup's rows: quarter-wave (16 lanes) per row, row
@@ -240,6 +262,14 @@ struct WSet {
     WChunk<Q5> w[NP][KCH];
     float bias[NP];
 };
+
+template <int KCH, int NP, bool Q5>
+__device__ __forceinline__ void wset_pre(WSet<KCH, NP, Q5> &S, int l16) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int c = 0; c < KCH; ++c) wc_pre(S.w[p][c], (l16 & 3) * 8);
+}
 
 template <int KCH, int NP, bool Q5>
 __device__ __forceinline__ void wset_load(WSet<KCH, NP, Q5> &S, const WMat &m, const float *bias, int K, int rb, int r1,
@@ -358,6 +388,12 @@ __host__ __device__ constexpr int split_of(int kch, int rows) {
 }
 
 template <int KCH, int KS, bool Q5>
+__device__ __forceinline__ void wsplit_pre(WSplit<KCH, KS, Q5> &S, int l16) {
+#pragma unroll
+    for (int c = 0; c < WSplit<KCH, KS, Q5>::CQ; ++c) wc_pre(S.w[c], (l16 & 3) * 8);
+}
+
+template <int KCH, int KS, bool Q5>
 __device__ __forceinline__ void wsplit_load(WSplit<KCH, KS, Q5> &S, const WMat &m, int K, int rb, int r1, int slot,
                                             int l16) {
     constexpr int CQ = WSplit<KCH, KS, Q5>::CQ;
@@ -418,6 +454,7 @@ struct GSet {
         bias = 0.0f;
         if (b && slot < 16 / KS && rb + slot < r1) bias = *glb(b + rb + slot);
     }
+    __device__ __forceinline__ void pre(int l16) { wsplit_pre(s, l16); }
     template <int BT, typename Epi>
     __device__ __forceinline__ void dot(const f16 *xs, int K, int B, int rb, int r1, int slot, int l16, float *kpart,
                                         Epi &&epi) const {
@@ -430,6 +467,7 @@ struct GSet<KCH, NP, 1, Q5> {
     __device__ __forceinline__ void load(const WMat &W, const float *b, int K, int rb, int r1, int slot, int l16) {
         wset_load(s, W, b, K, rb, r1, slot, l16);
     }
+    __device__ __forceinline__ void pre(int l16) { wset_pre(s, l16); }
     template <int BT, typename Epi>
     __device__ __forceinline__ void dot(const f16 *xs, int K, int B, int rb, int r1, int slot, int l16, float *,
                                         Epi &&epi) const {
@@ -556,9 +594,10 @@ __device__ __forceinline__ bool ln1_vals(const float (&xv)[Ln1P<NS>::NE], const 
 }
 // poll one row's NS f32 granules (src[e], tag) into registers and xf, then
 // ln1_vals; false: the grid is aborting
-template <int NS>
+template <int NS, typename Pre = NoPre>
 __device__ __forceinline__ bool poll_ln1(const uint64_t *src, uint32_t tag, const Ln1P<NS> &P, float *xf, f16 *xs,
-                                         uint32_t *abortw, uint32_t *err, double *r1, double *r2, int *abort_) {
+                                         uint32_t *abortw, uint32_t *err, double *r1, double *r2, int *abort_,
+                                         Pre pre = Pre{}) {
     constexpr int NE = Ln1P<NS>::NE;
     int tid = (int)threadIdx.x;
     asm volatile("" : "+v"(tid));
@@ -568,6 +607,7 @@ __device__ __forceinline__ bool poll_ln1(const uint64_t *src, uint32_t tag, cons
         const int e = tid + PT * u;
         v[u] = e < NS ? gld(src + e) : ((uint64_t)tag << 32);
     }
+    pre();  // (see gpoll)
     bool ok = true;
     for (uint32_t it = 0;; ++it) {
         bool all = true;
@@ -820,6 +860,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         if (wg == 0 && tid < B && pos - a.feed_len < a.out_stride)
                             a.tokens_out[tid * a.out_stride + (pos - a.feed_len)] = sh.tok[tid];
                     }
+                    S.pre(l16);  // (no poll to hide it behind in layer 0)
                     // x = te[tok] + pe[pos]  (get_rows f16 -> f32, add)
                     for (int i = tid; i < B * NS / 4; i += PT) {
                         const int b = (i * 4) / NS, e = i * 4 - b * NS;
@@ -838,10 +879,11 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 } else {
                     if constexpr (BT == 1) {
                         if (!poll_ln1<NS>(xg + oX1, ptag(pos, L, l - 1, 10), l1, xf, xs, abortw, a.err, sh.redd, sh.redd2,
-                                          &sh.abort_))
+                                          &sh.abort_, [&] { S.pre(l16); }))
                             return;
                     } else {
-                        const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l - 1, 10), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
+                        const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l - 1, 10), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err,
+                                                   [&] { S.pre(l16); });
                         if (check(ok)) return;
                     }
                 PSTAMP(l * 32 + 16)
@@ -1143,7 +1185,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 S.load(lmat<Q5>(P.wo, P.wo5, NS * NS), P.bo, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll<PUX>(B * NS / 2, ptag(pos, L, l, 1), ptr_u64(xg + oO), (uint32_t *)xs, abortw, a.err);
+                const bool ok = gpoll<PUX>(B * NS / 2, ptag(pos, L, l, 1), ptr_u64(xg + oO), (uint32_t *)xs, abortw, a.err,
+                                           [&] { S.pre(l16); });
                 if (check(ok)) return;
                 PSTAMP(l * 32 + 18)
                 if (act)
@@ -1729,7 +1772,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 S.load(lmat<Q5>(P.wco, P.wco5, NS * NS), P.bco, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll<PUX>(B * NS / 2, ptag(pos, L, l, 7), ptr_u64(xg + oOC), (uint32_t *)xs, abortw, a.err);
+                const bool ok = gpoll<PUX>(B * NS / 2, ptag(pos, L, l, 7), ptr_u64(xg + oOC), (uint32_t *)xs, abortw, a.err,
+                                           [&] { S.pre(l16); });
                 if (check(ok)) return;
             PSTAMP(l * 32 + 24)
                 if (act)
@@ -1756,10 +1800,12 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PREFETCH_ISSUED
                 __syncthreads();
                 if constexpr (BT == 1) {
-                    if (!poll_ln1<NS>(xg + oX3, ptag(pos, L, l, 8), l1, xf, xs, abortw, a.err, sh.redd, sh.redd2, &sh.abort_))
+                    if (!poll_ln1<NS>(xg + oX3, ptag(pos, L, l, 8), l1, xf, xs, abortw, a.err, sh.redd, sh.redd2, &sh.abort_,
+                                      [&] { S.pre(l16); }))
                         return;
                 } else {
-                    const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l, 8), ptr_u64(xg + oX3), (uint32_t *)xf, abortw, a.err);
+                    const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, l, 8), ptr_u64(xg + oX3), (uint32_t *)xf, abortw, a.err,
+                                               [&] { S.pre(l16); });
                     if (check(ok)) return;
                     ln_rows<NS>(xf, lp, xs, B, w, lane);
                 }
@@ -1786,7 +1832,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 S.load(lmat<Q5>(P.w1, P.w15, 4 * NS * NS), P.b1, 4 * NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
                 __syncthreads();
-                const bool ok = gpoll<PUH>(B * 2 * NS, ptag(pos, L, l, 9), ptr_u64(xg + oH), (uint32_t *)xs, abortw, a.err);
+                const bool ok = gpoll<PUH>(B * 2 * NS, ptag(pos, L, l, 9), ptr_u64(xg + oH), (uint32_t *)xs, abortw, a.err,
+                                           [&] { S.pre(l16); });
                 if (check(ok)) return;
                 PSTAMP(l * 32 + 26)
                 if (act)
