@@ -46,7 +46,7 @@ def lib():
         L.or_decode_greedy.argtypes = [vp, hp_, hp_, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.POINTER(i32), fp]
         L.or_dequant.argtypes = [C.c_int, C.c_void_p, C.c_int64, hp_]
         L.or_decode_beam.argtypes = [vp, hp_, hp_, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.POINTER(i32),
-                                     C.POINTER(C.c_double), C.POINTER(C.c_float)]
+                                     C.POINTER(C.c_double), C.POINTER(C.c_float), fp]
         _lib = L
     return _lib
 
@@ -166,16 +166,21 @@ class OracleModel:
             raise OracleError(rc, "decode_greedy")
         return toks[:n.value], margins[:n.value]
 
-    def decode_beam(self, ck, cv, beam: int, max_tokens: int, suppress_eot: bool = False, n_threads: int = 8):
-        """Beam search (wmi_oracle.h): (tokens, score, smallest selection margin)."""
+    def decode_beam(self, ck, cv, beam: int, max_tokens: int, suppress_eot: bool = False, n_threads: int = 8,
+                    step_gaps: bool = False):
+        """Beam search (wmi_oracle.h): (tokens, score, smallest selection margin),
+        plus each step's selection margin when step_gaps."""
         toks = np.zeros(max_tokens + 1, np.int32)
         n = C.c_int32()
         score = C.c_double()
         gap = C.c_float()
+        sg = np.zeros(max_tokens, np.float32)
         rc = lib().or_decode_beam(self.h, ck, cv, ck.shape[1], beam, max_tokens, int(suppress_eot), n_threads, toks,
-                                  C.byref(n), C.byref(score), C.byref(gap))
+                                  C.byref(n), C.byref(score), C.byref(gap), sg)
         if rc:
             raise OracleError(rc, "decode_beam")
+        if step_gaps:
+            return toks[:n.value], score.value, gap.value, sg
         return toks[:n.value], score.value, gap.value
 
 

@@ -1256,7 +1256,7 @@ static double row_lse(const float *lg, int V) {
 
 int or_decode_beam(const or_model *m, const uint16_t *cross_k, const uint16_t *cross_v, int n_ctx, int beam,
                    int max_tokens, int suppress_eot, int nt, int32_t *tokens_out, int32_t *n_out, double *score_out,
-                   float *min_gap) {
+                   float *min_gap, float *step_gap) {
     if (n_ctx <= 0) n_ctx = m->hp[HP_N_AUDIO_CTX];
     if (beam < 1 || beam > 8 || max_tokens < 1) return WMI_E_INVALID_ARG;
     int32_t prompt[8];
@@ -1280,6 +1280,8 @@ int or_decode_beam(const or_model *m, const uint16_t *cross_k, const uint16_t *c
     int n_active = 1, t = 0;
     tok[0] = prompt[np - 1];
     score[0] = 0.0;
+    if (step_gap)
+        for (int i = 0; i < max_tokens; ++i) step_gap[i] = INFINITY;
     for (t = 0; t < max_tokens && n_fin < K; ++t, ++pos) {
         int nc = 0;
         for (int b = 0; b < n_active; ++b) {
@@ -1327,6 +1329,7 @@ int or_decode_beam(const or_model *m, const uint16_t *cross_k, const uint16_t *c
             if (cands[i].id != eot) {
                 const float g = (float)(nscore[na - 1] - cands[i].score);
                 gap = g < gap ? g : gap;
+                if (step_gap) step_gap[t] = g;
                 break;
             }
         for (int s = 0; s < na; ++s) {

@@ -94,10 +94,12 @@ int or_decode_greedy(const or_model *m, const uint16_t *cross_k, const uint16_t 
  *    K of: finished hypotheses in order, then active ones in slot order.
  * tokens_out receives the chosen sequence (with its EOT if finished);
  * min_gap (optional) the smallest selection margin met (last kept vs first
- * rejected candidate at every step, best vs second in the final choice). */
+ * rejected candidate at every step, best vs second in the final choice);
+ * step_gap (optional, [max_tokens]) each step's selection margin (INFINITY
+ * where none was met). */
 int or_decode_beam(const or_model *m, const uint16_t *cross_k, const uint16_t *cross_v, int n_ctx, int beam,
                    int max_tokens, int suppress_eot, int n_threads, int32_t *tokens_out, int32_t *n_out,
-                   double *score_out, float *min_gap);
+                   double *score_out, float *min_gap, float *step_gap);
 
 #ifdef __cplusplus
 }

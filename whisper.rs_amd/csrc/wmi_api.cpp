@@ -907,15 +907,39 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
     }
     HIPCHK(ctx, hipMalloc(&ctx->d_players, pl.size() * sizeof(PersistLayer)));
     HIPCHK(ctx, hipMemcpy(ctx->d_players, pl.data(), pl.size() * sizeof(PersistLayer), hipMemcpyHostToDevice));
-    // the persistent decoder's exp fallback list (64 entries + a count word)
-    HIPCHK(ctx, hipMalloc(&ctx->d_expfb, 65 * 4));
+    // the persistent decoder's exp fallback list (64 entries + a count word),
+    // rewritten as a 64-slot hash table {j << 16 | value} addressed by
+    // (j * K) >> 26 with K (word 65) chosen so the listed inputs get distinct
+    // slots (exp_f16_hash, wmi_persist.hip)
+    HIPCHK(ctx, hipMalloc(&ctx->d_expfb, 66 * 4));
     HIPCHK(ctx, hipMemset(ctx->d_expfb, 0xff, 64 * 4));
-    HIPCHK(ctx, hipMemset(ctx->d_expfb + 64, 0, 4));
+    HIPCHK(ctx, hipMemset(ctx->d_expfb + 64, 0, 8));
     HIPCHK(ctx, launch_exp_fallbacks(nullptr, ctx->exp_tab, ctx->n_exp, ctx->d_expfb, ctx->d_expfb + 64));
-    uint32_t nfb = 0;
-    HIPCHK(ctx, hipMemcpy(&nfb, ctx->d_expfb + 64, 4, hipMemcpyDeviceToHost));
+    uint32_t fb[65];
+    HIPCHK(ctx, hipMemcpy(fb, ctx->d_expfb, 65 * 4, hipMemcpyDeviceToHost));
+    const uint32_t nfb = fb[64];
     ctx->n_expfb = (int)nfb;
     if (nfb > 64) ctx->use_persist = false;  // (not seen: ~19 inputs) the kernel chain then decodes
+    if (nfb <= 64) {
+        uint32_t tab[66], K = 0;
+        for (uint32_t t = 0; t < 100000 && !K; ++t) {
+            const uint32_t k = 0x9E3779B1u + 2u * t;  // odd multipliers
+            uint64_t used = 0;
+            bool ok = true;
+            for (uint32_t i = 0; i < nfb && ok; ++i) {
+                const uint32_t slot = ((fb[i] >> 16) * k) >> 26;
+                ok = !(used >> slot & 1u);
+                used |= 1ull << slot;
+            }
+            if (ok) K = k;
+        }
+        if (!K) return set_err(ctx, WMI_E_HIP, "no collision-free exp fallback hash");
+        for (int i = 0; i < 64; ++i) tab[i] = 0xffffffffu;
+        for (uint32_t i = 0; i < nfb; ++i) tab[((fb[i] >> 16) * K) >> 26] = fb[i];
+        tab[64] = nfb;
+        tab[65] = K;
+        HIPCHK(ctx, hipMemcpy(ctx->d_expfb, tab, 66 * 4, hipMemcpyHostToDevice));
+    }
     if (ctx->wf32) ctx->use_persist = false;  // f32 matrices: the kernel chain with the f32 GEMVs
     return WMI_OK;
 }
@@ -1559,7 +1583,8 @@ int ptrace_dump(wmi_context *ctx, int steps) {
         }
         // sub-phase stamps (slots 27..31, when a build sets them): time after
         // the latest poll-done stamp of the same layer
-        for (int k = 27; k < 32; ++k) {
+        for (int k = 11; k < 32; ++k) {
+            if (k == 15) k = 27;
             double s = 0;
             int c = 0;
             for (int st = 1; st < steps; ++st)

@@ -657,21 +657,18 @@ __device__ __forceinline__ bool exp_f16_fast_ok(float arg, f16 &hx, float &hv) {
     const float ulp = __uint_as_float(__float_as_uint(r) & 0x7f800000u) * 1.1920928955078125e-7f;
     return fabsf(r - mid) > 4.0f * ulp;
 }
-__device__ __forceinline__ float exp_f16_fast(float arg, const uint32_t *fb) {
-    f16 hx;
-    float hv;
-    if (exp_f16_fast_ok(arg, hx, hv)) return hv;
+// The same value branch-free: the fallback inputs sit in a 64-slot table
+// addressed by a multiplicative hash of the f16 magnitude j (slot
+// (j * K) >> 26, K chosen on the host so the listed inputs get distinct
+// slots; an empty slot holds 0xffffffff).  Every lane reads its slot (one
+// word per bank: no bank conflicts) and takes the table value when the
+// slot's key is j, else the f16 of the f32 exp — no divergent list scan.
+__device__ __forceinline__ float exp_f16_hash(float arg, const uint32_t *fbt, uint32_t K) {
+    const f16 hx = (f16)arg;
+    const float hv = h2f_bits(f2h_bits(expf((float)hx)));
     const uint32_t j = __builtin_bit_cast(uint16_t, hx) & 0x7fff;
-    uint32_t hit = 0xffffffffu;
-#pragma unroll
-    for (int i = 0; i < EXPFB; i += 4) {
-        const uint4 e = *(const uint4 *)(fb + i);
-        hit = (e.x >> 16) == j ? e.x : hit;
-        hit = (e.y >> 16) == j ? e.y : hit;
-        hit = (e.z >> 16) == j ? e.z : hit;
-        hit = (e.w >> 16) == j ? e.w : hit;
-    }
-    return hit != 0xffffffffu ? h2f_bits((uint16_t)hit) : hv;
+    const uint32_t e = fbt[(j * K) >> 26];
+    return (e >> 16) == j ? h2f_bits((uint16_t)e) : hv;
 }
 
 // Every phase re-derives its lane indices from an opaque copy of threadIdx.x
@@ -797,6 +794,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     }
     if (tid == 0) sh.abort_ = 0;
     if (tid < EXPFB) sh.expfb[tid] = a.exp_fb[tid];
+    const uint32_t fbk = a.exp_fb[EXPFB + 1];  // the fallback table's hash multiplier
     __syncthreads();
     auto check = [&](bool ok) -> bool {  // workgroup-uniform abort after a poll
         if (!ok) sh.abort_ = 1;
@@ -983,7 +981,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #pragma unroll 1
                         for (int k = 0; k < nk; ++k) {
                             const int j = lane + 64 * k;
-                            const float pj = exp_f16_fast(sP[j] - mx, sh.expfb);
+                            const float pj = exp_f16_hash(sP[j] - mx, sh.expfb, fbk);
                             if (j < M) {
                                 sum += (double)pj;
                                 sP[j] = pj;
@@ -1115,13 +1113,14 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     if (lane == 0) sh.redf[w] = mx;
                     __syncthreads();
                     mx = fmaxf(fmaxf(sh.redf[0], sh.redf[1]), fmaxf(sh.redf[2], sh.redf[3]));
+                PSTAMP(l * 32 + 14)
                     double sum = 0.0;
                     float p[2];
 #pragma unroll
                     for (int r = 0; r < 2; ++r) {
                         p[r] = 0.0f;
                         if (tid + 256 * r < M) {
-                            p[r] = exp_f16_fast(sc[r] - mx, sh.expfb);
+                            p[r] = exp_f16_hash(sc[r] - mx, sh.expfb, fbk);
                             sum += (double)p[r];
                         }
                     }
@@ -1430,16 +1429,16 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
                         const int j = tid + 256 * u;
-                        const float pj = exp_f16_fast(sv[u] - m, sh.expfb);
-                        if (j < T) {
-                            sum += (double)pj;
-                            Sx[j] = pj;
-                        }
+                        const float pj = exp_f16_hash(sv[u] - m, sh.expfb, fbk);
+                        if (j < T) sum += (double)pj;
+                        if (j >= j0 && j < j1) Sx[j] = pj;  // (P.V reads only this task's keys)
                     }
                     sum = wave_sum(sum);
                     if (lane == 0) sh.redd[w] = sum;
                     __syncthreads();
+                PSTAMP(l * 32 + 11)
                     const float inv = (float)(1.0 / (((sh.redd[0] + sh.redd[1]) + sh.redd[2]) + sh.redd[3]));
+                PSTAMP(l * 32 + 12)
                     // one partial per 128-key sub-chunk: the grouping of a
                     // one-row run whatever the task's chunk (CL), so results
                     // do not depend on how many rows share the launch
@@ -1477,6 +1476,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                             if (j0 + 128 * p < j1)
 #pragma unroll
                                 for (int e = 0; e < 8; ++e) sh.ored[w][p * 64 + lane * 8 + e] = o[p][e];
+                PSTAMP(l * 32 + 13)
                     __syncthreads();
                     const int nsp = (j1 - j0 + 127) >> 7;  // sub-chunks of this task
                     if (tid < 64 * nsp)
@@ -1510,7 +1510,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                             const int key = j0 + tid + 256 * u;
                             if (256 * u < CL) {
                                 const float sv = st[b * CL + (key < j1 ? key : j1 - 1) - j0];
-                                const float pj = exp_f16_fast(sv - m, sh.expfb);
+                                const float pj = exp_f16_hash(sv - m, sh.expfb, fbk);
                                 if (key < j1) {
                                     sum += (double)pj;
                                     st[b * CL + key - j0] = pj;
@@ -1556,7 +1556,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         const int key = j0 + tid + 256 * u;
                         if (256 * u < CL) {
                             const float sv = st[(key < j1 ? key : j1 - 1) - j0];
-                            const float pj = exp_f16_fast(sv - m, sh.expfb);
+                            const float pj = exp_f16_hash(sv - m, sh.expfb, fbk);
                             if (key < j1) {
                                 sum += (double)pj;
                                 st[key - j0] = pj;
@@ -2050,7 +2050,7 @@ __global__ void k_persist_selftest(const uint16_t *tab, int n_exp, const uint32_
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j > 0x7c00) return;
     const float x = h2f_bits((uint16_t)(0x8000u | (uint32_t)j));
-    const uint16_t got = f2h_bits(exp_f16_fast(x, fb));
+    const uint16_t got = f2h_bits(exp_f16_hash(x, fb, fb[EXPFB + 1]));
     const uint16_t want = j < n_exp ? tab[j] : (uint16_t)0;
     if (got != want) atomicAdd(mismatch, 1u);
 }
