@@ -15,6 +15,7 @@ typedef f16 half8 __attribute__((ext_vector_type(8)));
 typedef f16 half4 __attribute__((ext_vector_type(4)));
 typedef f16 half2v __attribute__((ext_vector_type(2)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint16_t f2h_bits(float x) { return __builtin_bit_cast(uint16_t, (f16)x); }
 __device__ __forceinline__ float h2f_bits(uint16_t b) { return (float)__builtin_bit_cast(f16, b); }

@@ -53,7 +53,9 @@ constexpr uint32_t PSPIN = 1u << 19;    // polls before a seam is declared dead
 constexpr int NPH = 11;                 // phases per decoder layer
 constexpr int PMAXB = 8;                // decoder rows
 constexpr int RNMAX = 16;               // rows of an n-row GEMV per workgroup
-constexpr int SCR_BYTES = 24 * 1024;    // attention / argmax scratch in LDS
+// attention / argmax scratch in LDS: one-row instances use at most ~14.3 KB
+// (LDS K/V self-attention), so they keep 8 KB more vocabulary rows resident
+__host__ __device__ constexpr int scr_bytes(int BT) { return BT == 1 ? 16 * 1024 : 24 * 1024; }
 constexpr int NKP = 4;                  // 128-key passes per cross-attention chunk (cl <= 512)
 constexpr int EXPFB = 64;               // exp fallback list entries (exp_f16_fast)
 constexpr int XS_OFF = 1024;            // cross-attention task scores / p in the LDS scratch
@@ -702,6 +704,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     constexpr int KC = NS / 128;        // 128-element chunks of a K = n row
     constexpr int H = NS / 64;
     constexpr int NPL = KC <= 4 ? 2 : 1;  // logits passes per register set
+    // logits on MFMA (n <= 512): v_mfma_f32_16x16x32_f16 with the rows'
+    // hidden states as A (rows >= B zero) and 16 vocabulary rows as B
+#ifdef WMI_NO_LMF
+    constexpr bool LMF = false;
+#else
+    constexpr bool LMF = KC <= 4;
+#endif
 #ifndef WMI_XQF_KC
 #define WMI_XQF_KC 6
 #endif
@@ -731,8 +740,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     constexpr int PUH = BT == 1 ? (NS <= 512 ? 4 : NS <= 1024 ? 8 : 16) : 16;  // B x 2n f16 pairs
     float *xf = (float *)smem;                                          // [B][NS] f32
     f16 *xs = (f16 *)(smem + (size_t)B * NS * 4);                       // [B][4 NS] f16
-    unsigned char *scr = smem + (size_t)B * NS * 4 + (size_t)B * NS * 8;  // SCR_BYTES
-    f16 *vres = (f16 *)(scr + SCR_BYTES);                                  // [nres][NS] resident vocabulary rows
+    unsigned char *scr = smem + (size_t)B * NS * 4 + (size_t)B * NS * 8;  // scr_bytes(BT)
+    f16 *vres = (f16 *)(scr + scr_bytes(BT));                              // [nres][NS] resident vocabulary rows
     // exchange offsets as plain scalars (a struct captured by the lambdas
     // below would be kept in scratch memory)
     int oX1, oX2, oX3, oQ, oK, oV, oO, oXQ, oOC, oH, oS, oM, oP, oA;
@@ -790,7 +799,12 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     } else {
         const uint4 *src = (const uint4 *)((const f16 *)a.te + (int64_t)rv0 * NS);
         uint4 *dst = (uint4 *)vres;
-        for (int i = tid; i < (rs0 - rv0) * NS / 8; i += PT) dst[i] = src[i];
+        // (MFMA logits: 16-byte chunk c of resident row j at c ^ (j & 15), so
+        // the 16 rows of a B fragment read hit distinct banks)
+        for (int i = tid; i < (rs0 - rv0) * NS / 8; i += PT) {
+            const int j = i / (NS / 8), c = i - j * (NS / 8);
+            dst[LMF ? j * (NS / 8) + (c ^ (j & 15)) : i] = src[i];
+        }
     }
     if (tid == 0) sh.abort_ = 0;
     if (tid < EXPFB) sh.expfb[tid] = a.exp_fb[tid];
@@ -1850,7 +1864,118 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
         // ---- logits: LN_final + vocabulary rows + per-WG argmax -------------
         // rows [rv0, rs0) are resident in LDS (loaded once per launch), the
         // rest [rs0, rv1) stream through two register sets issued before the poll
-        {
+        if constexpr (LMF) {
+            // MFMA logits: wave w takes the 16-row tiles w, w + 4, ... of the
+            // resident rows (B fragments from the swizzled LDS copy), then of
+            // the streamed rows (B fragments loaded straight into registers,
+            // the next tile's loads in flight during this tile's MFMAs).
+            // Lane l: A = hidden row l & 15 (zero for rows >= B), B = vocab
+            // row n0 + (l & 15), k = 32 kk + 8 (l >> 4) + 0..7; result D: vocab
+            // row n0 + (l & 15), hidden rows 4 (l >> 4) + r.  Each logit is one
+            // MFMA chain over k in order: independent of the other rows.
+            PHASE_IDS
+            constexpr int NK = NS / 32;
+            LnP<NS> lp;
+            Ln1P<NS> l1;
+            if constexpr (BT == 1) ln1_params<NS>(a.dln_w, a.dln_b, l1, tid);
+            else ln_params<NS>(a.dln_w, a.dln_b, lp, lane);
+            PREFETCH_ISSUED
+            __syncthreads();
+            if constexpr (BT == 1) {
+                if (!poll_ln1<NS>(xg + oX1, ptag(pos, L, L - 1, 10), l1, xf, xs, abortw, a.err, sh.redd, sh.redd2, &sh.abort_))
+                    return;
+            } else {
+                const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, L - 1, 10), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
+                if (check(ok)) return;
+            }
+                PSTAMP(L * 32 + 16)
+            const int lr = lane & 15, lh = lane >> 4;
+            const int rres = rv0 + ((rs0 - rv0) & ~15);  // resident tiles end (whole tiles)
+            const int nst = (rv1 - rres + 15) >> 4;        // streamed tiles
+            const f16 *te = (const f16 *)a.te;
+            const half8 z8 = {};
+            auto sload = [&](half8 (&f)[NK], int t) {  // streamed tile t's B fragments
+                int row = rres + 16 * t + lr;
+                row = row < rv1 ? row : rv1 - 1;
+                const f16 *wr = te + (int64_t)row * NS + 8 * lh;
+#pragma unroll
+                for (int kk = 0; kk < NK; ++kk) f[kk] = t < nst ? sld((const half8 *)(wr + 32 * kk)) : z8;
+            };
+            half8 bA[NK], bB[NK];
+            sload(bA, w);  // (requested after the poll: the resident tiles cover their latency)
+            if constexpr (BT > 1) sload(bB, w + 4);  // (one row: behind the resident tiles, measured faster)
+            PREFETCH_ISSUED
+            if constexpr (BT > 1) ln_rows<NS>(xf, lp, xs, B, w, lane);
+            __syncthreads();
+            PSTAMP(L * 32 + 1)
+            half8 af[NK];
+#pragma unroll
+            for (int kk = 0; kk < NK; ++kk) {
+                const half8 v = *(const half8 *)(xs + (lr < B ? lr : 0) * NS + 32 * kk + 8 * lh);
+                af[kk] = lr < B ? v : z8;
+            }
+            unsigned long long best[4] = {0ull, 0ull, 0ull, 0ull};
+            auto epi = [&](const floatx4 &d, int n0, int nend) {
+                const int n = n0 + lr;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = 4 * lh + r;
+                    const bool valid = m < B && n < nend;
+                    if (a.logits_out && valid) a.logits_out[(int64_t)m * a.V + n] = d[r];
+                    const unsigned long long k =
+                        ((unsigned long long)ord_f32(d[r]) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)n);
+                    if (valid && n != a.suppress_id) best[r] = k > best[r] ? k : best[r];
+                }
+            };
+            for (int t = w; 16 * t < rres - rv0; t += 4) {  // resident tiles
+                const int j = 16 * t + lr;                   // row within the resident copy
+                const f16 *wr = vres + j * NS;
+                floatx4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kk = 0; kk < NK; ++kk) {
+                    const half8 bv = *(const half8 *)(wr + (((4 * kk + lh) ^ (j & 15)) * 8));
+                    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[kk], bv, d, 0, 0, 0);
+                }
+                epi(d, rv0 + 16 * t, rres);
+            }
+            PSTAMP(L * 32 + 2)
+            if constexpr (BT == 1) sload(bB, w + 4);
+            PREFETCH_ISSUED
+            for (int t = w; t < nst; t += 8) {  // streamed tiles, two register sets in flight
+                floatx4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kk = 0; kk < NK; ++kk) d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[kk], bA[kk], d, 0, 0, 0);
+                epi(d, rres + 16 * t, rv1);
+                if (t + 4 >= nst) break;
+                sload(bA, t + 8);
+                PREFETCH_ISSUED
+                d = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kk = 0; kk < NK; ++kk) d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[kk], bB[kk], d, 0, 0, 0);
+                epi(d, rres + 16 * (t + 4), rv1);
+                sload(bB, t + 12);
+                PREFETCH_ISSUED
+            }
+            PSTAMP(L * 32 + 3)
+            // the 16 lanes of a row group hold rows 4 (l >> 4) + r: reduce them
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                unsigned long long k = best[r];
+                k = kstep<8>(k);
+                k = kstep<4>(k);
+                k = kstep<2>(k);
+                k = kstep<1>(k);
+                if (lr == 0 && 4 * lh + r < PMAXB) sh.best[w][4 * lh + r] = k;
+            }
+            __syncthreads();
+            if (tid < B) {
+                unsigned long long k = sh.best[0][tid];
+                for (int i = 1; i < 4; ++i) k = sh.best[i][tid] > k ? sh.best[i][tid] : k;
+                const uint32_t tg = atag(pos, L);
+                gput(xg + oA + ((int64_t)tid * G + wg) * 2, tg, (uint32_t)(k >> 32));
+                gput(xg + oA + ((int64_t)tid * G + wg) * 2 + 1, tg, (uint32_t)k);
+            }
+        } else {
                 PHASE_IDS
             WSet<KC, NPL> S0, S1;
             constexpr int RS = 16 * NPL;  // rows per register set
@@ -1976,19 +2101,34 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     if (tid == 0) a.st->pos = pos;
 }
 
-template <int NS>
+template <int NS, int BT>
 size_t persist_lds(int B) {
-    return (size_t)B * NS * 4 + (size_t)B * NS * 8 + SCR_BYTES;
+    return (size_t)B * NS * 4 + (size_t)B * NS * 8 + scr_bytes(BT);
 }
 constexpr size_t LDS_CU = 160 * 1024;
 
 template <int NS, int BT, bool BEAM, bool Q5>
 hipError_t launch_nsb(hipStream_t s, const PersistArgs &a, int G) {
-    const size_t lds = persist_lds<NS>(a.B) + (size_t)a.nres * NS * 2;
+    // resident vocabulary rows as this instance's LDS holds them (the
+    // context's count is sized for the one-row instance at B = 1, whose
+    // scratch is smaller than a beam launch's at K = 1)
+    static const size_t stat = [] {
+        hipFuncAttributes fa;
+        return hipFuncGetAttributes(&fa, (const void *)k_dec_persist<NS, BT, BEAM, Q5>) == hipSuccess
+                   ? fa.sharedSizeBytes
+                   : LDS_CU;
+    }();
+    const size_t base = persist_lds<NS, BT>(a.B), avail = LDS_CU - stat - 1024;
+    if (base > avail) return hipErrorInvalidValue;
+    PersistArgs b = a;
+    const int maxr = (int)((avail - base) / (NS * 2));
+    if (b.nres > maxr) b.nres = maxr;
+    if (b.kvl && (int64_t)b.kvcap * 256 > (int64_t)b.nres * NS * 2) return hipErrorInvalidValue;
+    const size_t lds = base + (size_t)b.nres * NS * 2;
     hipError_t e = hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM, Q5>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_dec_persist<NS, BT, BEAM, Q5>), dim3(G), dim3(PT), lds, s, a);
+    hipLaunchKernelGGL((k_dec_persist<NS, BT, BEAM, Q5>), dim3(G), dim3(PT), lds, s, b);
     return hipGetLastError();
 }
 #ifndef WMI_PERSIST_Q5_TU
@@ -2006,7 +2146,7 @@ template <int NS, int BT, bool BEAM, bool Q5>
 int grid_nsb(int device, int B, int V, int *nres) {
     hipFuncAttributes fa;
     if (hipFuncGetAttributes(&fa, (const void *)k_dec_persist<NS, BT, BEAM, Q5>) != hipSuccess) return 0;
-    const size_t base = persist_lds<NS>(B), avail = LDS_CU - fa.sharedSizeBytes - 1024;
+    const size_t base = persist_lds<NS, BT>(B), avail = LDS_CU - fa.sharedSizeBytes - 1024;
     if (base > avail) return 0;
     // resident vocabulary rows: as many of a workgroup's rows as the LDS holds
     const int G0 = PX_GMAX, rpw = (V + G0 - 1) / G0;
