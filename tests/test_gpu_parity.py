@@ -205,6 +205,10 @@ def test_greedy_tokens_micro(micro_ctx, oracle_micro):
 
 
 def test_batch_equals_single(micro_ctx):
+    """A clip's encoder output is bitwise the same alone and in a batch; its
+    greedy ids too (the multi-row decoder instance sums its GEMV dots on MFMA,
+    the one-row instance on the VALU: each a fixed order, so the ids agree
+    unless a step's top-2 logits are within ~1e-6)."""
     clips = [synth.synth_pcm_f32(2.0, s) for s in (1, 2, 3)]
     micro_ctx.set_audio_ctx(64)
     micro_ctx.pcm_to_mel_batch(clips)
@@ -385,8 +389,9 @@ def test_beam_search_finishing(wmi, eot_twin_model):
 
 def test_base_batch_of_8_equals_single(wmi, model_cache):
     """C4's per-GPU shard: 8 x 30 s clips through the batched encoder (M =
-    12000 rows per GEMM) and the 8-row persistent decoder give bitwise the
-    single-clip results (which the full-size test pins to the oracle)."""
+    12000 rows per GEMM) and the 8-row persistent decoder give the single-clip
+    results (which the full-size test pins to the oracle): encoder output
+    bitwise, greedy ids equal (see test_batch_equals_single)."""
     ctx = wmi.WhisperContext.new(synth.model_path("base", model_cache), 0, max_clips=8)
     try:
         clips = [synth.synth_pcm_f32(30.0, 1234 + i) for i in range(8)]

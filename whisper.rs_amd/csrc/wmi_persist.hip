@@ -34,6 +34,8 @@
 // one partial per 128 keys, so a row's result never depends on the batch).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "wmi_device.h"
 #include "wmi_internal.h"
 
@@ -477,6 +479,92 @@ struct GSet<KCH, NP, 1, Q5> {
     }
 };
 
+// ---- MFMA GEMV (n <= 512): a phase's rows [rb, r1) (at most 16 NP) as
+// v_mfma_f32_16x16x32_f16 tiles with the decoder rows' inputs as A (rows >= B
+// zero) and 16 weight rows as B; wave w takes the 32-k steps
+// [w NKQ, (w + 1) NKQ), and the four waves' partials meet in LDS (kp) and
+// are added in wave order.  Each (weight row, decoder row) result is one fixed
+// chain of MFMAs and additions, independent of B.  The epilogue runs in the
+// quarter-wave layout of wset_dot (quarter slot = weight row rb + 16 p +
+// slot, lane l16 = decoder row), so the phases' callbacks (and their pairing
+// shuffles) are shared with the VALU GEMVs.
+template <int KCH, int NP, bool Q5 = false>
+struct MSet {
+    static constexpr int NKQ = KCH;  // (K / 32) / 4 MFMA steps per wave
+    WChunk<Q5> c[NP][NKQ];
+    float bias[NP];
+    __device__ __forceinline__ void load(const WMat &W, const float *b, int K, int rb, int r1, int slot, int) {
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 15, lh = lane >> 4;
+#pragma unroll
+        for (int t = 0; t < NP; ++t) {
+            const int row = rb + 16 * t + lr;
+            const bool ok = row < r1;
+            const int64_t e0 = (int64_t)(ok ? row : 0) * K + 32 * (w * NKQ) + 8 * lh;
+#pragma unroll
+            for (int i = 0; i < NKQ; ++i) wc_zero(c[t][i]);
+            if (ok) {
+#pragma unroll
+                for (int i = 0; i < NKQ; ++i) wc_load(c[t][i], W, e0 + 32 * i);
+            }
+            const int r2 = rb + 16 * t + slot;
+            bias[t] = 0.0f;
+            if (b && r2 < r1) bias[t] = *glb(b + r2);
+        }
+    }
+    __device__ __forceinline__ void pre(int) {
+        const int lh = (threadIdx.x & 63) >> 4;
+#pragma unroll
+        for (int t = 0; t < NP; ++t)
+#pragma unroll
+            for (int i = 0; i < NKQ; ++i) wc_pre(c[t][i], 8 * lh);
+    }
+    // kp: LDS [4][NP][16][8] floats
+    template <int BT, typename Epi>
+    __device__ __forceinline__ void dot(const f16 *xs, int K, int B, int rb, int r1, int slot, int l16, float *kp,
+                                        Epi &&epi) const {
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 15, lh = lane >> 4;
+        const half8 z8 = {};
+        half8 af[NKQ];
+#pragma unroll
+        for (int i = 0; i < NKQ; ++i) {
+            const half8 v = *(const half8 *)(xs + (lr < B ? lr : 0) * K + 32 * (w * NKQ + i) + 8 * lh);
+            af[i] = lr < B ? v : z8;
+        }
+#pragma unroll
+        for (int t = 0; t < NP; ++t) {
+            if (rb + 16 * t >= r1) break;  // workgroup-uniform
+            floatx4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < NKQ; ++i) d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], wc_h8(c[t][i], 0), d, 0, 0, 0);
+            if (lh < 2)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) kp[((w * NP + t) * 16 + lr) * 8 + 4 * lh + r] = d[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            if (rb + 16 * p >= r1) break;  // workgroup-uniform
+            const int row = rb + 16 * p + slot, bq = l16 < 8 ? l16 : 0;
+            const float v0 = kp[((0 * NP + p) * 16 + slot) * 8 + bq], v1 = kp[((1 * NP + p) * 16 + slot) * 8 + bq];
+            const float v2 = kp[((2 * NP + p) * 16 + slot) * 8 + bq], v3 = kp[((3 * NP + p) * 16 + slot) * 8 + bq];
+            const float v = ((v0 + v1) + v2) + v3;
+            epi(row, l16, l16 < 8 ? v : 0.0f, bias[p], row < r1 && l16 < B);
+        }
+    }
+};
+#ifdef WMI_NO_MGV
+constexpr bool kMGV = false;  // (build option: the VALU GEMVs at every n)
+#else
+constexpr bool kMGV = true;
+#endif
+// a phase's weight set: MFMA for several rows at n <= 512, else VALU.  One
+// row keeps the quarter-wave VALU GEMVs: on MFMA its step took 3.6 % longer
+// (base 18.56 vs 17.84 ms decode; 8 rows 28.8 vs 32.0 ms, A/B x3,
+// profiles/r03/gemv_mfma_ab.txt), so a clip decoded alone and in a batch sum
+// its GEMV dots in different (each fixed) orders
+template <int NS, int BT, int KCH, int NP, int KS, bool Q5>
+using PSet = typename std::conditional<kMGV && NS <= 512 && (BT > 1), MSet<KCH, NP, Q5>, GSet<KCH, NP, KS, Q5>>::type;
+
 // LayerNorm (ggml norm: double mean / variance, eps 1e-5; then * w + b) of
 // rows b < B of xf [B][NS] into xs [B][NS] f16 — wave w takes rows w, w + 4.
 // One pass: var = E[x^2] - mean^2 in double (the f32 inputs' squares are
@@ -767,6 +855,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     // LDS-resident self-attention K / V (PersistArgs::kvl): workgroups
     // [0, L H) own one (layer, head) each
     const bool kvl = BT == 1 && a.kvl;
+    // the GEMV phases' partial sums: LDS scratch for the MFMA GEMVs, else the split-K buffer
+    float *kpbuf = NS <= 512 && BT > 1 && kMGV ? (float *)scr : sh.kpart;
     const int nkw = kvl ? L * H : 0;
     const bool kvw = wg < nkw;
     f16 *Kl = vres, *Vl = vres + (size_t)a.kvcap * 64;  // [kvcap][64] each (K chunks swizzled)
@@ -850,7 +940,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 0);
-                GSet<KC, 2, KS_A, Q5> S;
+                PSet<NS, BT, KC, 2, KS_A, Q5> S;
                 const bool act = ra0 < ra1;
                 S.load(lmat<Q5>(P.wqkv, P.wqkv5, 3 * NS * NS), P.bqkv, NS, ra0, ra1, slot, l16);
                 LnP<NS> lp;
@@ -911,7 +1001,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 }
                 PSTAMP(l * 32 + 27)
                 if (act)
-                    S.template dot<BT>(xs, NS, B, ra0, ra1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
+                    S.template dot<BT>(xs, NS, B, ra0, ra1, slot, l16, kpbuf, [&](int row, int b, float v, float eb, bool valid) {
                         const float vn = from_next_row(v), ebn = from_next_row(eb);
                         if (!valid || (q & 1)) return;
                         const int which = row / NS, c = row - which * NS;
@@ -1193,7 +1283,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 2);
-                GSet<KC, 1, KS_N, Q5> S;
+                PSet<NS, BT, KC, 1, KS_N, Q5> S;
                 const bool act = rn0 < rn1;
                 S.load(lmat<Q5>(P.wo, P.wo5, NS * NS), P.bo, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
@@ -1203,7 +1293,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 if (check(ok)) return;
                 PSTAMP(l * 32 + 18)
                 if (act)
-                    S.template dot<BT>(xs, NS, B, rn0, rn1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
+                    S.template dot<BT>(xs, NS, B, rn0, rn1, slot, l16, kpbuf, [&](int row, int b, float v, float eb, bool valid) {
                         if (!valid) return;
                         const float x = (v + eb) + sh.xres[b][row - rn0];
                         sh.xres[b][row - rn0] = x;
@@ -1237,7 +1327,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PSTAMP(l * 32 + 19)
                 __syncthreads();
                 if (act)
-                    S.template dot<BT>(xs, NS, B, rn0, rn1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
+                    S.template dot<BT>(xs, NS, B, rn0, rn1, slot, l16, kpbuf, [&](int row, int b, float v, float eb, bool valid) {
                         const float vn = from_next_row(v), ebn = from_next_row(eb);
                         if (!valid || (q & 1)) return;
                         gput(xg + oXQ + b * (NS / 2) + row / 2, tag, pack2((v + eb) * qs, (vn + ebn) * qs));
@@ -1781,7 +1871,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 8);
-                GSet<KC, 1, KS_N, Q5> S;
+                PSet<NS, BT, KC, 1, KS_N, Q5> S;
                 const bool act = rn0 < rn1;
                 S.load(lmat<Q5>(P.wco, P.wco5, NS * NS), P.bco, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
@@ -1791,7 +1881,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 if (check(ok)) return;
             PSTAMP(l * 32 + 24)
                 if (act)
-                    S.template dot<BT>(xs, NS, B, rn0, rn1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
+                    S.template dot<BT>(xs, NS, B, rn0, rn1, slot, l16, kpbuf, [&](int row, int b, float v, float eb, bool valid) {
                         if (!valid) return;
                         const float x = (v + eb) + sh.xres[b][row - rn0];
                         sh.xres[b][row - rn0] = x;
@@ -1804,7 +1894,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 9);
-                GSet<KC, 2, KS_H, Q5> S;
+                PSet<NS, BT, KC, 2, KS_H, Q5> S;
                 const bool act = rh0 < rh1;
                 S.load(lmat<Q5>(P.w0, P.w05, 4 * NS * NS), P.b0, NS, rh0, rh1, slot, l16);
                 LnP<NS> lp;
@@ -1827,7 +1917,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 __syncthreads();
                 PSTAMP(l * 32 + 28)
                 if (act)
-                    S.template dot<BT>(xs, NS, B, rh0, rh1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
+                    S.template dot<BT>(xs, NS, B, rh0, rh1, slot, l16, kpbuf, [&](int row, int b, float v, float eb, bool valid) {
                         const float vn = from_next_row(v), ebn = from_next_row(eb);
                         if (!valid || (q & 1)) return;
                         const uint16_t h0 = f2h_bits(v + eb), h1 = f2h_bits(vn + ebn);
@@ -1841,7 +1931,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 10);
-                GSet<4 * KC, 1, KS_I, Q5> S;
+                PSet<NS, BT, 4 * KC, 1, KS_I, Q5> S;
                 const bool act = rn0 < rn1;
                 S.load(lmat<Q5>(P.w1, P.w15, 4 * NS * NS), P.b1, 4 * NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
@@ -1851,7 +1941,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 if (check(ok)) return;
                 PSTAMP(l * 32 + 26)
                 if (act)
-                    S.template dot<BT>(xs, 4 * NS, B, rn0, rn1, slot, l16, sh.kpart, [&](int row, int b, float v, float eb, bool valid) {
+                    S.template dot<BT>(xs, 4 * NS, B, rn0, rn1, slot, l16, kpbuf, [&](int row, int b, float v, float eb, bool valid) {
                         if (!valid) return;
                         const float x = (v + eb) + sh.xres[b][row - rn0];
                         sh.xres[b][row - rn0] = x;
