@@ -219,7 +219,7 @@ def test_batch_equals_single(micro_ctx):
         micro_ctx.pcm_to_mel_batch([c])
         micro_ctx.encode(1, 0)
         np.testing.assert_array_equal(micro_ctx.encoder_out(0), enc_b[i])
-        np.testing.assert_array_equal(micro_ctx.decode_greedy(12, suppress_eot=True)[0], tok_b[i])
+        _ids_agree_to_near_tie(micro_ctx, micro_ctx.decode_greedy(12, suppress_eot=True)[0], tok_b[i])
 
 
 def test_staged_pipeline_matches_api(micro_ctx):
@@ -403,7 +403,7 @@ def test_base_batch_of_8_equals_single(wmi, model_cache):
             ctx.pcm_to_mel_batch([clips[i]])
             ctx.encode(1, 0)
             np.testing.assert_array_equal(ctx.encoder_out(0), enc_b[i])
-            np.testing.assert_array_equal(ctx.decode_greedy(12, suppress_eot=True)[0], tok_b[i])
+            _ids_agree_to_near_tie(ctx, ctx.decode_greedy(12, suppress_eot=True)[0], tok_b[i])
     finally:
         ctx.close()
 
@@ -597,6 +597,21 @@ def test_persistent_matches_chain(wmi, model_cache, model, n_clips, n_ctx):
     finally:
         for ctx in ctxs:
             ctx.close()
+
+
+def _ids_agree_to_near_tie(ctx, single, batched, gap=2e-3):
+    """Greedy ids of clip 0 decoded alone vs in a batch: identical up to the
+    first difference, which may only fall on a step whose top-2 margin (in
+    the one-row decoder's teacher-forced logits of the single run) is < gap."""
+    diff = np.nonzero(np.asarray(single) != np.asarray(batched))[0]
+    if not diff.size:
+        return
+    d = int(diff[0])
+    feed = np.concatenate([_prompt(ctx), np.asarray(single[:d], np.int32)]).astype(np.int32)
+    lg = ctx.decode_logits(feed, 0)[-1].copy()
+    lg[ctx.special["eot"]] = -np.inf  # (the greedy runs suppress EOT)
+    top2 = np.sort(lg)[-2:]
+    assert top2[1] - top2[0] < gap, (d, float(top2[1] - top2[0]))
 
 
 def _prompt(ctx):
