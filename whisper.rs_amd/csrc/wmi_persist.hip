@@ -784,23 +784,6 @@ __device__ __forceinline__ float exp_f16_hash(float arg, const uint32_t *fbt, ui
 // whole load latency lands behind the seam.  Nothing waits here.
 #define PREFETCH_ISSUED asm volatile("" : : : "memory");
 
-// L2 warm-up of a later phase's weights (n > 768, f16: the layers stream from
-// HBM, 46 MB a layer at large-v3, and a phase's 13-51 KB per workgroup in
-// flight in front of its poll delayed the poll itself): one dword load per
-// 128-byte line of the rows [base, base + bytes), PFN per thread, issued
-// phases ahead; the values are only consumed by pf_sink (a later point, so
-// the loads never make anything wait before they have long completed)
-constexpr int PFN = 2;
-__device__ __forceinline__ void pf_touch(uint32_t (&pf)[PFN], const void *base, int64_t bytes) {
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < PFN; ++i) {
-        const int64_t off = (int64_t)(tid + PT * i) * 128;
-        pf[i] = off < bytes ? *glb((const uint32_t *)((const unsigned char *)base + off)) : 0u;
-    }
-}
-__device__ __forceinline__ void pf_sink(const uint32_t (&pf)[PFN]) { asm volatile("" : : "v"(pf[0]), "v"(pf[1])); }
-
 // BT: rows at compile time (1) or at most (8, runtime B); BEAM: beam-search
 // launches (self-attention history through kv_src; its index registers stay
 // out of the greedy instances)
@@ -832,12 +815,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     // rows a workgroup owns at the full grid
     constexpr int KS_N = split_of(KC, rows_full(NS)), KS_I = split_of(4 * KC, rows_full(NS));
     constexpr int KS_A = split_of(KC, rows_full(3 * NS)), KS_H = split_of(KC, rows_full(4 * NS));
-#ifdef WMI_NO_PF
-    constexpr bool PF = false;
-#else
-    constexpr bool PF = NS > 768 && !Q5;  // L2 warm-up of later phases' weights (pf_touch)
-#endif
-    uint32_t pfA[PFN] = {0u, 0u}, pfD[PFN] = {0u, 0u}, pfH[PFN] = {0u, 0u}, pfI[PFN] = {0u, 0u};
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ PShared sh;
     const int B = BT == 1 ? 1 : a.B, G = gridDim.x, wg = blockIdx.x;
@@ -1048,10 +1025,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }
 
             PSTAMP(l * 32 + 0)
-            if constexpr (PF) {
-                pf_sink(pfA);
-                pf_touch(pfD, P.wcq + (int64_t)rn0 * NS, (int64_t)(rn1 - rn0) * NS * 2);
-            }
             // ---- B: self-attention per (row, head) ---------------------
             {
                 PHASE_IDS
@@ -1362,10 +1335,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }
 
             PSTAMP(l * 32 + 3)
-            if constexpr (PF) {
-                pf_sink(pfD);
-                pf_touch(pfH, P.w0 + (int64_t)rh0 * NS, (int64_t)(rh1 - rh0) * NS * 2);
-            }
             // beam search (rows = hypotheses of one clip, cross q from D): one
             // task per (head, key chunk) covers every row, so each K / V chunk
             // is read once a step (the per-row tasks read it once per row); a
@@ -1511,7 +1480,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }
 
             PSTAMP(l * 32 + 4)
-            if constexpr (PF) pf_touch(pfI, P.w1 + (int64_t)rn0 * 4 * NS, (int64_t)(rn1 - rn0) * 4 * NS * 2);
             if constexpr (!FSPLIT) {
             PSTAMP(l * 32 + 5)
             // ---- F: exact softmax + P16.V partial per chunk ----------------
@@ -1922,10 +1890,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }
 
             PSTAMP(l * 32 + 8)
-            if constexpr (PF) {  // the next layer's (or the next step's first layer's) Wqkv rows
-                ConstLayer &Pn = ((ConstLayer *)a.layers)[l + 1 < L ? l + 1 : 0];
-                pf_touch(pfA, Pn.wqkv + (int64_t)ra0 * NS, (int64_t)(ra1 - ra0) * NS * 2);
-            }
             // ---- H: LN2(x'') + W0 rows + GELU -> hidden ---------------------
             {
                 PHASE_IDS
@@ -1963,7 +1927,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }
 
             PSTAMP(l * 32 + 9)
-            if constexpr (PF) pf_sink(pfH);
             // ---- I: W1 rows + residual -> next layer's x --------------------
             {
                 PHASE_IDS
@@ -1986,7 +1949,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     });
             }
             PSTAMP(l * 32 + 10)
-            if constexpr (PF) pf_sink(pfI);
         }
 
         // ---- logits: LN_final + vocabulary rows + per-WG argmax -------------
