@@ -562,8 +562,16 @@ constexpr bool kMGV = true;
 // (base 18.56 vs 17.84 ms decode; 8 rows 28.8 vs 32.0 ms, A/B x3,
 // profiles/r03/gemv_mfma_ab.txt), so a clip decoded alone and in a batch sum
 // its GEMV dots in different (each fixed) orders
+// (K = n phases at every n; the K = 4n phase I only up to n = 512, where its
+// 4n / 128 chunks per lane fit the registers)
+#ifdef WMI_MGV_512  // (build option: MFMA GEMVs only up to n = 512)
+constexpr int kMGVN = 512;
+#else
+constexpr int kMGVN = 1280;
+#endif
 template <int NS, int BT, int KCH, int NP, int KS, bool Q5>
-using PSet = typename std::conditional<kMGV && NS <= 512 && (BT > 1), MSet<KCH, NP, Q5>, GSet<KCH, NP, KS, Q5>>::type;
+using PSet = typename std::conditional<kMGV && (BT > 1) && NS <= kMGVN && (NS <= 512 || KCH <= NS / 128), MSet<KCH, NP, Q5>,
+                                       GSet<KCH, NP, KS, Q5>>::type;
 
 // LayerNorm (ggml norm: double mean / variance, eps 1e-5; then * w + b) of
 // rows b < B of xf [B][NS] into xs [B][NS] f16 — wave w takes rows w, w + 4.
@@ -856,7 +864,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     // [0, L H) own one (layer, head) each
     const bool kvl = BT == 1 && a.kvl;
     // the GEMV phases' partial sums: LDS scratch for the MFMA GEMVs, else the split-K buffer
-    float *kpbuf = NS <= 512 && BT > 1 && kMGV ? (float *)scr : sh.kpart;
+    float *kpbuf = BT > 1 && kMGV ? (float *)scr : sh.kpart;  // (an MSet phase's partials; sh.kpart for GSet's split-K)
     const int nkw = kvl ? L * H : 0;
     const bool kvw = wg < nkw;
     f16 *Kl = vres, *Vl = vres + (size_t)a.kvcap * 64;  // [kvcap][64] each (K chunks swizzled)
