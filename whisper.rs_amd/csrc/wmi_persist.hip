@@ -596,6 +596,50 @@ __device__ __forceinline__ void ln_params(const float *lw, const float *lb, LnP<
 template <int NS>
 __device__ __forceinline__ void ln_rows(const float *xf, const LnP<NS> &P, f16 *xs, int B, int w, int lane) {
     constexpr int LV = LnP<NS>::V;
+    if (w + 4 < B) {
+        // rows w and w + 4 of this wave together (independent chains: twice
+        // the ILP of the row-by-row loop); each row's arithmetic as below
+        float4 xa[LV], xb[LV];
+#pragma unroll
+        for (int i = 0; i < LV; ++i) {
+            const int e = (lane + 64 * i) * 4, ec = e < NS ? e : 0;
+            xa[i] = *(const float4 *)(xf + w * NS + ec);
+            xb[i] = *(const float4 *)(xf + (w + 4) * NS + ec);
+        }
+        double sa1 = 0.0, sa2 = 0.0, sb1 = 0.0, sb2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < LV; ++i)
+            if ((lane + 64 * i) * 4 < NS) {
+                const double a0 = xa[i].x, a1 = xa[i].y, a2 = xa[i].z, a3 = xa[i].w;
+                const double b0 = xb[i].x, b1 = xb[i].y, b2 = xb[i].z, b3 = xb[i].w;
+                sa1 += (a0 + a1) + (a2 + a3);
+                sa2 += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+                sb1 += (b0 + b1) + (b2 + b3);
+                sb2 += (b0 * b0 + b1 * b1) + (b2 * b2 + b3 * b3);
+            }
+        sa1 = wave_sum(sa1);
+        sb1 = wave_sum(sb1);
+        sa2 = wave_sum(sa2);
+        sb2 = wave_sum(sb2);
+        const double ma = sa1 / NS, mb = sb1 / NS;
+        const float ka = (float)(1.0 / sqrt((sa2 / NS - ma * ma) + (double)1e-5f));
+        const float kb = (float)(1.0 / sqrt((sb2 / NS - mb * mb) + (double)1e-5f));
+#pragma unroll
+        for (int i = 0; i < LV; ++i) {
+            const int e = (lane + 64 * i) * 4;
+            if (e < NS) {
+                const float a4[4] = {xa[i].x, xa[i].y, xa[i].z, xa[i].w}, b4[4] = {xb[i].x, xb[i].y, xb[i].z, xb[i].w};
+                const float ww[4] = {P.w[i].x, P.w[i].y, P.w[i].z, P.w[i].w};
+                const float bb[4] = {P.b[i].x, P.b[i].y, P.b[i].z, P.b[i].w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    xs[w * NS + e + u] = (f16)(bb[u] + ww[u] * ((float)((double)a4[u] - ma) * ka));
+                    xs[(w + 4) * NS + e + u] = (f16)(bb[u] + ww[u] * ((float)((double)b4[u] - mb) * kb));
+                }
+            }
+        }
+        return;
+    }
     for (int b = w; b < B; b += 4) {
         float4 xv[LV];
 #pragma unroll
@@ -1428,21 +1472,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         // Wcq rows h*64 .. h*64+63, the D phase's arithmetic
                         WSet<KC, 4> S;
                         wset_load(S, wmat(P.wcq), P.bcq, NS, h * 64, h * 64 + 64, slot, l16);
-                        LnP<NS> lp;
-                        Ln1P<NS> l1;
-                        if constexpr (BT == 1) ln1_params<NS>(P.lnc_w, P.lnc_b, l1, tid);
-                        else ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
+                        Ln1P<NS> l1;  // (one row: the whole workgroup's LayerNorm from the poll registers)
+                        ln1_params<NS>(P.lnc_w, P.lnc_b, l1, tid);
                         PREFETCH_ISSUED
                         __syncthreads();
-                        if constexpr (BT == 1) {
-                            if (!poll_ln1<NS>(xg + oX2 + b * NS, ptag(pos, L, l, 2), l1, xf, xs, abortw, a.err, sh.redd,
-                                              sh.redd2, &sh.abort_))
-                                return;
-                        } else {
-                            const bool ok = gpoll<PUX>(NS, ptag(pos, L, l, 2), ptr_u64(xg + oX2 + b * NS), (uint32_t *)xf, abortw, a.err);
-                            if (check(ok)) return;
-                            ln_rows<NS>(xf, lp, xs, 1, w, lane);
-                        }
+                        if (!poll_ln1<NS>(xg + oX2 + b * NS, ptag(pos, L, l, 2), l1, xf, xs, abortw, a.err, sh.redd, sh.redd2,
+                                          &sh.abort_))
+                            return;
                 PSTAMP(l * 32 + 20)
                         __syncthreads();
                 PSTAMP(l * 32 + 29)
