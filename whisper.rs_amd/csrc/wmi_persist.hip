@@ -2296,7 +2296,12 @@ int grid_nsb(int device, int B, int V, int *nres) {
         return 0;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
+    // the grid must be co-resident: a device that cannot launch cooperatively
+    // gives no such guarantee even at one workgroup per CU
+    int coop = 0;
+    if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess || !coop) return 0;
     const int G = prop.multiProcessorCount < PX_GMAX ? prop.multiProcessorCount : PX_GMAX;
+    if (per_cu * prop.multiProcessorCount < G) return 0;
     // row-partition limits of the register sets (see wset_dot users); the
     // split-K phases need the full grid's rows per workgroup
     if ((3 * NS + G - 1) / G > 31 || (4 * NS + G - 1) / G > 31 || (NS + G - 1) / G > RNMAX - 1) return 0;
