@@ -1359,7 +1359,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             if constexpr (!XQF) {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 3);
-                GSet<KC, 1, KS_N> S;
+                PSet<NS, BT, KC, 1, KS_N, false> S;  // (MFMA with several rows)
                 const bool act = rn0 < rn1;
                 S.load(wmat(P.wcq), P.bcq, NS, rn0, rn1, slot, l16);
                 LnP<NS> lp;
