@@ -488,7 +488,7 @@ struct GSet<KCH, NP, 1, Q5> {
 // quarter-wave layout of wset_dot (quarter slot = weight row rb + 16 p +
 // slot, lane l16 = decoder row), so the phases' callbacks (and their pairing
 // shuffles) are shared with the VALU GEMVs.
-template <int KCH, int NP, bool Q5 = false>
+template <int KCH, int NP, bool Q5 = false, bool ALDS = false>  // ALDS: A fragments read from LDS per step
 struct MSet {
     static constexpr int NKQ = KCH;  // (K / 32) / 4 MFMA steps per wave
     WChunk<Q5> c[NP][NKQ];
@@ -524,18 +524,22 @@ struct MSet {
                                         Epi &&epi) const {
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, lr = lane & 15, lh = lane >> 4;
         const half8 z8 = {};
-        half8 af[NKQ];
-#pragma unroll
-        for (int i = 0; i < NKQ; ++i) {
+        half8 af[ALDS ? 1 : NKQ];
+        auto afrag = [&](int i) {
             const half8 v = *(const half8 *)(xs + (lr < B ? lr : 0) * K + 32 * (w * NKQ + i) + 8 * lh);
-            af[i] = lr < B ? v : z8;
+            return lr < B ? v : z8;
+        };
+        if constexpr (!ALDS) {
+#pragma unroll
+            for (int i = 0; i < NKQ; ++i) af[i] = afrag(i);
         }
 #pragma unroll
         for (int t = 0; t < NP; ++t) {
             if (rb + 16 * t >= r1) break;  // workgroup-uniform
             floatx4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int i = 0; i < NKQ; ++i) d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], wc_h8(c[t][i], 0), d, 0, 0, 0);
+            for (int i = 0; i < NKQ; ++i)
+                d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ALDS ? afrag(i) : af[i], wc_h8(c[t][i], 0), d, 0, 0, 0);
             if (lh < 2)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) kp[((w * NP + t) * 16 + lr) * 8 + 4 * lh + r] = d[r];
@@ -562,16 +566,18 @@ constexpr bool kMGV = true;
 // (base 18.56 vs 17.84 ms decode; 8 rows 28.8 vs 32.0 ms, A/B x3,
 // profiles/r03/gemv_mfma_ab.txt), so a clip decoded alone and in a batch sum
 // its GEMV dots in different (each fixed) orders
-// (K = n phases at every n; the K = 4n phase I only up to n = 512, where its
-// 4n / 128 chunks per lane fit the registers)
+// (the K = 4n phase I above n = 512 reads its A fragments from LDS at each
+// MFMA step instead of holding all 4n / 128 of them in registers)
 #ifdef WMI_MGV_512  // (build option: MFMA GEMVs only up to n = 512)
 constexpr int kMGVN = 512;
 #else
 constexpr int kMGVN = 1280;
 #endif
 template <int NS, int BT, int KCH, int NP, int KS, bool Q5>
-using PSet = typename std::conditional<kMGV && (BT > 1) && NS <= kMGVN && (NS <= 512 || KCH <= NS / 128), MSet<KCH, NP, Q5>,
-                                       GSet<KCH, NP, KS, Q5>>::type;
+using PSet = typename std::conditional<
+    kMGV && (BT > 1) && NS <= kMGVN,
+    typename std::conditional<(NS <= 512 || KCH <= NS / 128), MSet<KCH, NP, Q5>, MSet<KCH, NP, Q5, true>>::type,
+    GSet<KCH, NP, KS, Q5>>::type;
 
 // LayerNorm (ggml norm: double mean / variance, eps 1e-5; then * w + b) of
 // rows b < B of xf [B][NS] into xs [B][NS] f16 — wave w takes rows w, w + 4.
