@@ -857,6 +857,10 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 #else
     constexpr bool LMF = KC <= 4;
 #endif
+    // several rows at n > 512: the four waves split K (n / 4 each) over every
+    // 16-row tile, partials added in wave order through LDS (the A fragments
+    // and a tile's B fragments of all of K would not fit the registers)
+    constexpr bool LMF2 = !LMF && BT > 1 && kMGV;
 #ifndef WMI_XQF_KC
 #define WMI_XQF_KC 6
 #endif
@@ -951,7 +955,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
         // the 16 rows of a B fragment read hit distinct banks)
         for (int i = tid; i < (rs0 - rv0) * NS / 8; i += PT) {
             const int j = i / (NS / 8), c = i - j * (NS / 8);
-            dst[LMF ? j * (NS / 8) + (c ^ (j & 15)) : i] = src[i];
+            dst[LMF || LMF2 ? j * (NS / 8) + (c ^ (j & 15)) : i] = src[i];
         }
     }
     if (tid == 0) sh.abort_ = 0;
@@ -2107,6 +2111,102 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 k = kstep<1>(k);
                 if (lr == 0 && 4 * lh + r < PMAXB) sh.best[w][4 * lh + r] = k;
             }
+            __syncthreads();
+            if (tid < B) {
+                unsigned long long k = sh.best[0][tid];
+                for (int i = 1; i < 4; ++i) k = sh.best[i][tid] > k ? sh.best[i][tid] : k;
+                const uint32_t tg = atag(pos, L);
+                gput(xg + oA + ((int64_t)tid * G + wg) * 2, tg, (uint32_t)(k >> 32));
+                gput(xg + oA + ((int64_t)tid * G + wg) * 2 + 1, tg, (uint32_t)k);
+            }
+        } else if constexpr (LMF2) {
+            PHASE_IDS
+            constexpr int KQ = NS / 4, NKW = KQ / 32, TG = 8;  // k per wave, MFMA steps per wave, tiles per LDS group
+            LnP<NS> lp;
+            ln_params<NS>(a.dln_w, a.dln_b, lp, lane);
+            PREFETCH_ISSUED
+            __syncthreads();
+            {
+                const bool ok = gpoll<PUX>(B * NS, ptag(pos, L, L - 1, 10), ptr_u64(xg + oX1), (uint32_t *)xf, abortw, a.err);
+                if (check(ok)) return;
+            }
+                PSTAMP(L * 32 + 16)
+            const int lr = lane & 15, lh = lane >> 4, k0 = w * KQ;
+            const int rres = rv0 + ((rs0 - rv0) & ~15);
+            const int nres_t = (rres - rv0) >> 4, ntile = nres_t + ((rv1 - rres + 15) >> 4);
+            const f16 *te = (const f16 *)a.te;
+            const half8 z8 = {};
+            auto bload = [&](half8 (&f)[NKW], int t) {  // streamed tile t (t >= nres_t) B fragments of this wave's K
+                int row = rv0 + 16 * t + lr;
+                row = row < rv1 ? row : rv1 - 1;
+                const f16 *wr = te + (int64_t)row * NS + k0 + 8 * lh;
+#pragma unroll
+                for (int i = 0; i < NKW; ++i) f[i] = t < ntile ? sld((const half8 *)(wr + 32 * i)) : z8;
+            };
+            half8 bA[NKW], bB[NKW];
+            bload(bA, nres_t);
+            bload(bB, nres_t + 1);
+            PREFETCH_ISSUED
+            ln_rows<NS>(xf, lp, xs, B, w, lane);
+            __syncthreads();
+            PSTAMP(L * 32 + 1)
+            half8 af[NKW];
+#pragma unroll
+            for (int i = 0; i < NKW; ++i) {
+                const half8 v = *(const half8 *)(xs + (lr < B ? lr : 0) * NS + k0 + 32 * i + 8 * lh);
+                af[i] = lr < B ? v : z8;
+            }
+            float *kp = (float *)scr;  // [TG][4][16][8]
+            unsigned long long best = 0ull;  // this thread's decoder row m = tid & 7
+            for (int g0 = 0; g0 < ntile; g0 += TG) {
+                for (int t = g0; t < g0 + TG && t < ntile; ++t) {  // workgroup-uniform
+                    floatx4 d = {0.f, 0.f, 0.f, 0.f};
+                    if (t < nres_t) {
+                        const int j = 16 * t + lr;
+                        const f16 *wr = vres + j * NS;
+#pragma unroll
+                        for (int i = 0; i < NKW; ++i) {
+                            const half8 bv = *(const half8 *)(wr + ((((k0 >> 3) + 4 * i + lh) ^ (j & 15)) * 8));
+                            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bv, d, 0, 0, 0);
+                        }
+                    } else if (((t - nres_t) & 1) == 0) {
+#pragma unroll
+                        for (int i = 0; i < NKW; ++i) d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bA[i], d, 0, 0, 0);
+                        bload(bA, t + 2);
+                        PREFETCH_ISSUED
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < NKW; ++i) d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bB[i], d, 0, 0, 0);
+                        bload(bB, t + 2);
+                        PREFETCH_ISSUED
+                    }
+                    if (lh < 2)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) kp[(((t - g0) * 4 + w) * 16 + lr) * 8 + 4 * lh + r] = d[r];
+                }
+                __syncthreads();
+                for (int idx = tid; idx < TG * 128; idx += PT) {  // (tile, row, m) with m = tid & 7
+                    const int tg = idx >> 7, rr = (idx >> 3) & 15, m = idx & 7, t = g0 + tg;
+                    const int n = rv0 + 16 * t + rr;
+                    if (t >= ntile || m >= B || n >= rv1) continue;
+                    const float v = ((kp[((tg * 4 + 0) * 16 + rr) * 8 + m] + kp[((tg * 4 + 1) * 16 + rr) * 8 + m]) +
+                                     kp[((tg * 4 + 2) * 16 + rr) * 8 + m]) +
+                                    kp[((tg * 4 + 3) * 16 + rr) * 8 + m];
+                    if (a.logits_out) a.logits_out[(int64_t)m * a.V + n] = v;
+                    if (n == a.suppress_id) continue;
+                    const unsigned long long k =
+                        ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)n);
+                    best = k > best ? k : best;
+                }
+                __syncthreads();  // kp reused by the next group
+            }
+            PSTAMP(L * 32 + 2)
+            PSTAMP(L * 32 + 3)
+            // lanes with equal lane & 7 hold the same decoder row: reduce them
+            best = kstep<8>(best);
+            best = kstep<16>(best);
+            best = kstep<32>(best);
+            if (lane < PMAXB) sh.best[w][lane] = best;
             __syncthreads();
             if (tid < B) {
                 unsigned long long k = sh.best[0][tid];
