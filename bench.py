@@ -30,6 +30,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -93,19 +94,36 @@ def cpu_threads() -> int:
 
 
 def free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A MASTER_PORT whose rendezvous hub ports (dist.hub_ports) can be bound
+    too: checked by binding them, not assumed."""
+    for _ in range(64):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        if p + dist.hub_ports(0)[-1] > 65535:
+            continue
+        try:
+            t = socket.socket()
+            t.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            t.bind(("127.0.0.1", dist.hub_ports(p)[0]))
+            t.close()
+            return p
+        except OSError:
+            t.close()
+    raise OSError("no free rendezvous port")
 
 
-def launch_ranks(n: int, argv) -> int:
+def launch_ranks(n: int, argv, deadline_s: float) -> int:
     """Start one rank process of this script per GPU (RANK, LOCAL_RANK,
     WORLD_SIZE, MASTER_ADDR, MASTER_PORT set as torch.distributed.run would),
-    relay rank 0's stdout and return the first non-zero exit status.  Nothing
-    in this process touches a GPU: it only imports the synthetic-input module
-    (numpy) and generates the model file once, so the ranks do not race on it."""
+    relay rank 0's result line and return non-zero if any rank fails: the
+    first rank to exit non-zero (or by a signal) makes the launcher kill the
+    others, and so does the deadline (deadline_s seconds for the whole run:
+    a rank stuck in the rendezvous or in RCCL's init cannot hang the
+    launcher).  Nothing in this process touches a GPU: it only imports the
+    synthetic-input module (numpy) and generates the model file once, so the
+    ranks do not race on it."""
     if "--dry-run" not in argv:
         model = "base"
         for i, a in enumerate(argv):
@@ -115,7 +133,7 @@ def launch_ranks(n: int, argv) -> int:
                 model = a.split("=", 1)[1]
         synth.model_path(model)
     port = free_port()
-    log(f"launching {n} rank processes (rendezvous 127.0.0.1:{port})")
+    log(f"launching {n} rank processes (rendezvous 127.0.0.1:{port}, deadline {deadline_s:.0f} s)")
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
@@ -123,6 +141,10 @@ def launch_ranks(n: int, argv) -> int:
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = []  # rank 0's stdout, drained while the ranks run (a full pipe would stall it)
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    t_end = time.monotonic() + deadline_s
     rc = 0
     while True:
         states = [p.poll() for p in procs]
@@ -130,17 +152,22 @@ def launch_ranks(n: int, argv) -> int:
         if bad:
             rc = bad[0][1]
             log(f"rank {bad[0][0]} exited with status {rc}; stopping the other ranks")
-            for p in procs:
-                if p.poll() is None:
-                    p.kill()
             break
         if all(s == 0 for s in states):
             break
+        if time.monotonic() > t_end:
+            log(f"deadline of {deadline_s:.0f} s passed with rank(s) "
+                f"{[r for r, s in enumerate(states) if s is None]} still running; stopping every rank")
+            rc = 124
+            break
         time.sleep(0.1)
-    out = procs[0].stdout.read().decode()
+    for p in procs:
+        if p.poll() is None:
+            p.kill()
     for p in procs:
         p.wait()
-    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    reader.join(10)
+    lines = [ln for ln in (out[0] if out else b"").decode().splitlines() if ln.startswith("{")]
     if rc == 0 and lines:
         print(lines[-1], flush=True)
     elif rc == 0:
@@ -220,21 +247,20 @@ def encoder_flops(hp: dict) -> float:
     return conv + L * layer + 2.0 * T * n * 2 * hp["n_text_layer"] * hp["n_text_state"]
 
 
-def decode_bytes(hp: dict, rows: int, steps: int, beam: bool) -> float:
-    """Algorithmic bytes of one decode (wmi_bench_kernel 14's count): every
-    step reads each decoder weight once (shared by the rows), the vocabulary
-    matrix once, the cross K/V once per clip (beam rows share their clip's),
-    and each row's self K/V rows [0, pos]; greedy rows run in blocks of 8."""
-    nt, L, T, V = hp["n_text_state"], hp["n_text_layer"], hp["n_audio_ctx"], hp["n_vocab"]
-    w_step = L * (28.0 * nt * nt + 68.0 * nt) + V * nt * 2 + 2 * nt * 4
-    total = 0.0
-    blocks = [rows] if beam else [min(8, rows - b0) for b0 in range(0, rows, 8)]
-    for r in blocks:
-        for pos in range(steps):
-            total += w_step + r * nt * 6
-            total += (1 if beam else r) * L * T * nt * 4
-            total += r * L * (pos * nt * 4 + nt * 4)
-    return total
+def persist_q5(model: str) -> bool:
+    """q5_1 files decode with the q5_1-block GEMVs unless WMI_PERSIST_Q5=0;
+    beam launches read the f16 copies (wmi_persist.hip launch_ns)."""
+    return model.endswith("q5_1") and os.environ.get("WMI_PERSIST_Q5", "1") != "0"
+
+
+def decode_bytes(wmi, hp: dict, rows: int, steps: int, beam: bool, q5: bool) -> float:
+    """Algorithmic bytes of one decode — the library's count
+    (wmi_decode_alg_bytes, the one wmi_bench_kernel 14 reports): every step
+    reads each decoder weight once (shared by the rows; the q5_1 GEMV matrices
+    at their block size when the decode runs on them), the vocabulary matrix
+    once, the cross K/V once per clip (beam rows share their clip's), and each
+    row's self K/V rows [0, pos]; greedy rows run in blocks of 8."""
+    return wmi.decode_alg_bytes(hp, rows, steps, beam, q5 and not beam)[0]
 
 
 def measure_config(wmi, name, model, clips, beam, steps, warmup, n_decode, device, what):
@@ -256,13 +282,13 @@ def measure_config(wmi, name, model, clips, beam, steps, warmup, n_decode, devic
         ms = el / steps * 1e3
         enc_ms = tm["encode_ms"] + tm["cross_kv_ms"]
         dec_steps = tm["n_decode_steps"]
-        dbytes = decode_bytes(hp, clips if not beam else beam, dec_steps, bool(beam))
+        dbytes = decode_bytes(wmi, hp, clips if not beam else beam, dec_steps, bool(beam), persist_q5(model))
         dec = {"bound": "hbm", "alg_bytes": dbytes, "decode_ms": round(tm["decode_ms"], 3),
                "achieved": round(dbytes / (tm["decode_ms"] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
         if not beam:
-            try:  # the persistent decoder's own launch, timed live (HIP events)
+            try:  # the persistent decoder's own launch, timed live (HIP events); same byte count
                 kb = ctx.bench_kernel(14, 1)
-                dec.update(kernel=kb["name"], avg_us=round(kb["avg_us"], 1),
+                dec.update(kernel=kb["name"], avg_us=round(kb["avg_us"], 1), alg_bytes=kb["alg_bytes"],
                            achieved=round(kb["alg_bytes"] / (kb["avg_us"] * 1e-6) / 1e9, 1))
             except Exception as e:  # the chain decoder ran (no persistent instance)
                 log(f"{name}: kernel 14: {e}")
@@ -305,6 +331,14 @@ def whole_step_bytes(hp: dict, clips: int, dec_bytes: float) -> float:
 
 def run_rank(args, rank: int, world: int, local: int) -> None:
     group = dist.Group(rank, world)
+    # test knobs (tests/test_dist_cpu.py): this rank fails, or hangs, right
+    # after the rendezvous, so the launcher's kill / deadline paths run for real
+    if os.environ.get("WMI_TEST_FAIL_RANK") == str(rank):
+        log(f"rank {rank}: WMI_TEST_FAIL_RANK: exiting with status 3 after the rendezvous")
+        sys.exit(3)
+    if os.environ.get("WMI_TEST_HANG_RANK") == str(rank):
+        log(f"rank {rank}: WMI_TEST_HANG_RANK: hanging after the rendezvous")
+        time.sleep(3600)
     cpg = args.clips_per_gpu
     audio_s = 30.0 * cpg
     ctx = None
@@ -476,13 +510,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-min-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-max-seconds", type=float, default=30.0)
+    ap.add_argument("--launch-deadline", type=float, default=1500.0,
+                    help="--gpus N without torchrun: seconds before the launcher kills every rank and fails")
     ap.add_argument("--dry-run", action="store_true",
                     help="no device: exercise the rank launcher, rendezvous and max-over-ranks timing on the CPU")
     args = ap.parse_args()
     if args.clips_per_gpu is None:
         args.clips_per_gpu = 8 if args.gpus > 1 else 1
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_deadline))
     rank, world, local = dist.env_rank_world()
     if world != args.gpus:
         log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using the launcher's world size")

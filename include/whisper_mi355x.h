@@ -218,6 +218,16 @@ typedef struct wmi_kernel_bench {
 } wmi_kernel_bench;
 int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *out);
 
+/* Algorithmic bytes and FLOPs of one decode on a model of hparams hp (host
+ * only, no device): `steps` decoder steps of `rows` rows; beam != 0: the rows
+ * are hypotheses of ONE clip (its cross K/V read once a step), else clips
+ * decoded in blocks of 8 rows; q5 != 0: the five q5_1 GEMV matrices (Wqkv,
+ * Wo, Wco, W0, W1 = 13 n^2 weights) at 24 bytes a 32-weight block, Wcq and the
+ * vocabulary f16.  Every step reads each decoder weight once (shared by the
+ * block's rows), each row's cross K/V and self K/V rows [0, pos] and writes
+ * its new K/V row.  wmi_bench_kernel 14 and bench.py use this one count. */
+int wmi_decode_alg_bytes(const wmi_hparams *hp, int rows, int steps, int beam, int q5, double *bytes, double *flops);
+
 /* Device self-test: the decoder computes ggml's f16 exp table entries
  * instead of looking them up; *n_mismatch = entries (of 31745 non-positive
  * f16 inputs) where the computed value differs from the host-built table. */

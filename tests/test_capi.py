@@ -177,3 +177,33 @@ def test_hostile_headers_allocate_nothing(tmp_path, micro_model):
     open(wav, "wb").write(b"RIFF" + struct.pack("<I", len(body)) + body)
     with pytest.raises(wmi.UnexpectIO):
         wmi.read_wav(wav)
+
+
+def test_decode_alg_bytes_counts_q5_blocks():
+    """wmi_decode_alg_bytes (host only) is the one byte count of a decode:
+    wmi_bench_kernel 14 reports it and bench.py's roofline uses it.  For a
+    q5_1 decode the five GEMV matrices (13 n^2 weights) count at 24 bytes a
+    32-weight block and Wcq stays f16: per layer and step 28 n^2 -> 11.75 n^2
+    bytes; beam rows read their clip's cross K/V once."""
+    import bench
+    hp = dict(synth.MODEL_DIMS["small"], f16=1)
+    n, L, T = hp["n_text_state"], hp["n_text_layer"], hp["n_audio_ctx"]
+    steps = 131
+    f16, fl = wmi.decode_alg_bytes(hp, 1, steps)
+    q5, fl5 = wmi.decode_alg_bytes(hp, 1, steps, q5=True)
+    assert fl == fl5 > 0
+    assert f16 - q5 == pytest.approx(steps * L * (28.0 - 11.75) * n * n, rel=1e-12)
+    # the bench leg of C3 charges exactly the library's q5_1 count (WMI_PERSIST_Q5 unset)
+    old = os.environ.pop("WMI_PERSIST_Q5", None)
+    try:
+        assert bench.persist_q5("small-q5_1") and not bench.persist_q5("small")
+        assert bench.decode_bytes(wmi, hp, 1, steps, False, bench.persist_q5("small-q5_1")) == q5
+        assert bench.decode_bytes(wmi, hp, 5, steps, True, True) == wmi.decode_alg_bytes(hp, 5, steps, beam=True)[0]
+    finally:
+        if old is not None:
+            os.environ["WMI_PERSIST_Q5"] = old
+    b5, _ = wmi.decode_alg_bytes(hp, 5, steps, beam=True)
+    g5, _ = wmi.decode_alg_bytes(hp, 5, steps)
+    assert g5 - b5 == pytest.approx(steps * 4 * L * T * n * 4, rel=1e-12)  # 4 more clips' cross K/V
+    with pytest.raises(wmi.InvalidArgument):
+        wmi.decode_alg_bytes(hp, 0, steps)

@@ -8,6 +8,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import numpy as np
 
@@ -69,12 +70,80 @@ def test_bench_launches_its_own_ranks():
     assert abs(res["value"] / (2 * 8 * 30.0 * 4 / (max(res["rank_ms"]) / 1e3)) - 1) < 1e-3
 
 
+def _launcher(extra_env, *args, timeout=120):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT", "WMI_TEST_FAIL_RANK", "WMI_TEST_HANG_RANK")}
+    env.update(extra_env)
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"] + list(args),
+                       env=env, capture_output=True, text=True, timeout=timeout)
+    return p, time.monotonic() - t0
+
+
 def test_bench_launcher_fails_when_a_rank_fails():
-    """A rank that exits non-zero makes the launcher exit non-zero."""
-    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--dry-run",
-                        "--roofline-kernel", "99"], env=env, capture_output=True, text=True, timeout=120)
-    assert p.returncode != 0
+    """Rank 1 exits with status 3 after the rendezvous while rank 0 hangs
+    (as a rank blocked inside RCCL would): the launcher kills rank 0 at once —
+    long before its deadline — and exits with rank 1's status, without a
+    result line.  Without the hang, rank 0 notices the closed peer itself and
+    the launcher still exits non-zero."""
+    p, el = _launcher({"WMI_TEST_FAIL_RANK": "1", "WMI_TEST_HANG_RANK": "0"}, "--steps", "2", "--warmup", "1")
+    assert p.returncode == 3, p.stderr[-2000:]
+    assert "rank 1 exited with status 3" in p.stderr
+    assert "WMI_TEST_FAIL_RANK" in p.stderr  # the rank got past the rendezvous before failing
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert el < 60
+    p, _ = _launcher({"WMI_TEST_FAIL_RANK": "1"}, "--steps", "2", "--warmup", "1")
+    assert p.returncode != 0 and "stopping the other ranks" in p.stderr
+
+
+def test_bench_launcher_deadline_kills_a_hung_rank():
+    """Rank 1 hangs after the rendezvous: at the deadline the launcher kills
+    every rank and exits non-zero (124) instead of polling forever."""
+    p, el = _launcher({"WMI_TEST_HANG_RANK": "1"}, "--steps", "2", "--warmup", "1", "--launch-deadline", "8")
+    assert p.returncode == 124, p.stderr[-2000:]
+    assert "deadline of 8 s passed" in p.stderr
+    assert 8 <= el < 60
+
+
+def test_rendezvous_skips_a_busy_hub_port():
+    """The first hub port is held by another listener that never answers the
+    handshake: rank 0 binds the next candidate and rank 1 finds it there."""
+    import threading
+
+    import dist
+    base = _free_port()
+    ports = dist.hub_ports(base)
+    squatter = socket.socket()
+    squatter.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    try:
+        squatter.bind(("127.0.0.1", ports[0]))
+    except OSError:
+        import pytest
+        pytest.skip("candidate port taken")
+    squatter.listen(4)
+    old = os.environ.get("MASTER_PORT")
+    os.environ["MASTER_PORT"] = str(base)
+    try:
+        res = {}
+
+        def hub():
+            g = dist.Group(0, 2, "127.0.0.1", timeout=30)
+            res["gather"] = g.all_gather("hub")
+            g.close()
+
+        t = threading.Thread(target=hub)
+        t.start()
+        peer = dist.Group(1, 2, "127.0.0.1", timeout=30)
+        assert peer.all_gather("peer") == ["hub", "peer"]
+        peer.close()
+        t.join(30)
+        assert res["gather"] == ["hub", "peer"]
+    finally:
+        squatter.close()
+        if old is None:
+            del os.environ["MASTER_PORT"]
+        else:
+            os.environ["MASTER_PORT"] = old
 
 
 def test_rendezvous_messages_are_data_only():

@@ -285,11 +285,9 @@ struct wmi_context {
     bool persist_logits = false;      // WMI_PERSIST_LOGITS=1: also store every step's logits (dlogits)
     int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
     int enc_layers = 0;               // WMI_ENC_LAYERS (debug): run only the first encoder layers
-    int fault_inject = 0;             // WMI_FAULT_INJECT=1 (test): mark the first persistent block as timed out
-    // WMI_KVL=1: one-row launches hold self-attention K / V in LDS with the
-    // wave-local attention (bitwise equal to the memory path, but 149.5 vs
-    // 141.2 us a base step on one box, profiles/r03/ab_r03g_*): off by default
-    bool use_kvl = false;
+    int fault_inject = 0;             // WMI_FAULT_INJECT=1 (test): the first persistent launch runs with one
+                                      // workgroup missing (PersistArgs::stall_wg): the device abort path
+    bool persist_coop = true;         // WMI_COOP=0: plain launches of the persistent grid
     bool use_xshare = true;           // WMI_XSHARE=0: beam rows read the cross K / V per row
     int n_fallbacks = 0;              // decodes re-run on the kernel chain after a persistent exchange timeout
     PersistLayer *d_players = nullptr;
@@ -933,12 +931,15 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
             }
             if (ok) K = k;
         }
-        if (!K) return set_err(ctx, WMI_E_HIP, "no collision-free exp fallback hash");
-        for (int i = 0; i < 64; ++i) tab[i] = 0xffffffffu;
-        for (uint32_t i = 0; i < nfb; ++i) tab[((fb[i] >> 16) * K) >> 26] = fb[i];
-        tab[64] = nfb;
-        tab[65] = K;
-        HIPCHK(ctx, hipMemcpy(ctx->d_expfb, tab, 66 * 4, hipMemcpyHostToDevice));
+        if (!K) {
+            ctx->use_persist = false;  // (not seen) no collision-free hash: the kernel chain decodes
+        } else {
+            for (int i = 0; i < 64; ++i) tab[i] = 0xffffffffu;
+            for (uint32_t i = 0; i < nfb; ++i) tab[((fb[i] >> 16) * K) >> 26] = fb[i];
+            tab[64] = nfb;
+            tab[65] = K;
+            HIPCHK(ctx, hipMemcpy(ctx->d_expfb, tab, 66 * 4, hipMemcpyHostToDevice));
+        }
     }
     if (ctx->wf32) ctx->use_persist = false;  // f32 matrices: the kernel chain with the f32 GEMVs
     return WMI_OK;
@@ -1481,6 +1482,19 @@ int dec_err(wmi_context *ctx, uint32_t err) {
 // self-attention key capacity for M = pos + 1 keys
 int self_mk_for(int M) { return M <= 64 ? 64 : M <= 128 ? 128 : M <= 256 ? 256 : 512; }
 
+// err bit 3: a persistent grid was not co-resident (the decoder assumes one
+// context per GPU and nothing else running on it); its workgroups drained
+// through the abort word.  The context then decodes on the kernel chain for
+// good (a later decode would otherwise pay the bounded spin again), and the
+// caller re-runs the decode that failed.
+bool persist_fallback(wmi_context *ctx, uint32_t err) {
+    if (!(err & 8u) || !ctx->use_persist) return false;
+    fprintf(stderr, "[wmi] persistent decoder exchange timed out; this context decodes on the kernel chain from now on\n");
+    ++ctx->n_fallbacks;
+    ctx->use_persist = false;
+    return true;
+}
+
 // run `steps` decoder steps for clips [b0, b0+B), the first at position pos0,
 // via captured hipGraphs: one per configuration and self-attention key
 // capacity, so a chunk is split where pos + 1 crosses 64 / 128 / 256
@@ -1642,6 +1656,12 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     a.cur_tok = ctx->d_curtok; a.suppress_id = suppress_eot ? ctx->sp.eot : -1;
     a.xg = ctx->d_xg; a.err = ctx->derr;
     a.nres = ctx->persist_nres[B];
+    a.coop = ctx->persist_coop ? 1 : 0;
+    a.stall_wg = -1;
+    if (ctx->fault_inject == 1) {  // once per context: its first persistent launch
+        a.stall_wg = G - 1;
+        ctx->fault_inject = 2;
+    }
     a.logits_out = ctx->persist_logits ? ctx->dlogits : nullptr;
     // q5_1 blocks in the persistent GEMVs (the ggml dequant x activation
     // product of a q5_1 file), dequantised inside each phase's poll so the
@@ -1652,22 +1672,6 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     const bool have5 = ctx->use_q5 && !ctx->dec.empty() && ctx->dec[0].wqkv5;
     a.q5 = have5 && ctx->persist_q5 != 0 ? 1 : 0;
     return a;
-}
-
-// LDS-resident self-attention K / V for a one-row launch ending before
-// position pos_end (PersistArgs::kvl): every (layer, head) gets a workgroup of
-// its own, whose LDS (the vocabulary-row region) holds the head's rows; that
-// workgroup streams vkv vocabulary rows, chosen so its stream matches the
-// others' (resident nres + streamed rest)
-void set_kvl(wmi_context *ctx, PersistArgs &pa, int G, int pos_end) {
-    const int H = ctx->hp.n_text_head, L = ctx->dec_layers, n = ctx->hp.n_text_state, V = ctx->hp.n_vocab;
-    const int nk = L * H, cap = (pos_end + 31) / 32 * 32;
-    if (!ctx->use_kvl || pa.B != 1 || pa.beam || nk >= G || cap > 512 || (int64_t)cap * 256 > (int64_t)pa.nres * n * 2)
-        return;
-    pa.kvl = 1;
-    pa.kvcap = cap;
-    const int64_t vk = ((int64_t)V - (int64_t)pa.nres * (G - nk) + G - 1) / G;
-    pa.vkv = (int)(vk > 0 ? vk : 0);
 }
 
 // greedy decode of every encoded clip; tokens stay in ctx->dtokens
@@ -1705,11 +1709,8 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
             if (G > 0) {  // persistent decoder: the chunk's steps in one launch
                 PersistArgs pa = persist_args(ctx, b0, B, G, np, np, suppress_eot, n_gen);
                 pa.n_steps = chunk;
-                if (chunk >= 8) set_kvl(ctx, pa, G, done_steps + chunk);
                 if (ctx->d_ptrace && done_steps == 0 && b0 == 0) pa.ptrace = ctx->d_ptrace;
                 HIPCHK(ctx, launch_dec_persist(ctx->stream, pa, G));
-                if (ctx->fault_inject && b0 == 0 && done_steps == 0)  // as a stranded grid reports it
-                    HIPCHK(ctx, hipMemsetAsync(ctx->derr, 8, 1, ctx->stream));
                 if (pa.ptrace) rc = ptrace_dump(ctx, chunk);
                 else rc = 0;
             } else {
@@ -1747,17 +1748,7 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
         uint32_t err = 0;
         HIPCHK(ctx, hipMemcpyAsync(&err, ctx->derr, 4, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        if ((err & 8u) && ctx->use_persist) {
-            // a persistent grid was not co-resident (the decoder assumes one
-            // context per GPU and nothing else running on it): the kernels
-            // drained through the abort word; decode again on the kernel chain
-            fprintf(stderr, "[wmi] persistent decoder exchange timed out; decoding on the kernel chain\n");
-            ++ctx->n_fallbacks;
-            ctx->use_persist = false;
-            const int r2 = run_greedy(ctx, n_gen, suppress_eot, early_stop, host_tokens, host_counts);
-            ctx->use_persist = true;
-            return r2;
-        }
+        if (persist_fallback(ctx, err)) return run_greedy(ctx, n_gen, suppress_eot, early_stop, host_tokens, host_counts);
         if (err) return dec_err(ctx, err);
     }
     if (ctx->trace_on) {
@@ -1850,6 +1841,7 @@ int run_ts_window(wmi_context *ctx, int clip, const std::vector<int32_t> &prompt
     }
     uint32_t err = 0;
     HIPCHK(ctx, hipMemcpy(&err, ctx->derr, 4, hipMemcpyDeviceToHost));
+    if (persist_fallback(ctx, err)) return run_ts_window(ctx, clip, prompt, max_tokens, out);
     if (err) return dec_err(ctx, err);
     out->assign(rec.begin(), rec.begin() + n_out);
     return WMI_OK;
@@ -2002,8 +1994,12 @@ int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_st
             }
         }
         BeamState bs{};
+        uint32_t err = 0;
         HIPCHK(ctx, hipMemcpyAsync(&bs, ctx->dbstate, sizeof bs, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(&err, ctx->derr, 4, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (persist_fallback(ctx, err)) return run_beam(ctx, K, n_gen, suppress_eot, early_stop, out_tokens, out_scores);
+        if (err) return dec_err(ctx, err);
         const int ns = bs.n_steps;
         if (ns < 1) return set_err(ctx, WMI_E_HIP, "beam search produced no step");
         std::vector<int32_t> hpar((size_t)ns * BEAM_MAX), htok((size_t)ns * BEAM_MAX);
@@ -2042,9 +2038,6 @@ int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_st
         if (out_tokens) (*out_tokens)[clip] = seq;
         if (out_scores) (*out_scores)[clip] = score;
     }
-    uint32_t err = 0;
-    HIPCHK(ctx, hipMemcpy(&err, ctx->derr, 4, hipMemcpyDeviceToHost));
-    if (err) return dec_err(ctx, err);
     return WMI_OK;
 }
 
@@ -2140,8 +2133,8 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (getenv("WMI_PERSIST_LOGITS")) ctx->persist_logits = true;
     if (const char *e = getenv("WMI_PERSIST_Q5")) ctx->persist_q5 = atoi(e) ? 1 : 0;
     if (const char *c = getenv("WMI_CHECKSUMS")) ctx->checksums = atoi(c) != 0;
-    if (const char *c = getenv("WMI_FAULT_INJECT")) ctx->fault_inject = atoi(c);
-    if (const char *c = getenv("WMI_KVL")) ctx->use_kvl = atoi(c) != 0;
+    if (const char *c = getenv("WMI_FAULT_INJECT")) ctx->fault_inject = atoi(c) ? 1 : 0;
+    if (const char *c = getenv("WMI_COOP")) ctx->persist_coop = atoi(c) != 0;
     if (const char *c = getenv("WMI_XSHARE")) ctx->use_xshare = atoi(c) != 0;
     ctx->dec_layers = ctx->hp.n_text_layer;
     if (const char *c = getenv("WMI_DEC_LAYERS")) ctx->dec_layers = std::max(1, std::min(atoi(c), ctx->hp.n_text_layer));
@@ -2457,6 +2450,7 @@ static int wmi_decode_logits_impl(wmi_context *ctx, int clip, const int32_t *tok
     uint32_t err = 0;
     HIPCHK(ctx, hipMemcpyAsync(&err, ctx->derr, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (persist_fallback(ctx, err)) return wmi_decode_logits_impl(ctx, clip, tokens, n_tokens, logits);
     if (err) return dec_err(ctx, err);
     return WMI_OK;
 }
@@ -2595,6 +2589,29 @@ int wmi_get_cross_kv(const wmi_context *ctx, int clip, uint16_t *k, uint16_t *v,
     return WMI_OK;
 }
 
+int wmi_decode_alg_bytes(const wmi_hparams *hp, int rows, int steps, int beam, int q5, double *bytes_out,
+                         double *flops_out) {
+    if (!hp || rows < 1 || steps < 0 || !bytes_out) return WMI_E_INVALID_ARG;
+    const double nt = hp->n_text_state, L = hp->n_text_layer, Tx = hp->n_audio_ctx, V = hp->n_vocab;
+    // (q5_1 GEMVs: Wqkv, Wo, Wco, W0, W1 = 13 n^2 weights at 24 bytes a
+    // 32-weight block; Wcq stays f16)
+    const double w_mat = q5 ? 13.0 * nt * nt * 0.75 + 2.0 * nt * nt : 28.0 * nt * nt;
+    const double w_step = L * (w_mat + 68.0 * nt) + V * nt * 2 + 2 * nt * 4;
+    double bytes = 0, flops = 0;
+    for (int b0 = 0; b0 < rows; b0 += beam ? rows : 8) {
+        const double r = beam ? rows : (rows - b0 < 8 ? rows - b0 : 8);
+        for (int pos = 0; pos < steps; ++pos) {
+            bytes += w_step + r * (nt * 2 + nt * 4);                      // weights, token + position rows
+            bytes += (beam ? 1.0 : r) * L * Tx * nt * 2 * 2;              // cross K, V (one clip's when beam)
+            bytes += r * L * ((double)pos * nt * 2 * 2 + nt * 2 * 2);     // self K, V read + new row
+            flops += r * (2.0 * L * (14.0 * nt * nt + 2.0 * Tx * nt + 2.0 * (pos + 1) * nt) + 2.0 * V * nt);
+        }
+    }
+    *bytes_out = bytes;
+    if (flops_out) *flops_out = flops;
+    return WMI_OK;
+}
+
 int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *out) {
     if (!valid(ctx) || !out || iters < 1) return WMI_E_INVALID_ARG;
     if (ctx->enc_T <= 0) return set_err(ctx, WMI_E_INVALID_ARG, "bench_kernel before a pipeline run");
@@ -2674,30 +2691,10 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
         if (nw != 1 && nw != 2 && nw != 4) nw = (int64_t)((T + 127) / 128) * hp.n_audio_head * B >= 512 ? 4 : 2;
         snprintf(out->name, sizeof out->name, "k_attn_enc4<%d>", nw);
     } else if (which == 14) {
-        // algorithmic bytes of one decode: every step reads each decoder
-        // weight, bias and LayerNorm vector once (shared by the block's rows),
-        // the vocabulary matrix once, each row's cross K/V and self K/V rows
-        // [0, pos] once, and writes its new self K/V row
-        const double L = hp.n_text_layer, Tx = T;
         int32_t prompt[8];
         const int np = prompt_tokens(ctx, prompt), steps = np + ctx->staged_n_decode - 1;
-        // (q5_1 GEMVs: Wqkv, Wo, Wco, W0, W1 = 13 n^2 weights at 24 bytes a
-        // 32-weight block; Wcq stays f16)
         const bool dq5 = ctx->use_q5 && !ctx->dec.empty() && ctx->dec[0].wqkv5 && ctx->persist_q5 != 0;
-        const double w_mat = dq5 ? 13.0 * nt * nt * 0.75 + 2.0 * nt * nt : 28.0 * nt * nt;
-        const double w_step = L * (w_mat + 68.0 * nt) + V * nt * 2 + 2 * nt * 4;
-        double bytes = 0, flops = 0;
-        for (int b0 = 0; b0 < B; b0 += 8) {
-            const double rows = B - b0 < 8 ? B - b0 : 8;
-            for (int pos = 0; pos < steps; ++pos) {
-                bytes += w_step + rows * (nt * 2 + nt * 4);                 // weights, token + position rows
-                bytes += rows * L * Tx * nt * 2 * 2;                         // cross K, V
-                bytes += rows * L * ((double)pos * nt * 2 * 2 + nt * 2 * 2);  // self K, V read + new row
-                flops += rows * (2.0 * L * (14.0 * nt * nt + 2.0 * Tx * nt + 2.0 * (pos + 1) * nt) + 2.0 * V * nt);
-            }
-        }
-        out->alg_bytes = bytes;
-        out->alg_flops = flops;
+        wmi_decode_alg_bytes(&hp, B, steps, 0, dq5 ? 1 : 0, &out->alg_bytes, &out->alg_flops);
         snprintf(out->name, sizeof out->name, "k_dec_persist<%d,%d%s> (%d steps)", (int)nt, B == 1 ? 1 : 8,
                  dq5 ? ",Q5" : "", steps);
     } else {

@@ -360,16 +360,18 @@ struct PersistArgs {
     const int32_t *kv_src;       // [B][kv_src_stride] or null
     int kv_src_stride;
     int q5;                      // GEMVs of phases A, C, G2, H, I read the layers' q5_1 repacks
-    // one-row launches: self-attention K / V rows held in LDS.  Workgroup
-    // l * H + h owns head h of layer l for the whole launch: it copies rows
-    // [0, pos) of its head from the cache at the start and appends each new
-    // row itself, so no step reads the cache through memory; its LDS holds
-    // no vocabulary rows, and it takes vkv vocabulary rows (all streamed)
-    int kvl, kvcap, vkv;
     // beam launches (rows = hypotheses of one clip, n > 768): one cross-
     // attention task per (head, key chunk) covers every row (PersistArgs::nch
     // then counts the chunks of one head: H * nch tasks)
     int xshare;
+    // fault injection (tests): workgroup stall_wg exits at once, as a
+    // workgroup that never became resident — every other workgroup's first
+    // poll of its rows runs into the bounded spin, raises the abort word and
+    // err bit 3, and the grid drains (-1: none)
+    int stall_wg;
+    // host side: launch through hipLaunchCooperativeKernel (the runtime then
+    // checks the grid against the device's co-residency limit at launch)
+    int coop;
 };
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G);
 // the inputs whose f32 exp is too close to an f16 midpoint, with their table

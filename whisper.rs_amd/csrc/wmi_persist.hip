@@ -111,15 +111,10 @@ __device__ __forceinline__ const WMI_AS(1) T *glb(const T *p) {
     return (const WMI_AS(1) T *)p;
 }
 typedef const WMI_AS(4) PersistLayer ConstLayer;
-// once-per-step streams (weight chunks, cross K/V): the non-temporal policy
-// in WMI_PNT builds (MI355X_MICROARCH.md nt-weights), else the default
+// once-per-step streams (weight chunks, cross K/V), default cache policy
 template <typename T>
 __device__ __forceinline__ T sld(const T *p) {
-#ifdef WMI_PNT
-    return __builtin_nontemporal_load(glb(p));
-#else
     return *glb(p);
-#endif
 }
 
 struct PShared {
@@ -556,11 +551,6 @@ struct MSet {
         }
     }
 };
-#ifdef WMI_NO_MGV
-constexpr bool kMGV = false;  // (build option: the VALU GEMVs at every n)
-#else
-constexpr bool kMGV = true;
-#endif
 // a phase's weight set: MFMA for several rows at n <= 512, else VALU.  One
 // row keeps the quarter-wave VALU GEMVs: on MFMA its step took 3.6 % longer
 // (base 18.56 vs 17.84 ms decode; 8 rows 28.8 vs 32.0 ms, A/B x3,
@@ -568,14 +558,9 @@ constexpr bool kMGV = true;
 // its GEMV dots in different (each fixed) orders
 // (the K = 4n phase I above n = 512 reads its A fragments from LDS at each
 // MFMA step instead of holding all 4n / 128 of them in registers)
-#ifdef WMI_MGV_512  // (build option: MFMA GEMVs only up to n = 512)
-constexpr int kMGVN = 512;
-#else
-constexpr int kMGVN = 1280;
-#endif
 template <int NS, int BT, int KCH, int NP, int KS, bool Q5>
 using PSet = typename std::conditional<
-    kMGV && (BT > 1) && NS <= kMGVN,
+    (BT > 1),
     typename std::conditional<(NS <= 512 || KCH <= NS / 128), MSet<KCH, NP, Q5>, MSet<KCH, NP, Q5, true>>::type,
     GSet<KCH, NP, KS, Q5>>::type;
 
@@ -852,19 +837,12 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     constexpr int NPL = KC <= 4 ? 2 : 1;  // logits passes per register set
     // logits on MFMA (n <= 512): v_mfma_f32_16x16x32_f16 with the rows'
     // hidden states as A (rows >= B zero) and 16 vocabulary rows as B
-#ifdef WMI_NO_LMF
-    constexpr bool LMF = false;
-#else
     constexpr bool LMF = KC <= 4;
-#endif
     // several rows at n > 512: the four waves split K (n / 4 each) over every
     // 16-row tile, partials added in wave order through LDS (the A fragments
     // and a tile's B fragments of all of K would not fit the registers)
-    constexpr bool LMF2 = !LMF && BT > 1 && kMGV;
-#ifndef WMI_XQF_KC
-#define WMI_XQF_KC 6
-#endif
-    constexpr bool XQF = KC <= WMI_XQF_KC;  // cross q computed inside the score tasks (registers allow)
+    constexpr bool LMF2 = !LMF && BT > 1;
+    constexpr bool XQF = KC <= 6;  // cross q computed inside the score tasks (registers allow)
     // cross-attention softmax: several rows (8 clips, beam slots) split it in
     // two small hand-offs (chunk maxima, then chunk exp sums; each task's
     // scores stay in LDS) instead of every task sweeping its row's T scores;
@@ -880,6 +858,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ PShared sh;
     const int B = BT == 1 ? 1 : a.B, G = gridDim.x, wg = blockIdx.x;
+    if (wg == a.stall_wg) return;  // (fault injection: a workgroup that never ran)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int L = a.L, T = a.T, tctx = a.tctx, nch = a.nch, CL = a.cl;
     const int nsub = (T + 127) >> 7;  // 128-key P.V partials per (row, head)
@@ -914,41 +893,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     part(NS, true, rn0, rn1);      // Wo / Wcq / Wco / W1 rows = this WG's residual rows
     part(3 * NS, true, ra0, ra1);  // Wqkv rows
     part(4 * NS, true, rh0, rh1);  // W0 rows
-    // LDS-resident self-attention K / V (PersistArgs::kvl): workgroups
-    // [0, L H) own one (layer, head) each
-    const bool kvl = BT == 1 && a.kvl;
     // the GEMV phases' partial sums: LDS scratch for the MFMA GEMVs, else the split-K buffer
-    float *kpbuf = BT > 1 && kMGV ? (float *)scr : sh.kpart;  // (an MSet phase's partials; sh.kpart for GSet's split-K)
-    const int nkw = kvl ? L * H : 0;
-    const bool kvw = wg < nkw;
-    f16 *Kl = vres, *Vl = vres + (size_t)a.kvcap * 64;  // [kvcap][64] each (K chunks swizzled)
-    if (kvl) {  // vocabulary rows: vkv for each K / V owner, the rest spread over the others
-        const int ro = (a.V - nkw * a.vkv + (G - nkw) - 1) / (G - nkw);
-        rv0 = kvw ? wg * a.vkv : nkw * a.vkv + (wg - nkw) * ro;
-        rv0 = rv0 < a.V ? rv0 : a.V;
-        rv1 = rv0 + (kvw ? a.vkv : ro);
-        rv1 = rv1 < a.V ? rv1 : a.V;
-    } else {
-        part(a.V, false, rv0, rv1);
-    }
+    float *kpbuf = BT > 1 ? (float *)scr : sh.kpart;  // (an MSet phase's partials; sh.kpart for GSet's split-K)
+    part(a.V, false, rv0, rv1);
     const int rn = rn1 - rn0;
     // this workgroup's first vocabulary rows stay in LDS for the whole launch
-    // (a K / V owner keeps its head's rows there instead)
-    const int rs0 = kvw ? rv0 : rv0 + a.nres < rv1 ? rv0 + a.nres : rv1;
-    if (kvw) {
-        // rows [0, pos) of head h, layer l from the cache (written by earlier
-        // launches: plain loads); K chunk c of row j at slot c ^ (j & 7) and V
-        // chunk c at slot c ^ ((j >> 3) & 7), so the row-per-lane reads of the
-        // score loop and of P.V hit distinct banks
-        const int l0 = wg / H, h0 = wg - l0 * H, p0 = a.st->pos;
-        const f16 *kcs = (const f16 *)a.kcache + (size_t)l0 * DEC_ROWS * tctx * NS + h0 * 64;
-        const f16 *vcs = (const f16 *)a.vcache + (size_t)l0 * DEC_ROWS * tctx * NS + h0 * 64;
-        for (int i = tid; i < p0 * 8; i += PT) {
-            const int j = i >> 3, c = i & 7;
-            *(half8 *)(Kl + j * 64 + ((c ^ (j & 7)) * 8)) = *(const half8 *)(kcs + (int64_t)j * NS + c * 8);
-            *(half8 *)(Vl + j * 64 + ((c ^ ((j >> 3) & 7)) * 8)) = *(const half8 *)(vcs + (int64_t)j * NS + c * 8);
-        }
-    } else {
+    const int rs0 = rv0 + a.nres < rv1 ? rv0 + a.nres : rv1;
+    {
         const uint4 *src = (const uint4 *)((const f16 *)a.te + (int64_t)rv0 * NS);
         uint4 *dst = (uint4 *)vres;
         // (MFMA logits: 16-byte chunk c of resident row j at c ^ (j & 15), so
@@ -1096,105 +1047,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 const __amdgpu_buffer_rsrc_t rv = rsrc_of(vc, (uint32_t)(DEC_ROWS * tctx * NS * 2));
                 f16 *qn = (f16 *)scr, *kn = qn + 64, *vn = qn + 128;  // this step's q, k, v of the head
                 uint16_t *P16 = (uint16_t *)(scr + 512);                 // [512]
-                // (K / V owners: workgroup l H + h takes head h of layer l)
-                for (int t = kvl ? wg - l * H : wg; t >= 0 && t < B * H; t += G) {
+                for (int t = wg; t < B * H; t += G) {
                     const int b = t / H, h = t - b * H;
-                    if (kvl) {
-                        // K / V from this workgroup's LDS copy and no exchange
-                        // between its waves: every wave computes all M = pos + 1
-                        // scores and the softmax (the max, and the double sum
-                        // of f16 values, are exact in any order: the same P16
-                        // in every wave), then P.V for its 16 output dims.  Each
-                        // P.V lane sums its keys kg + 32 i in i order and the
-                        // key groups combine in the memory path's order (xor 8,
-                        // 16, 32, then groups 0..3 in sequence), so the outputs
-                        // are bitwise those of the memory path.
-                        __syncthreads();
-                        const int64_t hq = b * (NS / 2) + h * 32;
-                        const bool ok = gpoll(96, ptag(pos, L, l, 0),
-                                              [=](int i) { return xg + oQ + (i >> 5) * (4 * NS) + hq + (i & 31); },
-                                              (uint32_t *)qn, abortw, a.err);
-                        if (check(ok)) return;
-                PSTAMP(l * 32 + 17)
-                        const int M = pos + 1;
-                        if (tid < 16 && pos < a.kvcap) {  // this step's row joins the LDS copy
-                            if (tid < 8) *(half8 *)(Kl + pos * 64 + ((tid ^ (pos & 7)) * 8)) = *(const half8 *)(kn + tid * 8);
-                            else *(half8 *)(Vl + pos * 64 + (((tid - 8) ^ ((pos >> 3) & 7)) * 8)) = *(const half8 *)(vn + (tid - 8) * 8);
-                        }
-                        // (loops over a lane's key slots are not unrolled: the
-                        // scores and p live in this wave's LDS, not in registers)
-                        float *sP = (float *)(scr + 2048) + w * 512;                 // this wave's scores, then p [512]
-                        uint16_t *P16w = (uint16_t *)(scr + 2048 + 4 * 2048) + w * 512;  // this wave's P16 [512]
-                        const int nk = (M + 63) >> 6;
-                        float mx = -INFINITY;
-#pragma unroll 1
-                        for (int k = 0; k < nk; ++k) {
-                            const int j = lane + 64 * k;
-                            const int jr = j < pos ? j : 0;
-                            float s = 0.0f;
-#pragma unroll
-                            for (int i = 0; i < 8; ++i) {
-                                const half8 q = *(const half8 *)(qn + 8 * i);
-                                const half8 kl = *(const half8 *)(Kl + jr * 64 + ((i ^ (jr & 7)) * 8));
-                                const half8 kp = *(const half8 *)(kn + 8 * i);
-                                s = dot8(j == pos ? kp : kl, q, s);
-                            }
-                            sP[j] = s;
-                            if (j < M) mx = fmaxf(mx, s);
-                        }
-                        mx = wave_max(mx);
-                        double sum = 0.0;
-#pragma unroll 1
-                        for (int k = 0; k < nk; ++k) {
-                            const int j = lane + 64 * k;
-                            const float pj = exp_f16_hash(sP[j] - mx, sh.expfb, fbk);
-                            if (j < M) {
-                                sum += (double)pj;
-                                sP[j] = pj;
-                            }
-                        }
-                        sum = wave_sum(sum);
-                        const float inv = (float)(1.0 / sum);
-#pragma unroll 1
-                        for (int k = 0; k < nk; ++k) {
-                            const int j = lane + 64 * k;
-                            if (j < M) P16w[j] = f2h_bits(sP[j] * inv);
-                        }
-                        wave_sync();
-                        // P.V: lane -> key group kg (bits 0-2 from lane bits 3-5, bits
-                        // 3-4 from lane bits 0-1), dim octet 2 w + lane bit 2
-                        const int kg = ((lane >> 3) & 7) | ((lane & 3) << 3), dct = 2 * w + ((lane >> 2) & 1);
-                        float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-                        for (int i = 0; 32 * i < pos; ++i) {  // (the rest add zeros)
-                            const int j = kg + 32 * i;
-                            const int jr = j < pos ? j : 0;
-                            const half8 vr = *(const half8 *)(Vl + jr * 64 + ((dct ^ ((jr >> 3) & 7)) * 8));
-                            const float pj = j < pos ? h2f_bits(P16w[jr]) : 0.0f;
-#pragma unroll
-                            for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vr[e];
-                        }
-                        if (kg == (pos & 31)) {
-                            const float pj = h2f_bits(P16w[pos]);
-                            const half8 vr = *(const half8 *)(vn + dct * 8);
-#pragma unroll
-                            for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vr[e];
-                        }
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) {
-                            float v = red_8_16_32(o[e]);
-                            // key groups 0..3 (lane bits 0-1) in sequence: ((g0 + g1) + g2) + g3
-                            const float g1 = __uint_as_float(dpp_xor1(__float_as_uint(v)));
-                            const float g2 = __uint_as_float(dpp_xor2(__float_as_uint(v)));
-                            const float g3 = __uint_as_float(dpp_xor3(__float_as_uint(v)));
-                            o[e] = ((v + g1) + g2) + g3;
-                        }
-                        if ((lane & ~4) == 0)  // lanes 0 and 4: dims dct * 8 .. + 7
-#pragma unroll
-                            for (int e = 0; e < 8; e += 2)
-                                gput(xg + oO + b * (NS / 2) + h * 32 + dct * 4 + e / 2, ptag(pos, L, l, 1), pack2(o[e], o[e + 1]));
-                        continue;
-                    }
                     const int doct = tid & 7, jg = tid >> 3;
                     // cache rows j < pos (this step's row comes from the granules)
                     half8 kv[2][8];
@@ -1226,25 +1080,15 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     for (int r = 0; r < 2; ++r) {
                         const int j = tid + 256 * r;
                         const uint32_t off = (uint32_t)((((int64_t)srk[r] * tctx + j) * NS + h * 64) * 2);
-#ifdef WMI_EXP_NOKV  // timing diagnostic only: no cache reads (wrong results)
-                        (void)off;
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) kv[r][i] = z8;
-#else
 #pragma unroll
                         for (int i = 0; i < 8; ++i) kv[r][i] = j < pos ? bload_sc1(rk, off + 16 * i) : z8;
-#endif
                     }
                     // value rows j < pos, in flight across the poll as well
                     half8 vv[16];
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
                         const int j = jg + 32 * i;
-#ifdef WMI_EXP_NOKV
-                        vv[i] = z8;
-#else
                         vv[i] = j < pos ? bload_sc1(rv, (uint32_t)((((int64_t)srv[i] * tctx + j) * NS + h * 64 + doct * 8) * 2)) : z8;
-#endif
                     }
                     PREFETCH_ISSUED
                     __syncthreads();
@@ -2363,11 +2207,15 @@ hipError_t launch_nsb(hipStream_t s, const PersistArgs &a, int G) {
     PersistArgs b = a;
     const int maxr = (int)((avail - base) / (NS * 2));
     if (b.nres > maxr) b.nres = maxr;
-    if (b.kvl && (int64_t)b.kvcap * 256 > (int64_t)b.nres * NS * 2) return hipErrorInvalidValue;
     const size_t lds = base + (size_t)b.nres * NS * 2;
     hipError_t e = hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM, Q5>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
+    if (b.coop) {
+        void *args[] = {&b};
+        return hipLaunchCooperativeKernel((const void *)k_dec_persist<NS, BT, BEAM, Q5>, dim3(G), dim3(PT), args,
+                                          (unsigned)lds, s);
+    }
     hipLaunchKernelGGL((k_dec_persist<NS, BT, BEAM, Q5>), dim3(G), dim3(PT), lds, s, b);
     return hipGetLastError();
 }
@@ -2495,9 +2343,7 @@ hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G) {
         a.tctx > 512 || a.cl % 128 || (a.beam && a.n_steps != 1) || (a.kv_src && a.kv_src_stride < a.tctx) ||
         ((int64_t)a.B * (a.n / 64) * a.nch + G - 1) / G * a.cl * 4 > XS_BYTES ||  // task scores in LDS
         (a.xshare && (!a.beam || a.n <= 768 || ((int64_t)(a.n / 64) * a.nch + G - 1) / G * a.B * a.cl * 4 > XS_BYTES ||
-                      a.B * a.nch * 4 > 2048 || a.B * a.nch * 8 > 4096)) ||
-        (a.kvl && (a.B != 1 || a.beam || a.L * (a.n / 64) >= G || a.kvcap < 32 || a.kvcap > 512 ||
-                   (int64_t)a.kvcap * 256 > (int64_t)a.nres * a.n * 2 || a.vkv < 0)))
+                      a.B * a.nch * 4 > 2048 || a.B * a.nch * 8 > 4096)))
         return hipErrorInvalidValue;
     switch (a.n) {
         case 128: return launch_ns<128>(s, a, G);

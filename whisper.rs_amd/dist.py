@@ -16,7 +16,17 @@ import struct
 import time
 
 _PORT_OFFSET = 23  # torchrun's own TCPStore holds MASTER_PORT itself
+_PORT_TRIES = 8     # hub ports MASTER_PORT + 23 + 97 k, k < 8: the first one rank 0 can bind
+_PORT_STRIDE = 97
 _MAX_MSG = 1 << 24  # messages are ids, timings and small token lists
+_MAGIC = b"wmi-rdv1"
+
+
+def hub_ports(master_port: int):
+    """Candidate ports of the rank-0 hub.  Rank 0 binds the first free one;
+    peers try them in order and keep the one whose listener answers the
+    rendezvous handshake (a foreign program on a candidate port is skipped)."""
+    return [master_port + _PORT_OFFSET + _PORT_STRIDE * k for k in range(_PORT_TRIES)]
 
 
 def _enc(obj) -> bytes:
@@ -79,48 +89,85 @@ class Group:
 
     def __init__(self, rank: int, world: int, addr: str | None = None, port: int | None = None,
                  timeout: float = 300.0):
+        """port: the hub's port, bound as given (tests); by default the first
+        bindable port of hub_ports(MASTER_PORT).  Every socket operation and
+        the whole rendezvous are bounded by `timeout` seconds."""
         self.rank, self.world = rank, world
         self.peers = []
         self.sock = None
         if world == 1:
             return
         addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
-        port = port or int(os.environ.get("MASTER_PORT", "29500")) + _PORT_OFFSET
+        ports = [port] if port else hub_ports(int(os.environ.get("MASTER_PORT", "29500")))
+        hello = _MAGIC + struct.pack("<ii", world, ports[0])
         if rank == 0:
-            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
-            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-            srv.bind((addr, port))
-            srv.listen(world)
-            srv.settimeout(timeout)
-            peers = {}
-            while len(peers) < world - 1:
-                c, _ = srv.accept()
-                c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                c.settimeout(timeout)
+            srv = None
+            for p in ports:  # bind check: the first free candidate
+                s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+                s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
                 try:
-                    hello = _recv(c)
-                    r = struct.unpack("<i", hello)[0] if len(hello) == 4 else -1
-                except (ConnectionError, OSError):
-                    r = -1
-                if not 1 <= r < world or r in peers:  # out of range or duplicate: not a peer
-                    c.close()
+                    s.bind((addr, p))
+                except OSError:
+                    s.close()
                     continue
-                peers[r] = c
-            srv.close()
+                srv = s
+                break
+            if srv is None:
+                raise OSError(f"dist: none of the hub ports {ports} can be bound on {addr}")
+            srv.listen(world)
+            deadline = time.time() + timeout
+            peers = {}
+            try:
+                while len(peers) < world - 1:
+                    left = deadline - time.time()
+                    if left <= 0:
+                        raise TimeoutError(f"dist: {world - 1 - len(peers)} rank(s) did not join within {timeout} s")
+                    srv.settimeout(left)
+                    c, _ = srv.accept()
+                    c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                    c.settimeout(min(timeout, 10.0))
+                    try:
+                        msg = _recv(c)
+                        r = struct.unpack("<i", msg[-4:])[0] if len(msg) == len(hello) + 4 and msg[:-4] == hello \
+                            else -1
+                    except (ConnectionError, OSError):
+                        r = -1
+                    if not 1 <= r < world or r in peers:  # foreign, out of range or duplicate: not a peer
+                        c.close()
+                        continue
+                    _send(c, hello)  # ack: the peer knows it reached this rendezvous
+                    c.settimeout(timeout)
+                    peers[r] = c
+            except BaseException:
+                for c in peers.values():
+                    c.close()
+                raise
+            finally:
+                srv.close()
             self.peers = [peers[r] for r in range(1, world)]
         else:
             deadline = time.time() + timeout
+            k = 0
             while True:
+                p = ports[k % len(ports)]
+                k += 1
+                s = None
                 try:
-                    s = socket.create_connection((addr, port), timeout=10)
-                    break
-                except OSError:
-                    if time.time() > deadline:
-                        raise
+                    s = socket.create_connection((addr, p), timeout=5)
+                    s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                    s.settimeout(5)
+                    _send(s, hello + struct.pack("<i", rank))
+                    if _recv(s) == hello:
+                        break
+                    s.close()
+                except OSError:  # (ConnectionError, socket.timeout are OSErrors)
+                    if s is not None:
+                        s.close()
+                if time.time() > deadline:
+                    raise TimeoutError(f"dist: rank {rank} found no rendezvous on {addr}:{ports} within {timeout} s")
+                if k % len(ports) == 0:
                     time.sleep(0.2)
-            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             s.settimeout(timeout)
-            _send(s, struct.pack("<i", rank))
             self.sock = s
 
     def all_gather(self, obj):

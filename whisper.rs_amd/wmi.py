@@ -64,7 +64,8 @@ EXPORTS = (
     "wmi_decode_timestamps", "wmi_transcribe", "wmi_get_segment", "wmi_get_segment_tokens",
     "wmi_pcm_to_mel", "wmi_pcm_to_mel_batch", "wmi_encode", "wmi_decode_greedy", "wmi_decode_logits",
     "wmi_decode_beam", "wmi_full", "wmi_stage_pcm", "wmi_run_staged", "wmi_run_staged_beam", "wmi_get_tokens", "wmi_get_timings", "wmi_sync",
-    "wmi_get_mel", "wmi_get_checksums", "wmi_get_encoder_out", "wmi_get_cross_kv", "wmi_bench_kernel", "wmi_selftest", "wmi_debug_read",
+    "wmi_get_mel", "wmi_get_checksums", "wmi_get_encoder_out", "wmi_get_cross_kv", "wmi_bench_kernel", "wmi_decode_alg_bytes",
+    "wmi_selftest", "wmi_debug_read",
     "wmi_dist_id_size", "wmi_dist_make_id", "wmi_dist_init", "wmi_dist_gather_tokens", "wmi_dist_barrier",
 )
 
@@ -148,6 +149,8 @@ def lib():
         L.wmi_get_encoder_out.argtypes = [vp, C.c_int, vp, sz]
         L.wmi_get_cross_kv.argtypes = [vp, C.c_int, vp, vp, sz]
         L.wmi_bench_kernel.argtypes = [vp, C.c_int, C.c_int, C.POINTER(KernelBench)]
+        L.wmi_decode_alg_bytes.argtypes = [C.POINTER(Hparams), C.c_int, C.c_int, C.c_int, C.c_int,
+                                           C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.wmi_selftest.argtypes = [vp, C.POINTER(i32)]
         L.wmi_debug_read.argtypes = [vp, C.c_int, vp, C.c_size_t]
         L.wmi_get_checksums.argtypes = [vp, vp]
@@ -167,6 +170,15 @@ def _raise(rc: int, ctx=None):
     msg = (L.wmi_last_error(ctx) if ctx else L.wmi_last_error_global()) or b""
     cls = _ERRORS.get(rc, WsError)
     raise cls(f"{L.wmi_strerror(rc).decode()}: {msg.decode(errors='replace')}", rc)
+
+
+def decode_alg_bytes(hp: dict, rows: int, steps: int, beam: bool = False, q5: bool = False):
+    """(bytes, flops) of one decode (wmi_decode_alg_bytes: host-only, no device)."""
+    h = Hparams(**{n: int(hp.get(n, 1)) for n, _ in Hparams._fields_})
+    b, f = C.c_double(), C.c_double()
+    _raise(lib().wmi_decode_alg_bytes(C.byref(h), rows, steps, int(bool(beam)), int(bool(q5)), C.byref(b),
+                                      C.byref(f)))
+    return b.value, f.value
 
 
 def convert_integer_to_float_audio(samples) -> np.ndarray:
