@@ -39,6 +39,17 @@ if mode in ("all", "trace"):
     rows = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     path = synth.model_path(model)
     toks(path, {"WMI_PTRACE": "1"}, list(range(40, 40 + rows)), 130 if model != "large-v3" else 40)
+if mode == "beamtrace":
+    # beamtrace [model] [K] [n]: phase clocks of a beam search (one launch per
+    # step; phase A includes the launch gap and the beam kernels)
+    model = sys.argv[2] if len(sys.argv) > 2 else "large-v3"
+    K = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+    n = int(sys.argv[4]) if len(sys.argv) > 4 else 24
+    ctx = ctx_env(synth.model_path(model), {"WMI_PTRACE": "1"}, 1)
+    ctx.pcm_to_mel_batch([synth.synth_pcm_f32(30.0, 1234)])
+    ctx.encode(1, 0)
+    ctx.decode_beam(K, n, suppress_eot=True)
+    ctx.close()
 if mode in ("all", "rows"):
     path = synth.model_path("base")
     P, C = {"WMI_PERSIST": "1"}, {"WMI_PERSIST": "0", "WMI_NO_FUSE": "1"}

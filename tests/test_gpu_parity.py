@@ -413,19 +413,32 @@ def test_base_batch_of_8_equals_single(wmi, model_cache):
     """C4's per-GPU shard: 8 x 30 s clips through the batched encoder (M =
     12000 rows per GEMM) and the 8-row persistent decoder give the single-clip
     results (which the full-size test pins to the oracle): encoder output
-    bitwise, greedy ids equal (see test_batch_equals_single)."""
-    ctx = wmi.WhisperContext.new(synth.model_path("base", model_cache), 0, max_clips=8)
+    bitwise; greedy ids equal up to a near-tie of the one-row decoder
+    (BATCH_GAP).  The one-row instance sums its GEMV dots on the VALU, the
+    multi-row one on MFMA: where a clip's ids agree, the last step's logits of
+    the two are compared and their largest difference printed and bounded."""
+    ctx = _ctx_with_env(wmi, synth.model_path("base", model_cache), {"WMI_PERSIST_LOGITS": "1"}, max_clips=8)
     try:
+        V = ctx.hparams["n_vocab"]
         clips = [synth.synth_pcm_f32(30.0, 1234 + i) for i in range(8)]
         ctx.pcm_to_mel_batch(clips)
         ctx.encode(1, 0)
         enc_b = [ctx.encoder_out(i) for i in range(8)]
         tok_b = ctx.decode_greedy(12, suppress_eot=True)
-        for i in (0, 3, 7):
+        lg_b = np.frombuffer(ctx.debug_read(2, 8 * V * 4), np.float32).reshape(8, V).copy()
+        worst = 0.0
+        for i in range(8):
             ctx.pcm_to_mel_batch([clips[i]])
             ctx.encode(1, 0)
             np.testing.assert_array_equal(ctx.encoder_out(0), enc_b[i])
-            _ids_agree_to_near_tie(ctx, ctx.decode_greedy(12, suppress_eot=True)[0], tok_b[i])
+            single = ctx.decode_greedy(12, suppress_eot=True)[0]
+            if (single == tok_b[i]).all():
+                lg1 = np.frombuffer(ctx.debug_read(2, V * 4), np.float32)
+                worst = max(worst, float(np.abs(lg1 - lg_b[i]).max()))
+            else:
+                _ids_agree_to_near_tie(ctx, single, tok_b[i])
+        print(f"[batch scope] base: max |logit(B=1) - logit(B=8)| at the last step = {worst:.3g}")
+        assert worst <= BATCH_GAP
     finally:
         ctx.close()
 
@@ -453,6 +466,92 @@ def test_large_v3(wmi, model_cache):
     finally:
         ctx.close()
         om.close()
+
+
+# --- long decode horizons (round-4 verdict item 4) ----------------------------
+# The plain random models meet a top-2 near-tie within 7-12 steps, which caps
+# how far their ids can be compared.  The "-sharp" variants (synth.sharp_hook:
+# token embedding x 4, positional embedding x 100) keep every decision far
+# above f32 reordering noise, so the ids are compared over the whole horizon.
+@pytest.mark.slow
+def test_long_horizon_greedy_base_sharp(wmi, model_cache):
+    """base-sharp, 96 greedy tokens: one clip (the one-row instance) and 8
+    clips (C4's shard, the 8-row instance) against the oracle, id for id over
+    at least 64 decisive steps; teacher-forced argmax identical at every
+    decisive step."""
+    path = synth.model_path("base-sharp", model_cache)
+    om = pyoracle.OracleModel(path)
+    ctx = wmi.WhisperContext.new(path, 0, max_clips=8)
+    n_tok = 96
+    try:
+        n_dec, seed, _, _, ref = _greedy_case(ctx, om, range(1234, 1240), n_tok, 1500, 30.0, min_len=64)
+        seeds = [1234 + i for i in range(8)]
+        clips = [synth.synth_pcm_f32(30.0, sd) for sd in seeds]
+        ctx.pcm_to_mel_batch(clips)
+        ctx.encode(1, 0)
+        got8 = ctx.decode_greedy(n_tok, suppress_eot=True)
+        same = 0
+        for i, pcm in enumerate(clips):
+            mel = om.mel(pcm, n_threads=threads())
+            _, ck, cv = om.encode(mel, n_ctx=1500, n_threads=threads())
+            r, m = om.decode_greedy(ck, cv, n_tok, suppress_eot=True, n_threads=threads())
+            diff = np.nonzero(got8[i] != r)[0]
+            if diff.size:
+                assert m[diff[0]] < GREEDY_GAP, (i, int(diff[0]), float(m[diff[0]]))
+            same += int(diff[0]) if diff.size else n_tok
+            assert (m >= GREEDY_GAP).sum() >= 64
+        print(f"[long horizon] base-sharp: 1 clip {n_dec} decisive of {n_tok}; 8 clips: {same} of {8 * n_tok} "
+              f"ids identical to the oracle before any near-tie")
+        assert same >= 8 * 64
+    finally:
+        ctx.close()
+        om.close()
+
+
+@pytest.mark.slow
+def test_long_horizon_beam_large_v3_sharp(wmi, model_cache):
+    """large-v3-sharp, C5's search (5 beams, EOT suppressed) over 40 tokens:
+    the ids equal the oracle's, compared over at least 32 tokens."""
+    path = synth.model_path("large-v3-sharp", model_cache)
+    om = pyoracle.OracleModel(path)
+    ctx = wmi.WhisperContext.new(path, 0, max_clips=1)
+    try:
+        ref, score, got, got_score = _beam_case(ctx, om, range(1234, 1237), 5, 40, True, n_ctx=1500, secs=30.0,
+                                                fail=True, min_tok=32)
+        print(f"[long horizon] large-v3-sharp 5-beam ids compared over {len(ref)} tokens")
+        assert len(ref) >= 32
+        np.testing.assert_array_equal(got, ref)
+        assert abs(got_score - score) < 2e-2
+    finally:
+        ctx.close()
+        om.close()
+
+
+def test_multirow_instances_bitwise_independent_of_B(wmi, model_cache):
+    """The multi-row persistent instance (2 <= B <= 8 rows) gives every row the
+    same arithmetic whatever B is (MSet: one fixed MFMA / wave-order chain per
+    (weight row, decoder row); one partial per 128 keys in the cross softmax):
+    clips decoded as B = 2, 3 and 8 give bitwise the same ids and last-step
+    logits.  (B = 1 runs the VALU GEMVs: see test_batch_equals_single.)"""
+    path = synth.model_path("base", model_cache)
+    clips = [synth.synth_pcm_f32(30.0, 1234 + i) for i in range(8)]
+    V = None
+    res = {}
+    for nb in (8, 3, 2):
+        ctx = _ctx_with_env(wmi, path, {"WMI_PERSIST_LOGITS": "1"}, max_clips=nb)
+        try:
+            V = ctx.hparams["n_vocab"]
+            ctx.pcm_to_mel_batch(clips[:nb])
+            ctx.encode(1, 0)
+            toks = ctx.decode_greedy(24, suppress_eot=True)
+            lg = np.frombuffer(ctx.debug_read(2, nb * V * 4), np.float32).reshape(nb, V).copy()
+            res[nb] = (toks, lg)
+        finally:
+            ctx.close()
+    for nb in (3, 2):
+        for i in range(nb):
+            np.testing.assert_array_equal(res[nb][0][i], res[8][0][i])
+            np.testing.assert_array_equal(res[nb][1][i], res[8][1][i])
 
 
 @pytest.mark.slow
@@ -595,10 +694,20 @@ def test_persistent_matches_chain(wmi, model_cache, model, n_clips, n_ctx):
             ctx.close()
 
 
-def _ids_agree_to_near_tie(ctx, single, batched, gap=2e-3):
+# one-row (VALU GEMV) vs multi-row (MFMA GEMV) logits differ by up to ~1e-3
+# (1.04e-3 measured at base over 8 clips x 51865 logits; an f32 reordering
+# that flips one f16 rounding point inside a layer moves the logits by about
+# that much): ids may part only where the top-2 margin is below 2x that.
+# test_base_batch_of_8_equals_single measures and bounds it.
+BATCH_GAP = 2e-3
+
+
+def _ids_agree_to_near_tie(ctx, single, batched, gap=BATCH_GAP):
     """Greedy ids of clip 0 decoded alone vs in a batch: identical up to the
     first difference, which may only fall on a step whose top-2 margin (in
-    the one-row decoder's teacher-forced logits of the single run) is < gap."""
+    the one-row decoder's teacher-forced logits of the single run) is < gap,
+    the bound on the two instances' logit difference; nothing after the first
+    difference is compared (the histories differ from there)."""
     diff = np.nonzero(np.asarray(single) != np.asarray(batched))[0]
     if not diff.size:
         return

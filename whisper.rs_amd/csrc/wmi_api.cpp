@@ -1978,6 +1978,11 @@ int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_st
                     pa.kv_src_stride = hp.n_text_ctx;
                     pa.logits_out = ctx->dlogits;
                     pa.tokens_out = ctx->dtokens;  // (unused: no argmax in beam mode)
+                    // WMI_PTRACE: step s of clip 0 stamps slot s (its phase A
+                    // then includes the launch gap and the beam kernels)
+                    const int s_all = done_steps + i;
+                    if (ctx->d_ptrace && clip == 0 && s_all < hp.n_text_ctx)
+                        pa.ptrace = ctx->d_ptrace + (size_t)s_all * (hp.n_text_layer + 1) * 32 * 2;
                     HIPCHK(ctx, launch_dec_persist(ctx->stream, pa, G));
                     HIPCHK(ctx, launch_beam_step(ctx->stream, beam_args(ctx, np, suppress_eot)));
                 }
@@ -1986,6 +1991,10 @@ int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_st
                 if (rc) return rc;
             }
             done_steps += chunk;
+            if (G > 0 && ctx->d_ptrace && clip == 0 && done_steps >= total_steps) {
+                rc = ptrace_dump(ctx, std::min(total_steps, hp.n_text_ctx));
+                if (rc) return rc;
+            }
             if (early_stop && done_steps < total_steps) {
                 int32_t done = 0;
                 HIPCHK(ctx, hipMemcpyAsync(&done, &ctx->dbstate->done, 4, hipMemcpyDeviceToHost, ctx->stream));

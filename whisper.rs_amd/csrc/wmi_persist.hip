@@ -376,8 +376,17 @@ struct WSplit {
     static constexpr int CQ = (KCH + KS - 1) / KS;
     WChunk<Q5> w[CQ];
 };
-// rows per workgroup of an N-row GEMV at the full grid (PX_GMAX), even
-__host__ __device__ constexpr int rows_full(int N) { return (((N + PX_GMAX - 1) / PX_GMAX) + 1) & ~1; }
+// the grid the row partitions (and so the split-K factors of the GEMV
+// phases) are compiled for: min(CUs, PX_GDESIGN) workgroups.  A build with
+// -DWMI_GDESIGN=G (G <= PX_GMAX) runs a smaller grid (the grid-size sweep,
+// scripts/build_variant.sh)
+#ifndef WMI_GDESIGN
+#define WMI_GDESIGN PX_GMAX
+#endif
+constexpr int PX_GDESIGN = WMI_GDESIGN;
+static_assert(PX_GDESIGN >= 32 && PX_GDESIGN <= PX_GMAX, "design grid");
+// rows per workgroup of an N-row GEMV at the design grid, even
+__host__ __device__ constexpr int rows_full(int N) { return (((N + PX_GDESIGN - 1) / PX_GDESIGN) + 1) & ~1; }
 // the largest divisor of kch with rows * ks <= 16 (one pass of 16 quarters)
 __host__ __device__ constexpr int split_of(int kch, int rows) {
     int best = 1;
@@ -2237,7 +2246,7 @@ int grid_nsb(int device, int B, int V, int *nres) {
     const size_t base = persist_lds<NS, BT>(B), avail = LDS_CU - fa.sharedSizeBytes - 1024;
     if (base > avail) return 0;
     // resident vocabulary rows: as many of a workgroup's rows as the LDS holds
-    const int G0 = PX_GMAX, rpw = (V + G0 - 1) / G0;
+    const int G0 = PX_GDESIGN, rpw = (V + G0 - 1) / G0;
     int nr = (int)((avail - base) / (NS * 2));
     *nres = nr < rpw ? nr : rpw;
     const size_t lds = base + (size_t)*nres * NS * 2;
@@ -2254,7 +2263,7 @@ int grid_nsb(int device, int B, int V, int *nres) {
     // gives no such guarantee even at one workgroup per CU
     int coop = 0;
     if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess || !coop) return 0;
-    const int G = prop.multiProcessorCount < PX_GMAX ? prop.multiProcessorCount : PX_GMAX;
+    const int G = prop.multiProcessorCount < PX_GDESIGN ? prop.multiProcessorCount : PX_GDESIGN;
     if (per_cu * prop.multiProcessorCount < G) return 0;
     // row-partition limits of the register sets (see wset_dot users); the
     // split-K phases need the full grid's rows per workgroup

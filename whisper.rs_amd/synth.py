@@ -319,6 +319,24 @@ def write_ggml(path: str, model: str = "base", hp_override: dict | None = None,
     return hp
 
 
+SHARP_TE, SHARP_PE = 4.0, 100.0
+
+
+def sharp_hook(name: str, arr: np.ndarray) -> np.ndarray:
+    """The "-sharp" variants (e.g. "base-sharp"): decoder.token_embedding x 4
+    and decoder.positional_embedding x 100 (sigma 0.08 and 1.0).  The random
+    models' logits then spread widely and depend on the position, so greedy
+    decoding emits a long, varied id sequence whose top-2 margins stay far
+    above f32 reordering noise (base: ~95 distinct ids in 96 steps, smallest
+    margin ~8e-3; large-v3 5-beam: every selection margin >= 1e-2 over 40
+    steps) — a long decode horizon the parity tests can compare id for id."""
+    if name == "decoder.token_embedding.weight":
+        return (arr.astype(np.float32) * SHARP_TE).astype(arr.dtype)
+    if name == "decoder.positional_embedding":
+        return (arr.astype(np.float32) * SHARP_PE).astype(arr.dtype)
+    return arr
+
+
 def model_path(model: str, cache_dir: str | None = None) -> str:
     """Generate (once) and return the path of a synthetic model file."""
     cache_dir = cache_dir or os.environ.get("WMI_MODEL_CACHE", "/tmp/wmi_models")
@@ -326,7 +344,9 @@ def model_path(model: str, cache_dir: str | None = None) -> str:
     p = os.path.join(cache_dir, f"ggml-synth-{model}.bin")
     if not os.path.exists(p):
         base, _, quant = model.partition("-q")
-        if model.endswith("-f32"):  # e.g. "micro-f32": an ftype-0 (f32) file
+        if model.endswith("-sharp"):
+            write_ggml(p, model[:-6], tensor_hook=sharp_hook)
+        elif model.endswith("-f32"):  # e.g. "micro-f32": an ftype-0 (f32) file
             write_ggml(p, model[:-4], quant="f32")
         elif quant:  # e.g. "small-q5_1": the small model's weights in ggml q5_1
             write_ggml(p, base, quant="q" + quant)
