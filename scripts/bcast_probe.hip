@@ -52,6 +52,7 @@ __device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, uint32_t off, u32
 template <int LDF>
 __device__ __forceinline__ uint64_t ldf(const uint64_t *p) {
     if constexpr (LDF == 1) return __builtin_nontemporal_load(p);
+    else if constexpr (LDF >= 2) return *(const volatile uint64_t *)p;
     else return ld8(p);
 }
 template <int PU, int LDF = 0>
@@ -73,6 +74,7 @@ __device__ __forceinline__ bool gpoll(const uint64_t *g, int cnt, uint32_t tag, 
                     v[u] = ldf<LDF>(g + base + 256 * u);
                 }
             if (all) break;
+            if constexpr (LDF == 2) asm volatile("buffer_inv sc0" ::: "memory");
             if ((it & 63) == 63 && ld4(abortw)) return false;
             if (it > SPIN_MAX) { st4(abortw, 1u); return false; }
         }
@@ -160,6 +162,7 @@ __global__ __launch_bounds__(256, 1) void k_bcast(unsigned char *buf, uint32_t *
                 __syncthreads();
                 for (int i = p0 + t; i < p1; i += 256) xl[i] = ((uint64_t)tag << 32) | vec[i];
             }
+            if constexpr (LDF == 2) asm volatile("buffer_inv sc0" ::: "memory");
             if (!gpoll<PU, LDF>(xl, V, tag, vec, abortw)) bad = 1;
             if (bad) atomicOr(err, 1u);
         } else if constexpr (T == 0) {
@@ -315,12 +318,12 @@ int main(int argc, char **argv) {
                G, V, V * 4 / 1024.0, names[T], PU, NRLp, tm[0], tm[tm.size() / 2], herr[0], herr[1]);
         fflush(stdout);
     };
-    for (int V : {512, 2048, 6400, 12800, 25600}) {
+    for (int V : {2048, 12800, 25600}) {
         run(k_bcast<0, 16>, 0, 16, V, 256);
-        run(k_bcast<2, 16>, 2, 16, V, 256);
-        run(k_bcast<4, 16>, 4, 16, V, 256);
-        run(k_bcast<4, 4>, 4, 4, V, 256);
-        run(k_bcast<5, 16>, 5, 16, V, 256);
+        run(k_bcast<3, 16, 8, 0>, 3, 16, V, 256, 8);
+        run(k_bcast<3, 16, 8, 2>, 3, 16, V, 256, 82);
+        run(k_bcast<3, 16, 8, 3>, 3, 16, V, 256, 83);
+        run(k_bcast<3, 16, 32, 2>, 3, 16, V, 256, 322);
     }
     return 0;
 }

@@ -287,7 +287,13 @@ struct wmi_context {
     int enc_layers = 0;               // WMI_ENC_LAYERS (debug): run only the first encoder layers
     int fault_inject = 0;             // WMI_FAULT_INJECT=1 (test): the first persistent launch runs with one
                                       // workgroup missing (PersistArgs::stall_wg): the device abort path
-    bool persist_coop = true;         // WMI_COOP=0: plain launches of the persistent grid
+    // WMI_COOP=1: launch the persistent grid through hipLaunchCooperativeKernel
+    // (the runtime re-checks co-residency at every launch).  Off by default:
+    // it measured slower — base 1591/1598 vs 1574/1583 audio-s/s (one launch
+    // per decode: ~0.15 ms a launch), C5 116.5 vs 115.5 (one launch per beam
+    // step: ~17 us each), profiles/r04/coop_launch_ab.txt — and the grid is
+    // checked against the occupancy API at context creation instead (grid_nsb)
+    bool persist_coop = false;
     bool use_xshare = true;           // WMI_XSHARE=0: beam rows read the cross K / V per row
     int n_fallbacks = 0;              // decodes re-run on the kernel chain after a persistent exchange timeout
     PersistLayer *d_players = nullptr;

@@ -416,9 +416,25 @@ __device__ __forceinline__ void wsplit_load(WSplit<KCH, KS, Q5> &S, const WMat &
     }
 }
 
+// In-wave combine (KS = 2, or KS = 4 for epilogues that do not pair rows):
+// a row's KS quarters are quarters of ONE wave, so its partials are added
+// across lanes (permlane16 / permlane32 swaps) in ks order — bitwise the LDS
+// order — with no LDS round trip and no workgroup barrier.  The rows then sit
+// in the wave as wsplit_row says (KS = 2: wave w quarters 0 / 1 = rows 2w /
+// 2w + 1, adjacent for the pairing epilogues; KS = 4: wave w quarter 0 = row w).
+template <int KS, bool PAIR>
+constexpr bool wsplit_inwave() { return KS == 2 || (KS == 4 && !PAIR); }
+// this lane's row-local index after the in-wave combine, or -1
+template <int KS>
+__device__ __forceinline__ int wsplit_row(int w, int q) {
+    if constexpr (KS == 2) return q < 2 ? 2 * w + q : -1;
+    else return q == 0 ? w : -1;
+}
+
 // epi(row, b, v, bias, valid) as wset_dot's: called by every lane of the
-// first 16 / KS quarters, quarter q carrying row rb + q (lane l16: decoder row l16)
-template <int BT, int KCH, int KS, bool Q5, typename Epi>
+// first 16 / KS quarters, quarter q carrying row rb + q (lane l16: decoder row
+// l16); in-wave (wsplit_inwave): the quarters wsplit_row names
+template <int BT, int KCH, int KS, bool Q5, bool PAIR = true, typename Epi>
 __device__ __forceinline__ void wsplit_dot(const WSplit<KCH, KS, Q5> &S, const f16 *xs, int K, int B, int rb, int r1,
                                            int slot, int l16, float bias, float *kpart, Epi &&epi) {
     constexpr int CQ = WSplit<KCH, KS, Q5>::CQ;
@@ -440,6 +456,30 @@ __device__ __forceinline__ void wsplit_dot(const WSplit<KCH, KS, Q5> &S, const f
             const float t = red16_sum(acc[b]);
             if (l16 == b) v = t;
         }
+    if constexpr (wsplit_inwave<KS, PAIR>()) {
+        const int w = slot >> 2, q = slot & 3;
+        // (swap16: a0 = quarter 0 / 2's value in quarters 0-1 / 2-3, a1 =
+        // quarter 1 / 3's; swap32: c0 = quarter 0 / 1's value in both halves,
+        // c1 = quarter 2 / 3's)
+        uint32_t a0, a1, c0, c1;
+        swap16(__float_as_uint(v), a0, a1);
+        float sum;
+        if constexpr (KS == 2) {
+            sum = v + __uint_as_float(a1);          // quarters 0 / 2: p0 + p1 of rows 2w / 2w + 1
+            swap32(__float_as_uint(sum), c0, c1);   // quarter 0 <- quarter 2's sum (c1)
+            swap16(c1, a0, a1);                     // quarter 1 <- quarter 0's c1 (a0)
+            sum = q == 1 ? __uint_as_float(a0) : sum;
+        } else {
+            uint32_t d0, d1;
+            swap32(__float_as_uint(v), c0, c1);     // quarter 0 <- quarter 2 (p2)
+            swap32(a1, d0, d1);                     // quarter 0 <- quarter 2's a1 = p3
+            sum = ((v + __uint_as_float(a1)) + __uint_as_float(c1)) + __uint_as_float(d1);
+        }
+        const int rloc = wsplit_row<KS>(w, q);
+        const int row = rb + (rloc < 0 ? 0 : rloc);
+        epi(row, l16, sum, bias, rloc >= 0 && row < r1 && l16 < B);
+        return;
+    }
     if (l16 < PMAXB && rl < 16 / KS) kpart[(rl * KS + ks) * PMAXB + l16] = v;
     __syncthreads();
     const int row = rb + slot;
@@ -453,24 +493,26 @@ __device__ __forceinline__ void wsplit_dot(const WSplit<KCH, KS, Q5> &S, const f
 }
 
 // a phase's weight set: split-K (KS > 1) or one quarter-wave per row
-template <int KCH, int NP, int KS, bool Q5 = false>
+template <int KCH, int NP, int KS, bool Q5 = false, bool PAIR = true>
 struct GSet {
     WSplit<KCH, KS, Q5> s;
     float bias;
     __device__ __forceinline__ void load(const WMat &W, const float *b, int K, int rb, int r1, int slot, int l16) {
         wsplit_load(s, W, K, rb, r1, slot, l16);
         bias = 0.0f;
-        if (b && slot < 16 / KS && rb + slot < r1) bias = *glb(b + rb + slot);
+        // (the row this quarter carries into the epilogue)
+        const int rloc = wsplit_inwave<KS, PAIR>() ? wsplit_row<KS>(slot >> 2, slot & 3) : slot < 16 / KS ? slot : -1;
+        if (b && rloc >= 0 && rb + rloc < r1) bias = *glb(b + rb + rloc);
     }
     __device__ __forceinline__ void pre(int l16) { wsplit_pre(s, l16); }
     template <int BT, typename Epi>
     __device__ __forceinline__ void dot(const f16 *xs, int K, int B, int rb, int r1, int slot, int l16, float *kpart,
                                         Epi &&epi) const {
-        wsplit_dot<BT>(s, xs, K, B, rb, r1, slot, l16, bias, kpart, epi);
+        wsplit_dot<BT, KCH, KS, Q5, PAIR>(s, xs, K, B, rb, r1, slot, l16, bias, kpart, epi);
     }
 };
-template <int KCH, int NP, bool Q5>
-struct GSet<KCH, NP, 1, Q5> {
+template <int KCH, int NP, bool Q5, bool PAIR>
+struct GSet<KCH, NP, 1, Q5, PAIR> {
     WSet<KCH, NP, Q5> s;
     __device__ __forceinline__ void load(const WMat &W, const float *b, int K, int rb, int r1, int slot, int l16) {
         wset_load(s, W, b, K, rb, r1, slot, l16);
@@ -567,11 +609,12 @@ struct MSet {
 // its GEMV dots in different (each fixed) orders
 // (the K = 4n phase I above n = 512 reads its A fragments from LDS at each
 // MFMA step instead of holding all 4n / 128 of them in registers)
-template <int NS, int BT, int KCH, int NP, int KS, bool Q5>
+// PAIR: the phase's epilogue pairs adjacent rows (f16-pair outputs)
+template <int NS, int BT, int KCH, int NP, int KS, bool Q5, bool PAIR = true>
 using PSet = typename std::conditional<
     (BT > 1),
     typename std::conditional<(NS <= 512 || KCH <= NS / 128), MSet<KCH, NP, Q5>, MSet<KCH, NP, Q5, true>>::type,
-    GSet<KCH, NP, KS, Q5>>::type;
+    GSet<KCH, NP, KS, Q5, PAIR>>::type;
 
 // LayerNorm (ggml norm: double mean / variance, eps 1e-5; then * w + b) of
 // rows b < B of xf [B][NS] into xs [B][NS] f16 — wave w takes rows w, w + 4.
@@ -835,6 +878,9 @@ __device__ __forceinline__ float exp_f16_hash(float arg, const uint32_t *fbt, ui
 // compiler otherwise sinks them to their first use, after the poll, and the
 // whole load latency lands behind the seam.  Nothing waits here.
 #define PREFETCH_ISSUED asm volatile("" : : : "memory");
+// (the workgroup barrier in front of every poll stays even where no LDS
+// hazard needs it: without it the waves' polls spread out and the base step
+// took 142.5 vs 136.2 us, profiles/r04/prepoll_barrier_ab_REJECTED.txt)
 
 // BT: rows at compile time (1) or at most (8, runtime B); BEAM: beam-search
 // launches (self-attention history through kv_src; its index registers stay
@@ -1198,7 +1244,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 2);
-                PSet<NS, BT, KC, 1, KS_N, Q5> S;
+                PSet<NS, BT, KC, 1, KS_N, Q5, false> S;
                 const bool act = rn0 < rn1;
                 S.load(lmat<Q5>(P.wo, P.wo5, NS * NS), P.bo, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
@@ -1281,8 +1327,12 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                           (uint32_t *)qb, abortw, a.err);
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 20)
-                    for (int b = 0; b < B; ++b) {
-                        float m = -INFINITY;
+                    // (rows unrolled: their dot chains and max reductions interleave)
+                    float mb[PMAXB];
+#pragma unroll
+                    for (int b = 0; b < PMAXB; ++b) {
+                        mb[b] = -INFINITY;
+                        if (b >= B) continue;
 #pragma unroll
                         for (int p = 0; p < NKP; ++p)
                             if (j0 + 128 * p < j1) {
@@ -1294,12 +1344,16 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                 sv = xstep<XSum, 1>(sv);
                                 if (key < j1) {
                                     if ((tid & 1) == 0) st[b * CL + key - j0] = sv;
-                                    m = fmaxf(m, sv);
+                                    mb[b] = fmaxf(mb[b], sv);
                                 }
                             }
-                        m = wave_max(m);
-                        if (lane == 0) sh.redfb[b][w] = m;
                     }
+#pragma unroll
+                    for (int b = 0; b < PMAXB; ++b)
+                        if (b < B) {
+                            const float m = wave_max(mb[b]);
+                            if (lane == 0) sh.redfb[b][w] = m;
+                        }
                     __syncthreads();
                     if (tid < B)
                         gput(xg + oM + ((int64_t)tid * H + h) * nch + c, tag,
@@ -1513,13 +1567,16 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                           (uint32_t *)cmb, abortw, a.err);
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 21)
-                    for (int b = 0; b < B; ++b) {
+                    // wave w takes rows w, w + 4 (each row's keys in one wave:
+                    // no workgroup exchange); the double sum of f16 values in
+                    // [0, 1] is exact in any order, so it equals the per-row task's
+                    for (int b = w; b < B; b += 4) {
                         const float m = wave_max(cmb[b * nch + (lane < nch ? lane : 0)]);
                         double sum = 0.0;
 #pragma unroll
-                        for (int u = 0; u < NKP; ++u) {
-                            const int key = j0 + tid + 256 * u;
-                            if (256 * u < CL) {
+                        for (int u = 0; u < 4 * NKP; ++u) {
+                            const int key = j0 + lane + 64 * u;
+                            if (64 * u < CL) {
                                 const float sv = st[b * CL + (key < j1 ? key : j1 - 1) - j0];
                                 const float pj = exp_f16_hash(sv - m, sh.expfb, fbk);
                                 if (key < j1) {
@@ -1529,14 +1586,11 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                             }
                         }
                         sum = wave_sum(sum);
-                        if (lane == 0) sh.reddb[b][w] = sum;
-                    }
-                    __syncthreads();
-                    if (tid < B) {
-                        const double cs = ((sh.reddb[tid][0] + sh.reddb[tid][1]) + sh.reddb[tid][2]) + sh.reddb[tid][3];
-                        const int64_t tb = ((int64_t)tid * H + h) * nch + c;
-                        gput(xg + oS + 2 * tb, tag, lo32(cs));
-                        gput(xg + oS + 2 * tb + 1, tag, hi32(cs));
+                        if (lane == 0) {
+                            const int64_t tb = ((int64_t)b * H + h) * nch + c;
+                            gput(xg + oS + 2 * tb, tag, lo32(sum));
+                            gput(xg + oS + 2 * tb + 1, tag, hi32(sum));
+                        }
                     }
                 }
             } else
@@ -1587,9 +1641,11 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
 
             PSTAMP(l * 32 + 5)
             if (xsh) {  // beam rows sharing one clip (see E): V chunk read once, P.V per row
+                // (xshare launches use 128-key chunks: launch_dec_persist checks)
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 6);
                 uint32_t *csub = (uint32_t *)(scr + XS_OFF + XS_BYTES + 2048);  // [B][nch][2]
+                float *ob = (float *)(scr + XS_OFF + XS_BYTES + 6144);           // [B][4 waves][64]
                 const int ntask = H * nch;
                 for (int t = wg, k = 0; t < ntask; t += G) {
                     const int c = t % nch, h = t / nch;
@@ -1597,16 +1653,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     const float *st = (const float *)(scr + XS_OFF) + (k++) * (B * CL);
                     const int doct = tid & 7, jg = tid >> 3;
                     const f16 *Vb = (const f16 *)a.cv + ((int64_t)l * a.Bt + a.b0) * T * NS + h * 64 + doct * 8;
-                    half8 vf[NKP][4];
-                    const half8 z8 = {};
+                    half8 vf[4];
 #pragma unroll
-                    for (int p = 0; p < NKP; ++p)
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            int key = j0 + 128 * p + jg * 4 + u;
-                            key = key < j1 ? key : j1 - 1;
-                            vf[p][u] = 128 * p < CL ? sld((const half8 *)(Vb + (int64_t)key * NS)) : z8;
-                        }
+                    for (int u = 0; u < 4; ++u) {
+                        int key = j0 + jg * 4 + u;
+                        key = key < j1 ? key : j1 - 1;
+                        vf[u] = sld((const half8 *)(Vb + (int64_t)key * NS));
+                    }
                     PREFETCH_ISSUED
                     __syncthreads();
                     const bool ok = gpoll(B * 2 * nch, ptag(pos, L, l, 5),
@@ -1617,49 +1670,52 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                           csub, abortw, a.err);
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 22)
-                    const int nsp = (j1 - j0 + 127) >> 7;
-                    for (int b = 0; b < B; ++b) {
+                    // lane b < B: row b's exp sum over its chunks (exact in any
+                    // order) -> 1 / sum, read by every lane with readlane
+                    float invl = 0.0f;
+                    if (lane < B) {
                         double tot = 0.0;
-                        for (int i = 0; i < nch; ++i) tot += mk64(csub[(b * nch + i) * 2 + 1], csub[(b * nch + i) * 2]);
-                        const float inv = (float)(1.0 / tot);
-                        float o[NKP][8];
+                        for (int i = 0; i < nch; ++i) tot += mk64(csub[(lane * nch + i) * 2 + 1], csub[(lane * nch + i) * 2]);
+                        invl = (float)(1.0 / tot);
+                    }
+                    // every row's P.V partial at once (each row's keys and
+                    // dims in the per-row task's order), one exchange
+                    float o[PMAXB][8];
 #pragma unroll
-                        for (int p = 0; p < NKP; ++p)
+                    for (int b = 0; b < PMAXB; ++b) {
 #pragma unroll
-                            for (int e = 0; e < 8; ++e) o[p][e] = 0.0f;
+                        for (int e = 0; e < 8; ++e) o[b][e] = 0.0f;
+                        if (b >= B) continue;
+                        const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(invl), b));
+                        float sp[4];
 #pragma unroll
-                        for (int p = 0; p < NKP; ++p)
-                            if (j0 + 128 * p < j1) {
-                                float sp[4];
+                        for (int u = 0; u < 4; ++u) {
+                            const int key = j0 + jg * 4 + u;
+                            sp[u] = st[b * CL + (key < j1 ? key : j1 - 1) - j0];
+                        }
 #pragma unroll
-                                for (int u = 0; u < 4; ++u) {
-                                    const int key = j0 + 128 * p + jg * 4 + u;
-                                    sp[u] = st[b * CL + (key < j1 ? key : j1 - 1) - j0];
-                                }
+                        for (int u = 0; u < 4; ++u) {
+                            const int key = j0 + jg * 4 + u;
+                            const float pj = key < j1 ? h2f_bits(f2h_bits(sp[u] * inv)) : 0.0f;
 #pragma unroll
-                                for (int u = 0; u < 4; ++u) {
-                                    const int key = j0 + 128 * p + jg * 4 + u;
-                                    const float pj = key < j1 ? h2f_bits(f2h_bits(sp[u] * inv)) : 0.0f;
+                            for (int e = 0; e < 8; ++e) o[b][e] = o[b][e] + pj * (float)vf[u][e];
+                        }
+                    }
 #pragma unroll
-                                    for (int e = 0; e < 8; ++e) o[p][e] = o[p][e] + pj * (float)vf[p][u][e];
-                                }
-                            }
+                    for (int b = 0; b < PMAXB; ++b)
+                        if (b < B) {
 #pragma unroll
-                        for (int p = 0; p < NKP; ++p)
-                            if (j0 + 128 * p < j1)
+                            for (int e = 0; e < 8; ++e) o[b][e] = red_8_16_32(o[b][e]);
+                            if (lane < 8)
 #pragma unroll
-                                for (int e = 0; e < 8; ++e) o[p][e] = red_8_16_32(o[p][e]);
-                        if (lane < 8)
-#pragma unroll
-                            for (int p = 0; p < NKP; ++p)
-                                if (j0 + 128 * p < j1)
-#pragma unroll
-                                    for (int e = 0; e < 8; ++e) sh.ored[w][p * 64 + lane * 8 + e] = o[p][e];
-                        __syncthreads();
-                        if (tid < 64 * nsp)
-                            gput(xg + oP + (((int64_t)b * H + h) * nsub + (j0 >> 7)) * 64 + tid, tag,
-                                 __float_as_uint(((sh.ored[0][tid] + sh.ored[1][tid]) + sh.ored[2][tid]) + sh.ored[3][tid]));
-                        __syncthreads();
+                                for (int e = 0; e < 8; ++e) ob[(b * 4 + w) * 64 + lane * 8 + e] = o[b][e];
+                        }
+                    __syncthreads();
+                    for (int i = tid; i < B * 64; i += PT) {
+                        const int b = i >> 6, d = i & 63;
+                        const float* q4 = ob + b * 256 + d;
+                        gput(xg + oP + (((int64_t)b * H + h) * nsub + (j0 >> 7)) * 64 + d, tag,
+                             __float_as_uint(((q4[0] + q4[64]) + q4[128]) + q4[192]));
                     }
                 }
             } else
@@ -1778,7 +1834,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 8);
-                PSet<NS, BT, KC, 1, KS_N, Q5> S;
+                PSet<NS, BT, KC, 1, KS_N, Q5, false> S;
                 const bool act = rn0 < rn1;
                 S.load(lmat<Q5>(P.wco, P.wco5, NS * NS), P.bco, NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
@@ -1838,7 +1894,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 10);
-                PSet<NS, BT, 4 * KC, 1, KS_I, Q5> S;
+                PSet<NS, BT, 4 * KC, 1, KS_I, Q5, false> S;
                 const bool act = rn0 < rn1;
                 S.load(lmat<Q5>(P.w1, P.w15, 4 * NS * NS), P.b1, 4 * NS, rn0, rn1, slot, l16);
                 PREFETCH_ISSUED
@@ -2351,7 +2407,7 @@ hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G) {
         a.cl > 128 * NKP || (int64_t)a.nch * a.cl < a.T || (int64_t)a.B * (a.n / 64) * a.nch > PX_TASKS ||
         a.tctx > 512 || a.cl % 128 || (a.beam && a.n_steps != 1) || (a.kv_src && a.kv_src_stride < a.tctx) ||
         ((int64_t)a.B * (a.n / 64) * a.nch + G - 1) / G * a.cl * 4 > XS_BYTES ||  // task scores in LDS
-        (a.xshare && (!a.beam || a.n <= 768 || ((int64_t)(a.n / 64) * a.nch + G - 1) / G * a.B * a.cl * 4 > XS_BYTES ||
+        (a.xshare && (!a.beam || a.n <= 768 || a.cl != 128 || ((int64_t)(a.n / 64) * a.nch + G - 1) / G * a.B * a.cl * 4 > XS_BYTES ||
                       a.B * a.nch * 4 > 2048 || a.B * a.nch * 8 > 4096)))
         return hipErrorInvalidValue;
     switch (a.n) {
