@@ -1184,6 +1184,8 @@ int run_encode(wmi_context *ctx, int mel_offset) {
     g.M = B * T2; g.N = n; g.K = 3 * ctx->Cp1;
     g.conv = 1; g.conv_stride = 1; g.conv_tin = T2; g.conv_cp = ctx->Cp1; g.conv_tout = T2;
     g.out16 = ctx->g1; g.ldo = n; g.gelu_tab = ctx->gelu_tab; g.T = T2;
+    g.tune = &ctx->tune;
+
     HIPCHK(ctx, launch_gemm(s, EPI_CONV1, g));
     // conv2 + bias + GELU + positional embedding (main.rs:1856-1875)
     g = GemmArgs{};
@@ -1191,6 +1193,8 @@ int run_encode(wmi_context *ctx, int mel_offset) {
     g.M = B * T; g.N = n; g.K = 3 * n;
     g.conv = 1; g.conv_stride = 2; g.conv_tin = T2; g.conv_cp = n; g.conv_tout = T;
     g.out32 = ctx->h; g.ldo = n; g.gelu_tab = ctx->gelu_tab; g.pe = ctx->e_pe; g.T = T;
+    g.tune = &ctx->tune;
+
     HIPCHK(ctx, launch_gemm(s, EPI_CONV2PE, g));
     const int M = B * T;
     for (int l = 0; l < ctx->enc_layers; ++l) {
@@ -1200,6 +1204,8 @@ int run_encode(wmi_context *ctx, int mel_offset) {
         g.A = ctx->xln; g.lda = n; g.B = e.wqkv; g.bias = e.bqkv; g.M = M; g.N = 3 * n; g.K = n;
         g.A32 = ctx->xln32; g.B32 = W32(e.wqkv);
         g.q = ctx->q; g.k = ctx->k; g.vt = ctx->vt; g.T = T; g.Tp = Tp; g.n_state = n;
+        g.tune = &ctx->tune;
+
         HIPCHK(ctx, launch_gemm(s, EPI_QKV, g));
         AttnArgs at{}; at.tune = &ctx->tune;
         at.q = ctx->q; at.k = ctx->k; at.vt = ctx->vt; at.out = ctx->att; at.out32 = ctx->att32; at.exp_tab = ctx->exp_tab;
@@ -1210,16 +1216,22 @@ int run_encode(wmi_context *ctx, int mel_offset) {
         g.A = ctx->att; g.lda = n; g.B = e.wo; g.bias = e.bo; g.M = M; g.N = n; g.K = n;
         g.A32 = ctx->att32; g.B32 = W32(e.wo);
         g.out32 = ctx->h; g.ldo = n;
+        g.tune = &ctx->tune;
+
         HIPCHK(ctx, launch_gemm(s, EPI_RESID, g));
         HIPCHK(ctx, launch_layernorm(s, ctx->h, M, n, e.ln2_w, e.ln2_b, f32 ? nullptr : ctx->xln, ctx->xln32));
         g = GemmArgs{};
         g.A = ctx->xln; g.lda = n; g.B = e.w0; g.bias = e.b0; g.M = M; g.N = 4 * n; g.K = n;
         g.A32 = ctx->xln32; g.B32 = W32(e.w0);
         g.out16 = ctx->hid; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
+        g.tune = &ctx->tune;
+
         HIPCHK(ctx, launch_gemm(s, EPI_GELU16, g));
         g = GemmArgs{};
         g.A = ctx->hid; g.lda = 4 * n; g.B = e.w1; g.bias = e.b1; g.M = M; g.N = n; g.K = 4 * n; g.B32 = W32(e.w1);
         g.out32 = ctx->h; g.ldo = n;
+        g.tune = &ctx->tune;
+
         HIPCHK(ctx, launch_gemm(s, EPI_RESID, g));
     }
     // ln_post (main.rs:1977-1986)
@@ -1231,6 +1243,8 @@ int run_encode(wmi_context *ctx, int mel_offset) {
     if (f32) { g.A32 = ctx->enc32; g.B32 = W32(ctx->wckv); }
     g.ck = ctx->ck; g.cv = ctx->cv; g.T = T; g.n_state = nt; g.n_clips = B;
     g.kscale = powf((float)n / (float)H, -0.25f);  // main.rs:1994
+    g.tune = &ctx->tune;
+
     HIPCHK(ctx, launch_gemm(s, EPI_CROSSKV, g));
     ctx->enc_T = T;
     ctx->enc_clips = B;
@@ -2177,6 +2191,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     knob("WMI_XATTN_ROWS", tn.xattn_rows, 0);
     knob("WMI_SELF_SPLIT", tn.self_split, 0);
     knob("WMI_ENC_ATTN_NW", tn.enc_attn_nw, 0);
+    knob("WMI_GEMM_G", tn.gemm_g, 0);
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_trace, TRACE_SLOTS * 16 + 64 * 16 * 8));
@@ -2649,6 +2664,8 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
             const EncLayerDev &e = ctx->enc[0];
             g.A = ctx->xln; g.lda = n; g.B = e.w0; g.bias = e.b0; g.M = M; g.N = 4 * n; g.K = n;
             g.out16 = ctx->hid; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
+            g.tune = &ctx->tune;
+
             HIPCHK(ctx, launch_gemm(s, EPI_GELU16, g));
         } else if (which == 2) {
             AttnArgs at{}; at.tune = &ctx->tune;
@@ -2662,6 +2679,8 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
             g.N = hp.n_text_layer * 2 * hp.n_text_state; g.K = n;
             g.ck = ctx->ck; g.cv = ctx->cv; g.T = T; g.n_state = hp.n_text_state; g.n_clips = B;
             g.kscale = powf((float)n / (float)hp.n_audio_head, -0.25f);
+            g.tune = &ctx->tune;
+
             HIPCHK(ctx, launch_gemm(s, EPI_CROSSKV, g));
         } else if (which == 14) {
             // the persistent greedy decoder over the staged clips, exactly as

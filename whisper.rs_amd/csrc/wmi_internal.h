@@ -67,11 +67,13 @@ struct Tune {
     int self_split = 1;     // WMI_SELF_SPLIT: self-attention output projection over n / 128 WGs per head
     int graph_steps = 8;    // WMI_GRAPH_STEPS: chain decoder steps per captured graph
     int enc_attn_nw = 0;    // WMI_ENC_ATTN_NW: 32-query blocks (two waves each) per k_attn_enc4 workgroup (0 auto, 1, 2, 4)
+    int gemm_g = 1;         // WMI_GEMM_G: large-M encoder GEMMs on k_gemm_g (LDS-DMA staging); 0: k_gemm
 };
 extern const Tune kTuneDefault;
 inline const Tune &tune_of(const Tune *t) { return t ? *t : kTuneDefault; }
 
 struct GemmArgs {
+    const Tune *tune;   // context knobs (null: defaults)
     const uint16_t *A;  // plain: [M][lda]; conv: X[b][Tin + 2][Cp]
     const uint16_t *B;  // [N][K]
     const float *bias;  // [N] or null

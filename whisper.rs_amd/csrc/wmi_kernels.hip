@@ -453,6 +453,155 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
         }
 }
 
+// ---- large-M GEMM (the 8-clip encoder shapes): a 128 x 128 tile per
+// 256-thread workgroup (2 x 2 waves of 64 x 64, v_mfma_f32_32x32x16_f16),
+// k staged 64 at a time by global_load_lds (16 bytes a lane, no register
+// staging) into a lane-linear LDS image.  A wave-instruction's 1 KB covers 8
+// rows of 64 k (128-byte rows); the image's 16-byte chunk c of row r holds the
+// row's logical chunk c ^ ((r >> 1) & 7) — the swizzle is applied to the
+// per-lane SOURCE address (the DMA destination must stay lane-linear) and
+// undone on the read, so a fragment read's 32 rows fall on 16 distinct slots
+// of each 256-byte bank row in every 16-lane group (conflict-free
+// ds_read_b128).  Two LDS stages: the next tile's DMA is issued before this
+// tile's fragment reads and MFMAs, then one vmcnt(0) + barrier per tile.
+// The MFMA and the k order (16 at a time, ascending) are k_gemm's, so every
+// output is bitwise k_gemm's.
+__device__ __forceinline__ int gg_chunk(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+template <int EPI, bool CONV>
+__global__ __launch_bounds__(256) void k_gemm_g(GemmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];  // [2][A 128 x 64 | B 128 x 64] f16
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int nbm = (a.M + 127) / 128, nbn = (a.N + 127) / 128;
+    const int nwg = nbm * nbn;
+    int bid = blockIdx.x;
+    {  // XCD-aware bijective tile order (as k_gemm)
+        const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+    }
+    const int bn = bid % nbn, bm = bid / nbn;
+    const int m0 = bm * 128, n0 = bn * 128;
+    const int nk = a.K / 64;
+    // this lane's DMA rows: wave w, instruction j fills image bytes
+    // (4 w + j) KB + 16 lane = row (4 w + j) * 8 + lane / 8, chunk lane % 8
+    // (rows past M / N read the last row: their outputs are never stored)
+    const uint16_t *srcA[4], *srcB[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = (wave * 4 + j) * 8 + (lane >> 3), lc = gg_chunk(row, lane & 7);
+        const int m = m0 + row < a.M ? m0 + row : a.M - 1, n = n0 + row < a.N ? n0 + row : a.N - 1;
+        if constexpr (CONV) {
+            const int b = m / a.conv_tout, t = m - b * a.conv_tout;
+            srcA[j] = a.A + ((int64_t)b * (a.conv_tin + 2) + (int64_t)t * a.conv_stride) * a.conv_cp + lc * 8;
+        } else {
+            srcA[j] = a.A + (int64_t)m * a.lda + lc * 8;
+        }
+        srcB[j] = a.B + (int64_t)n * a.K + lc * 8;
+    }
+    typedef __attribute__((address_space(3))) void lds_t;
+    auto stage = [&](int buf, int kt) {
+        unsigned char *As = gsm + buf * 32768, *Bs = As + 16384;
+        // implicit-GEMM conv: k = tap * Cp + c, a tap's channels contiguous (Cp % 64 == 0)
+        int64_t ka = (int64_t)kt * 64;
+        if constexpr (CONV) {
+            const int tap = (kt * 64) / a.conv_cp, c = kt * 64 - tap * a.conv_cp;
+            ka = (int64_t)tap * a.conv_cp + c;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            __builtin_amdgcn_global_load_lds((const void *)(srcA[j] + ka), (lds_t *)(As + (wave * 4 + j) * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *)(srcB[j] + (int64_t)kt * 64), (lds_t *)(Bs + (wave * 4 + j) * 1024),
+                                             16, 0, 0);
+        }
+    };
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    const int lr = lane & 31, lh = lane >> 5;
+    // (three stages with two tiles in flight, a counted vmcnt and a raw
+    // s_barrier — 96 KB, one workgroup per CU — measured slower: 8-clip
+    // encoder 3.72 vs 3.00 ms, profiles/r04/gemm_g_ab.txt)
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) stage(buf ^ 1, kt + 1);
+        const unsigned char *As = gsm + buf * 32768, *Bs = As + 16384;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int c = 2 * ks + lh;
+            half8 af[2], bf[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int r = wm * 64 + i * 32 + lr;
+                af[i] = *(const half8 *)(As + r * 128 + gg_chunk(r, c) * 16);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int r = wn * 64 + j * 32 + lr;
+                bf[j] = *(const half8 *)(Bs + r * 128 + gg_chunk(r, c) * 16);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    // epilogue as k_gemm's: lane holds column n, rows (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = n0 + wn * 64 + j * 32 + lr;
+            const int mb = m0 + wm * 64 + i * 32 + 4 * lh;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                gemm_epi4<EPI>(a, mb + 8 * g, n, v);
+            }
+        }
+}
+
+template <bool CONV>
+static hipError_t gemm_g_dispatch(hipStream_t s, int epi, const GemmArgs &a) {
+    const int nwg = ((a.M + 127) / 128) * ((a.N + 127) / 128);
+    constexpr size_t lds = 65536;
+#define GEMMG_CASE(E)                                                                        \
+    case E: {                                                                               \
+        hipError_t e = allow_lds(k_gemm_g<E, CONV>, lds);                              \
+        if (e != hipSuccess) return e;                                                      \
+        hipLaunchKernelGGL((k_gemm_g<E, CONV>), dim3(nwg), dim3(256), lds, s, a);      \
+        break;                                                                              \
+    }
+    if constexpr (CONV) {
+        switch (epi) {
+            GEMMG_CASE(EPI_CONV1)
+            GEMMG_CASE(EPI_CONV2PE)
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (epi) {
+            GEMMG_CASE(EPI_F32)
+            GEMMG_CASE(EPI_RESID)
+            GEMMG_CASE(EPI_GELU16)
+            GEMMG_CASE(EPI_QKV)
+            GEMMG_CASE(EPI_CROSSKV)
+            default: return hipErrorInvalidValue;
+        }
+    }
+#undef GEMMG_CASE
+    return hipGetLastError();
+}
+
 template <int BM, int BN, int BK, bool CONV>
 static hipError_t gemm_dispatch_epi(hipStream_t s, int epi, const GemmArgs &a) {
     const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -491,6 +640,11 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a) {
     // k per stage: 64 for the smaller tiles when it divides K (and, for the
     // implicit-GEMM conv, a tap's channel block); LDS stays <= 64 KB
     const bool k64 = (a.conv ? a.conv_cp : a.K) % 64 == 0;
+    // large M: the LDS-DMA kernel (bitwise the same outputs)
+    // (8-clip encoder 3.10 -> 3.00 ms: conv2 84.6 -> 71.3, Wo 39.7 -> 34.8,
+    // mlp.2 77.0 -> 60.2 us; QKV and mlp.0 unchanged)
+    if (t128 >= 240 && tune_of(a.tune).gemm_g && a.K % 64 == 0 && (!a.conv || a.conv_cp % 64 == 0))
+        return a.conv ? gemm_g_dispatch<true>(s, epi, a) : gemm_g_dispatch<false>(s, epi, a);
     if (a.conv) {
         if (t128 >= 240) return gemm_dispatch_epi<128, 128, GBK, true>(s, epi, a);
         if (t12864 >= 240) return k64 ? gemm_dispatch_epi<128, 64, 64, true>(s, epi, a)
