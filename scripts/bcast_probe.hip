@@ -23,6 +23,11 @@
 //                 acquire after its flag poll and every thread reads the payload
 //                 with PLAIN 16-B loads (L2-served for the XCD's other CUs)
 //   T5 rel+acq   : as T4 with plain producer stores + an agent release fence
+//   T6 counter8  : T2's dense 16-byte sc1 payload, but one agent atomic add per
+//                 producer onto ONE of 8 counters (b % 8, each on its own
+//                 line); the consumer's lanes 0-7 poll the 8 counters (sc1),
+//                 a barrier, then every thread reads the payload (16-B sc1)
+//   T7 granule8+sleep: T0 with s_sleep 1 before every re-poll of a granule set
 // Every value is checked (word i of round r carries i * 3 + r).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -119,6 +124,12 @@ __global__ __launch_bounds__(256, 1) void k_bcast(unsigned char *buf, uint32_t *
                 const int e = b * per + i;
                 if (e < V) st8(g + e, ((uint64_t)tag << 32) | (uint32_t)(e * 3 + r));
             }
+        } else if constexpr (T == 7) {
+            uint64_t *g = (uint64_t *)(buf + ob);
+            for (int i = t; i < per; i += 256) {
+                const int e = b * per + i;
+                if (e < V) st8(g + e, ((uint64_t)tag << 32) | (uint32_t)(e * 3 + r));
+            }
         } else if constexpr (T == 1) {
             for (int i = t; i < (per + 2) / 3; i += 256) {
                 u32x4 v;
@@ -149,7 +160,8 @@ __global__ __launch_bounds__(256, 1) void k_bcast(unsigned char *buf, uint32_t *
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
-                st4(flags + b, tag);
+                if constexpr (T == 6) __hip_atomic_fetch_add(flags + 3072 + 32 * (b & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else st4(flags + b, tag);
             }
         }
         // ---- gather the whole vector of round r ----
@@ -165,7 +177,7 @@ __global__ __launch_bounds__(256, 1) void k_bcast(unsigned char *buf, uint32_t *
             if constexpr (LDF == 2) asm volatile("buffer_inv sc0" ::: "memory");
             if (!gpoll<PU, LDF>(xl, V, tag, vec, abortw)) bad = 1;
             if (bad) atomicOr(err, 1u);
-        } else if constexpr (T == 0) {
+        } else if constexpr (T == 0 || T == 7) {
             const uint64_t *g = (const uint64_t *)(buf + ob);
             for (int base = t; base < V; base += 256 * PU) {
                 uint64_t v[PU];
@@ -184,6 +196,7 @@ __global__ __launch_bounds__(256, 1) void k_bcast(unsigned char *buf, uint32_t *
                         }
                     if (all) break;
                     if (it > SPIN_MAX) { bad = 1; atomicOr(err, 1u); break; }
+                    if constexpr (T == 7) __builtin_amdgcn_s_sleep(1);
                 }
 #pragma unroll
                 for (int u = 0; u < PU; ++u) {
@@ -224,7 +237,13 @@ __global__ __launch_bounds__(256, 1) void k_bcast(unsigned char *buf, uint32_t *
                 }
             }
         } else {
-            if (w == 0) {  // poll the G flags, 4 per lane
+            if (T == 6 && w == 0) {  // lanes 0-7 poll the 8 counters: G / 8 arrivals per round each
+                for (uint32_t it = 0;; ++it) {
+                    const bool ok = lane >= 8 || ld4(flags + 3072 + 32 * lane) >= (uint32_t)(G / 8) * (uint32_t)r;
+                    if (__all(ok)) break;
+                    if (it > SPIN_MAX) { bad = 1; atomicOr(err, 1u); break; }
+                }
+            } else if (w == 0) {  // poll the G flags, 4 per lane
                 for (uint32_t it = 0;; ++it) {
                     bool all = true;
                     for (int f = 4 * lane; f < G; f += 256) {  // G % 4 == 0
@@ -234,7 +253,7 @@ __global__ __launch_bounds__(256, 1) void k_bcast(unsigned char *buf, uint32_t *
                     if (__all(all)) break;
                     if (it > SPIN_MAX) { bad = 1; atomicOr(err, 1u); break; }
                 }
-                if constexpr (T >= 4) {
+                if constexpr (T == 4 || T == 5) {
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
@@ -246,7 +265,7 @@ __global__ __launch_bounds__(256, 1) void k_bcast(unsigned char *buf, uint32_t *
 #pragma unroll
                 for (int u = 0; u < PU; ++u) {
                     const int i = base + 256 * u;
-                    if constexpr (T >= 4) v[u] = i < NQ ? *(const u32x4 *)(buf + ob + 16ll * i) : u32x4{0u, 0u, 0u, 0u};
+                    if constexpr (T == 4 || T == 5) v[u] = i < NQ ? *(const u32x4 *)(buf + ob + 16ll * i) : u32x4{0u, 0u, 0u, 0u};
                     else v[u] = i < NQ ? ld16(rs, (uint32_t)(ob + 16ll * i)) : u32x4{0u, 0u, 0u, 0u};
                 }
 #pragma unroll
@@ -290,7 +309,7 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char *names[] = {"granule8", "granule16", "flag+payload", "relay", "flag+acq", "rel+acq"};
+    const char *names[] = {"granule8", "granule16", "flag+payload", "relay", "flag+acq", "rel+acq", "counter8", "granule8+sleep"};
     auto run = [&](auto kern, int T, int PU, int V, int G, int NRLp = 0) {
         std::vector<float> tm;
         uint32_t herr[2] = {0, 0};
@@ -318,12 +337,12 @@ int main(int argc, char **argv) {
                G, V, V * 4 / 1024.0, names[T], PU, NRLp, tm[0], tm[tm.size() / 2], herr[0], herr[1]);
         fflush(stdout);
     };
-    for (int V : {2048, 12800, 25600}) {
+    for (int V : {2048, 6400, 12800, 25600}) {
         run(k_bcast<0, 16>, 0, 16, V, 256);
-        run(k_bcast<3, 16, 8, 0>, 3, 16, V, 256, 8);
-        run(k_bcast<3, 16, 8, 2>, 3, 16, V, 256, 82);
-        run(k_bcast<3, 16, 8, 3>, 3, 16, V, 256, 83);
-        run(k_bcast<3, 16, 32, 2>, 3, 16, V, 256, 322);
+        run(k_bcast<7, 16>, 7, 16, V, 256);
+        run(k_bcast<2, 16>, 2, 16, V, 256);
+        run(k_bcast<6, 16>, 6, 16, V, 256);
+        run(k_bcast<6, 4>, 6, 4, V, 256);
     }
     return 0;
 }

@@ -554,6 +554,31 @@ def test_multirow_instances_bitwise_independent_of_B(wmi, model_cache):
             np.testing.assert_array_equal(res[nb][1][i], res[8][1][i])
 
 
+def test_split_grid_equals_full_grid(wmi, model_cache):
+    """A block of 8 clips decodes as two concurrent half-grid launches (rows
+    0-3 and 4-7 on 128 workgroups each, two streams, separate exchange blocks,
+    cache rows and argmax carries): bitwise the ids and every step's logits
+    of the one full-grid launch (WMI_SPLIT_ROWS=0) — the row partition of the
+    multi-row phases changes which workgroup computes a dot, not its order."""
+    path = synth.model_path("base", model_cache)
+    clips = [synth.synth_pcm_f32(30.0, 1300 + i) for i in range(8)]
+    res = []
+    for env in ({"WMI_SPLIT_ROWS": "8"}, {"WMI_SPLIT_ROWS": "0"}):
+        ctx = _ctx_with_env(wmi, path, dict(env, WMI_PERSIST_LOGITS="1"), max_clips=8)
+        try:
+            V = ctx.hparams["n_vocab"]
+            ctx.pcm_to_mel_batch(clips)
+            ctx.encode(1, 0)
+            toks = ctx.decode_greedy(40, suppress_eot=True)
+            lg = np.frombuffer(ctx.debug_read(2, 8 * V * 4), np.float32).reshape(8, V).copy()
+            res.append((toks, lg))
+        finally:
+            ctx.close()
+    for i in range(8):
+        np.testing.assert_array_equal(res[0][0][i], res[1][0][i])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
 @pytest.mark.slow
 def test_beam_shared_cross_equals_per_row(wmi, model_cache):
     """C5's beam rows read their clip's cross K / V through one task per (head,

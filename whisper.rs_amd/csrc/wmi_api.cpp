@@ -295,6 +295,15 @@ struct wmi_context {
     // checked against the occupancy API at context creation instead (grid_nsb)
     bool persist_coop = false;
     bool use_xshare = true;           // WMI_XSHARE=0: beam rows read the cross K / V per row
+    // greedy blocks of at least split_rows clips decode as two concurrent
+    // half-grid launches (rows [0, B/2) and [B/2, B), each on half the CUs, a
+    // second stream): a workgroup's all-to-all gathers carry half the rows
+    // (WMI_SPLIT_ROWS; 0 = never)
+    int split_rows = 8;
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    uint64_t *d_xg2 = nullptr;        // the second launch's exchange block, state
+    DecState *dstate2 = nullptr;
     int n_fallbacks = 0;              // decodes re-run on the kernel chain after a persistent exchange timeout
     PersistLayer *d_players = nullptr;
     uint32_t *d_expfb = nullptr;       // exp fallback list of the persistent decoder [64] + count
@@ -999,6 +1008,8 @@ int alloc_workspace(wmi_context *ctx) {
     const size_t o_st = A.take(sizeof(DecState));
     const XLayout xl = persist_layout((int)nt, (int)Hd, (int)T);
     const size_t o_xg = A.take((size_t)xl.total * 8);
+    const size_t o_xg2 = A.take((size_t)xl.total * 8);
+    const size_t o_st2 = A.take(sizeof(DecState));
     const size_t o_ct = A.take(8 * 4);
     const size_t o_ptrs = A.take(B * sizeof(float *));
     const size_t o_ns = A.take(B * 8);
@@ -1057,12 +1068,17 @@ int alloc_workspace(wmi_context *ctx) {
     ctx->dstate = (DecState *)(b + o_st);
     ctx->d_xg = (uint64_t *)(b + o_xg);
     ctx->xg_bytes = (size_t)xl.total * 8;
+    ctx->d_xg2 = (uint64_t *)(b + o_xg2);
+    ctx->dstate2 = (DecState *)(b + o_st2);
     ctx->d_curtok = (int32_t *)(b + o_ct);
     ctx->d_pcm_ptrs = (float **)(b + o_ptrs);
     ctx->d_nsamp = (int64_t *)(b + o_ns);
     ctx->d_nlen = (int64_t *)(b + o_nl);
     ctx->d_melmax = (uint32_t *)(b + o_mm);
     for (int i = 0; i < 8; ++i) HIPCHK(ctx, hipEventCreate(&ctx->ev[i]));
+    HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
     return WMI_OK;
 }
 
@@ -1694,6 +1710,21 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     return a;
 }
 
+// the second half-grid launch of a split block (rows B1.. of the block): its
+// own exchange block and step state, self-attention cache rows B1.., argmax
+// carry and logits rows B1..; every workgroup owns twice the vocabulary rows
+// of the full grid, so as many of them stay resident as the LDS holds
+void split_second(wmi_context *ctx, PersistArgs &p1, int B1, int Gh) {
+    const size_t row = (size_t)ctx->hp.n_text_ctx * ctx->hp.n_text_state;
+    p1.xg = ctx->d_xg2;
+    p1.st = ctx->dstate2;
+    p1.kcache = ctx->kcache + B1 * row;
+    p1.vcache = ctx->vcache + B1 * row;
+    p1.cur_tok = ctx->d_curtok + B1;
+    if (p1.logits_out) p1.logits_out += (size_t)B1 * ctx->hp.n_vocab;
+    p1.nres = (ctx->hp.n_vocab + Gh - 1) / Gh;
+}
+
 // greedy decode of every encoded clip; tokens stay in ctx->dtokens
 // ([enc_clips][n_gen]); returns after enqueueing (no sync) unless early stop.
 int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, std::vector<int32_t> *host_tokens,
@@ -1721,12 +1752,32 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
         HIPCHK(ctx, hipMemsetAsync(ctx->dsync, 0, ctx->sync_bytes, ctx->stream));
         const int total_steps = np + n_gen - 1;
         const int G = persist_grid_for(ctx, B);
+        const int B1 = B / 2, Gh = G > 0 && ctx->split_rows > 1 && B >= ctx->split_rows
+                                       ? persist_split_grid(ctx->hp.n_text_state, G) : 0;
         if (G > 0) HIPCHK(ctx, hipMemsetAsync(ctx->d_xg, 0, ctx->xg_bytes, ctx->stream));
+        if (Gh > 0) {
+            HIPCHK(ctx, hipMemsetAsync(ctx->d_xg2, 0, ctx->xg_bytes, ctx->stream));
+            HIPCHK(ctx, hipMemsetAsync(ctx->dstate2, 0, sizeof(DecState), ctx->stream));
+        }
         int done_steps = 0;
         while (done_steps < total_steps) {
             int chunk = total_steps - done_steps;
             if (early_stop && chunk > 32) chunk = 32;
-            if (G > 0) {  // persistent decoder: the chunk's steps in one launch
+            if (Gh > 0) {  // two half-grid launches, rows [b0, b0 + B1) and [b0 + B1, b0 + B)
+                PersistArgs p0 = persist_args(ctx, b0, B1, Gh, np, np, suppress_eot, n_gen);
+                PersistArgs p1 = persist_args(ctx, b0 + B1, B - B1, Gh, np, np, suppress_eot, n_gen);
+                split_second(ctx, p1, B1, Gh);
+                p0.nres = p1.nres;
+                p0.n_steps = p1.n_steps = chunk;
+                if (ctx->d_ptrace && done_steps == 0 && b0 == 0) p0.ptrace = ctx->d_ptrace;
+                HIPCHK(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
+                HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+                HIPCHK(ctx, launch_dec_persist(ctx->stream, p0, Gh));
+                HIPCHK(ctx, launch_dec_persist(ctx->stream2, p1, Gh));
+                HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
+                HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+                rc = p0.ptrace ? ptrace_dump(ctx, chunk) : 0;
+            } else if (G > 0) {  // persistent decoder: the chunk's steps in one launch
                 PersistArgs pa = persist_args(ctx, b0, B, G, np, np, suppress_eot, n_gen);
                 pa.n_steps = chunk;
                 if (ctx->d_ptrace && done_steps == 0 && b0 == 0) pa.ptrace = ctx->d_ptrace;
@@ -2165,6 +2216,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (const char *c = getenv("WMI_FAULT_INJECT")) ctx->fault_inject = atoi(c) ? 1 : 0;
     if (const char *c = getenv("WMI_COOP")) ctx->persist_coop = atoi(c) != 0;
     if (const char *c = getenv("WMI_XSHARE")) ctx->use_xshare = atoi(c) != 0;
+    if (const char *c = getenv("WMI_SPLIT_ROWS")) ctx->split_rows = atoi(c);
     ctx->dec_layers = ctx->hp.n_text_layer;
     if (const char *c = getenv("WMI_DEC_LAYERS")) ctx->dec_layers = std::max(1, std::min(atoi(c), ctx->hp.n_text_layer));
     ctx->enc_layers = ctx->hp.n_audio_layer;
@@ -2222,6 +2274,9 @@ void wmi_free(wmi_context *ctx) {
     if (ctx->d_ptrace) (void)hipFree(ctx->d_ptrace);
     for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     delete ctx;
 }
 

@@ -385,5 +385,8 @@ hipError_t launch_persist_selftest(hipStream_t s, const uint16_t *exp_tab, int n
 // largest co-resident grid for the model (0: not supported for this n / B / T)
 // and the vocabulary rows per workgroup that fit in LDS beside the phases' data
 int persist_grid(int device, int n, int B, int T, int V, int *nres);
+// workgroups of each of two concurrent multi-row launches sharing the
+// device's G-workgroup grid (0: the rows per workgroup would not fit)
+int persist_split_grid(int n, int G);
 
 }  // namespace wmi

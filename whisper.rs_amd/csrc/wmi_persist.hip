@@ -2402,6 +2402,15 @@ int persist_grid(int device, int n, int B, int T, int V, int *nres) {
     }
 }
 
+int persist_split_grid(int n, int G) {
+    // the multi-row instances (MFMA GEMVs: no split-K factors tied to the
+    // design grid) at half the grid: every phase's rows per workgroup within
+    // the register sets' limits (grid_nsb)
+    const int Gh = G / 2;
+    if (Gh < 32 || (3 * n + Gh - 1) / Gh > 31 || (4 * n + Gh - 1) / Gh > 31 || (n + Gh - 1) / Gh > RNMAX - 1) return 0;
+    return Gh;
+}
+
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G) {
     if (G < 1 || G > PX_GMAX || a.B < 1 || a.B > PMAXB || a.T > 2048 || a.nch < 1 || a.nch > 64 ||
         a.cl > 128 * NKP || (int64_t)a.nch * a.cl < a.T || (int64_t)a.B * (a.n / 64) * a.nch > PX_TASKS ||
