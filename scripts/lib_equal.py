@@ -1,6 +1,6 @@
 """Bitwise comparison of two builds of the library (scripts/build_variant.sh)
-on the persistent decoder: greedy ids and last-step logits of base (1 clip
-and 8 clips) and micro.  Usage: lib_equal.py LIB_A LIB_B (run on the gpurun box)."""
+on the encoder output and the persistent decoder: greedy ids and last-step
+logits of base (1 clip and 8 clips), micro and small.  Usage: lib_equal.py LIB_A LIB_B (run on the gpurun box)."""
 import os
 import subprocess
 import sys
@@ -22,6 +22,7 @@ def run_one(out):
         ctx.set_audio_ctx(ctx_n)
         ctx.pcm_to_mel_batch([synth.synth_pcm_f32(secs, 1234 + i) for i in range(nc)])
         ctx.encode(1, 0)
+        res[f"{model}_{nc}_enc"] = np.stack([ctx.encoder_out(i) for i in range(nc)])
         toks = np.stack(ctx.decode_greedy(48, suppress_eot=True))
         V = ctx.hparams["n_vocab"]
         lg = np.frombuffer(ctx.debug_read(2, nc * V * 4), np.float32).copy()

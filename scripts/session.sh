@@ -12,7 +12,7 @@
 #   trace=MODEL:ROWS   decoder phase trace (WMI_PTRACE) of a greedy run: TAG_trace_MODEL_ROWS.log
 #   prof               rocprofv3 kernel-trace summary of the base bench: TAG_prof/
 #   pmc=MODEL:CLIPS    FETCH_SIZE / WRITE_SIZE passes of the persistent decoder (kernel 14): TAG_pmc_MODEL_CLIPS*
-#   ab=ENV1/ENV2/...   bench (base, 1 clip, 10 steps) alternating environments, e.g. ab=WMI_COOP=1/WMI_COOP=0
+#   ab=ENV1,ENV2,...   bench (base, 1 clip, 10 steps) alternating environments, e.g. ab=WMI_COOP=1,WMI_COOP=0
 #                      (MODEL, CPG, BEAM in the environment select another config): TAG_ab.txt
 # Replaces the one-off drivers of rounds 1-3 (their evidence is under profiles/).
 set -o pipefail
@@ -62,7 +62,7 @@ import json; d=json.load(open('${O}_bench.json')); print('bench', d['value'], d[
       unset WMI_NO_GRAPH
       cat ${O}_pmc_${m}_${c}_trace.log ;;
     ab)
-      IFS=/ read -ra envs <<< "$arg"
+      IFS=, read -ra envs <<< "$arg"
       for rep in 1 2; do
         for e in "${envs[@]}"; do
           timeout -k 10 300 env $e python3 bench.py --model ${MODEL:-base} --beam ${BEAM:-0} --clips-per-gpu ${CPG:-1} \

@@ -688,7 +688,9 @@ typedef uint32_t a4vec __attribute__((ext_vector_type(4)));
 // Sweep 0 keeps the max of the raw scores (scale > 0 and rounding are
 // monotone, so fl(max_raw * scale) is the max of the scaled scores); sweeps
 // 1 and 2 clamp the table index to n_exp, where the table holds a 0 (no
-// compare / select per element); scale and subtract run as packed f32 pairs.
+// compare / select per element); scale and subtract run as packed f32 pairs,
+// as m - S: fl(m - S) = -fl(S - m), so its f16 bits are the table index
+// f16(|S - m|) with no mask (m is never -0: the caller adds +0).
 typedef float f2v __attribute__((ext_vector_type(2)));
 template <int PASS, bool TAIL>
 __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, const f16 *Vb, int key0, int kb,
@@ -718,13 +720,11 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
             for (int r = 0; r < 16; r += 2) {
                 f2v v = {sc[r], sc[r + 1]};
                 v = v * scale2;
-                v = v - m2;
+                v = m2 - v;  // >= +0
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     const int key = key0 + kb * 32 + ((r + u) & 3) + 8 * ((r + u) >> 2) + 4 * lh;
-                    // f16(|v|) = the magnitude bits of f16(v) (v <= 0): the abs is a
-                    // free source modifier of the conversion
-                    uint32_t i = f2h_bits(fabsf(v[u]));
+                    uint32_t i = f2h_bits(v[u]);
                     i = i < n_exp ? i : n_exp;  // v_min: index n_exp holds 0
                     if (TAIL) i = key < T ? i : n_exp;
                     const float e = h2f_bits(tab[i]);  // unguarded read (a guarded one branches per element)
@@ -757,7 +757,9 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
 // other LDS buffer after the compute) and tile kt + 2's loads are in flight
 // into the other, so a load has two tiles of compute to land (the loop is
 // unrolled by two so the register sets are named statically; every load is
-// unconditional from a clamped tile, so no undef phi reaches scratch).
+// unconditional from a clamped tile, so no undef phi reaches scratch).  The
+// partial last tile runs after the loop: a full / tail branch inside it made
+// the compiler copy both MFMA accumulators every iteration (32 v_mov a tile).
 template <int NW, int PASS>
 __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, const f16 *Vt, f16 *Ks, f16 *Vs,
                                             const uint16_t *tab, const half8 (&qf)[4], float &mx, double &sum,
@@ -794,22 +796,24 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
     ATT4_SSTORE(0, kA, vA)
     ATT4_GLOAD(1, kB, vB)  // (kB, vB): the next tile, loop-carried
     __syncthreads();
-    for (int kt = 0; kt < ntiles; ++kt) {
+    const int nfull = a.T / AT4_KT;
+    for (int kt = 0; kt < nfull; ++kt) {
         const int buf = kt & 1;
         a4vec kF[SCH], vF[VCH];  // tile kt + 2, requested before this tile's compute
         ATT4_GLOAD(kt + 2, kF, vF)
-        if (kt * AT4_KT + AT4_KT <= a.T)
-            attn4_tile<PASS, false>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * AT4_KT * AT4_LD, kt * AT4_KT, kb, tab, qf,
-                                    mx, sum, m, inv, o0, o1);
-        else
-            attn4_tile<PASS, true>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * AT4_KT * AT4_LD, kt * AT4_KT, kb, tab, qf,
-                                   mx, sum, m, inv, o0, o1);
+        attn4_tile<PASS, false>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * AT4_KT * AT4_LD, kt * AT4_KT, kb, tab, qf,
+                                mx, sum, m, inv, o0, o1);
         ATT4_SSTORE(buf ^ 1, kB, vB)  // (after the last tile: unread)
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < SCH; ++i) kB[i] = kF[i];
 #pragma unroll
         for (int i = 0; i < VCH; ++i) vB[i] = vF[i];
+    }
+    if (nfull < ntiles) {  // the partial tile (stored by the last iteration)
+        attn4_tile<PASS, true>(a, Ks + (nfull & 1) * AT4_KT * AT4_LD, Vs + (nfull & 1) * AT4_KT * AT4_LD, nfull * AT4_KT, kb,
+                               tab, qf, mx, sum, m, inv, o0, o1);
+        __syncthreads();  // (callers reuse the tile buffers: as after every loop tile)
     }
 #undef ATT4_GLOAD
 #undef ATT4_SSTORE
@@ -859,7 +863,7 @@ __global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     xm[w * 64 + lane] = mx;
     __syncthreads();
-    const float m = fmaxf(mx, xm[partner * 64 + lane]) * a.scale;  // max of the raw scores, scaled once
+    const float m = fmaxf(mx, xm[partner * 64 + lane]) * a.scale + 0.0f;  // max of the raw scores, scaled once (never -0)
     attn4_sweep<NW, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
     sum = sum + __shfl_xor(sum, 32);
     xd[w * 64 + lane] = sum;
