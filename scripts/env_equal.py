@@ -53,6 +53,9 @@ if __name__ == "__main__":
         same = np.array_equal(outs[0][k], outs[1][k])
         if not same:
             print(k, f"DIFFER (max |d| {np.abs(outs[0][k].astype(np.float64) - outs[1][k]).max():.3g})")
+            d = np.argwhere(outs[0][k] != outs[1][k])
+            print(f"   {len(d)} of {outs[0][k].size} differ; first at {d[:4].tolist()}: "
+                  f"{[outs[0][k][tuple(i)] for i in d[:4]]} vs {[outs[1][k][tuple(i)] for i in d[:4]]}")
         bad += not same
     print("ENV_EQUAL", "OK" if not bad else f"{bad} of {len(outs[0].files)} differ", f"({len(outs[0].files)} arrays)")
     sys.exit(1 if bad else 0)

@@ -23,6 +23,10 @@ def run_one(out):
         ctx.pcm_to_mel_batch([synth.synth_pcm_f32(secs, 1234 + i) for i in range(nc)])
         ctx.encode(1, 0)
         res[f"{model}_{nc}_enc"] = np.stack([ctx.encoder_out(i) for i in range(nc)])
+        for i in range(nc):
+            k, v = ctx.cross_kv(i)
+            res[f"{model}_{nc}_ck{i}"] = k
+            res[f"{model}_{nc}_cv{i}"] = v
         toks = np.stack(ctx.decode_greedy(48, suppress_eot=True))
         V = ctx.hparams["n_vocab"]
         lg = np.frombuffer(ctx.debug_read(2, nc * V * 4), np.float32).copy()
@@ -46,6 +50,10 @@ if __name__ == "__main__":
     for k in outs[0].files:
         same = np.array_equal(outs[0][k], outs[1][k])
         print(k, "bitwise equal" if same else f"DIFFER (max |d| {np.abs(outs[0][k].astype(np.float64) - outs[1][k]).max():.3g})")
+        if not same:
+            d = np.argwhere(outs[0][k] != outs[1][k])
+            print(f"   {len(d)} of {outs[0][k].size} differ; first at {d[:4].tolist()}: "
+                  f"{[outs[0][k][tuple(i)] for i in d[:4]]} vs {[outs[1][k][tuple(i)] for i in d[:4]]}")
         bad += not same
     print("LIB_EQUAL", "OK" if not bad else f"{bad} differ")
     sys.exit(1 if bad else 0)

@@ -2244,6 +2244,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     knob("WMI_SELF_SPLIT", tn.self_split, 0);
     knob("WMI_ENC_ATTN_NW", tn.enc_attn_nw, 0);
     knob("WMI_GEMM_G", tn.gemm_g, 0);
+    knob("WMI_GEMM_EPI", tn.epi_staged, 0);
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_trace, TRACE_SLOTS * 16 + 64 * 16 * 8));

@@ -17,7 +17,15 @@ typedef f16 half2v __attribute__((ext_vector_type(2)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint16_t f2h_bits(float x) { return __builtin_bit_cast(uint16_t, (f16)x); }
+// f32 -> f16 of an f32 value, rounded once more (ggml's order: the f32
+// result first, then the f16 store).  The backend otherwise folds
+// fptrunc(fmul / fadd x, y) into v_fma_mixlo_f16, ONE rounding of the exact
+// product / sum — 1-ulp differences in ~1e-4 of the outputs (cross K, the
+// decoder's q and P16), whatever -ffp-contract says.  A canonicalize between
+// the two blocks the fold and costs no instruction (an empty asm there did
+// the same but slowed the decoder's F phase 0.4 us a layer).
+__device__ __forceinline__ f16 f16_rt(float x) { return (f16)__builtin_canonicalizef(x); }
+__device__ __forceinline__ uint16_t f2h_bits(float x) { return __builtin_bit_cast(uint16_t, f16_rt(x)); }
 __device__ __forceinline__ float h2f_bits(uint16_t b) { return (float)__builtin_bit_cast(f16, b); }
 // order-preserving map of f32 onto u32 (argmax keys)
 __device__ __forceinline__ uint32_t ord_f32(float v) {

@@ -32,7 +32,7 @@ __device__ __forceinline__ void gemm_epi4(const GemmArgs &a, int m, int n, const
             if (m + 3 < a.M && t0 + 3 < a.T && (t0 & 3) == 0) {
                 half4 hv;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) hv[r] = (f16)(v[r] + bias);
+                for (int r = 0; r < 4; ++r) hv[r] = f16_rt(v[r] + bias);
                 *(half4 *)(a.vt + (((int64_t)b0 * H + h) * 64 + d) * a.Tp + t0) = hv;
             } else {
 #pragma unroll

@@ -68,6 +68,7 @@ struct Tune {
     int graph_steps = 8;    // WMI_GRAPH_STEPS: chain decoder steps per captured graph
     int enc_attn_nw = 0;    // WMI_ENC_ATTN_NW: 32-query blocks (two waves each) per k_attn_enc4 workgroup (0 auto, 1, 2, 4)
     int gemm_g = 1;         // WMI_GEMM_G: large-M encoder GEMMs on k_gemm_g (LDS-DMA staging); 0: k_gemm
+    int epi_staged = 1;     // WMI_GEMM_EPI: GEMM epilogues through LDS, 16 / 8-byte stores (0: per-lane 2 / 4-byte stores)
 };
 extern const Tune kTuneDefault;
 inline const Tune &tune_of(const Tune *t) { return t ? *t : kTuneDefault; }
@@ -97,6 +98,7 @@ struct GemmArgs {
     // B32 = f32 weights [N][K] selects the f32 MFMA GEMM (wmi_f32.hip); its
     // A operand is A32 (f32) when set, else A (f16: GELU-table outputs, exact)
     const float *A32, *B32;
+    int epi_staged;     // set by launch_gemm from the context's knob (Tune::epi_staged)
 };
 hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a);
 hipError_t launch_gemm32(hipStream_t s, int epi, const GemmArgs &a);  // wmi_f32.hip

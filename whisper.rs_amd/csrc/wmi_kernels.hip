@@ -299,7 +299,7 @@ __device__ __forceinline__ void layernorm_wave(const float *x, int n, const floa
             }
             if (y16) {
                 half4 hv;
-                hv[0] = (f16)o[0]; hv[1] = (f16)o[1]; hv[2] = (f16)o[2]; hv[3] = (f16)o[3];
+                hv[0] = f16_rt(o[0]); hv[1] = f16_rt(o[1]); hv[2] = f16_rt(o[2]); hv[3] = f16_rt(o[3]);
                 *(half4 *)(y16 + e) = hv;
             }
             if (y32) *(float4 *)(y32 + e) = make_float4(o[0], o[1], o[2], o[3]);
@@ -347,6 +347,147 @@ __device__ __forceinline__ uint4 gemm_load_a(const GemmArgs &a, int m, int k) {
 }
 
 
+// ---- LDS-staged GEMM epilogue -------------------------------------------
+// The MFMA accumulators leave a lane as one column n and rows spaced 1, 8 and
+// 4 apart: stored straight from them (gemm_epi4) every store is 2 or 4 bytes
+// wide and a wave-instruction touches 2 rows x 64-128 bytes — the 8-clip
+// encoder GEMMs spent more than half their time there (mlp.0 69.6 vs 30.5 us
+// without the stores, cross K/V 212 vs 93).  Here the workgroup's BM x BN f32
+// tile goes through LDS (row-major, or column-major for the V^T tiles of the
+// QKV projection, whose output runs along m) and every thread then finishes
+// 4 consecutive outputs at a time: one 16-byte (f32) or 8-byte (f16) store,
+// consecutive threads on consecutive addresses.  The arithmetic per output
+// is gemm_epi4's, so the results are bitwise the same.  Needs N % 4 == 0 and
+// the caller's LDS free (after the k loop's last barrier).
+template <int BM, int BN>
+constexpr size_t epi_stage_bytes() {
+    return (size_t)4 * (BM * (BN + 4) > BN * (BM + 4) ? BM * (BN + 4) : BN * (BM + 4));
+}
+
+// the staged path's shape conditions (workgroup-uniform)
+template <int EPI, int BN>
+__device__ __forceinline__ bool epi_staged_ok(const GemmArgs &a) {
+    return a.epi_staged && a.N % 4 == 0 && a.ldo % 4 == 0 && (EPI != EPI_QKV || a.n_state % BN == 0);
+}
+
+template <int EPI, int BM, int BN>
+__device__ __forceinline__ void gemm_epi_staged(const GemmArgs &a, const floatx16 (&acc)[BM / 64][BN / 64], float *stg,
+                                                int m0, int n0) {
+    constexpr int TM = BM / 64, TN = BN / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+    const int lr = lane & 31, lh = lane >> 5;
+    // the QKV projection's V^T tiles (n in [2 ns, 3 ns): whole tiles, ns % BN == 0)
+    const bool tr = EPI == EPI_QKV && n0 >= 2 * a.n_state;
+    if (!tr) {
+        constexpr int LS = BN + 4;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = wm * (BM / 2) + i * 32 + 4 * lh + 8 * (r >> 2) + (r & 3);
+                    stg[row * LS + wn * (BN / 2) + j * 32 + lr] = acc[i][j][r];
+                }
+    } else {
+        constexpr int LS = BM + 4;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int col = wn * (BN / 2) + j * 32 + lr, row = wm * (BM / 2) + i * 32 + 4 * lh + 8 * g;
+                    *(float4 *)(stg + col * LS + row) =
+                        make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+                }
+    }
+    __syncthreads();
+    if (tr) {  // 4 consecutive rows m of one column n -> vt[b][h][d][t .. t + 3]
+        constexpr int LS = BM + 4, CPC = BM / 4;
+        const int ns = a.n_state, H = ns >> 6;
+        for (int c = tid; c < BN * CPC; c += 256) {
+            const int nn = c / CPC, m = m0 + 4 * (c - nn * CPC), n = n0 + nn;
+            if (n >= a.N || m >= a.M) continue;
+            const float4 v = *(const float4 *)(stg + nn * LS + 4 * (c - nn * CPC));
+            const float bias = a.bias ? a.bias[n] : 0.0f;
+            const int cc = n - 2 * ns, h = cc >> 6, d = cc & 63;
+            const int b0 = m / a.T, t0 = m - b0 * a.T;
+            const float vv[4] = {v.x, v.y, v.z, v.w};
+            if (m + 3 < a.M && t0 + 3 < a.T && (t0 & 3) == 0) {
+                half4 hv;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) hv[r] = f16_rt(vv[r] + bias);
+                *(half4 *)(a.vt + (((int64_t)b0 * H + h) * 64 + d) * a.Tp + t0) = hv;
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int mm = m + r;
+                    if (mm >= a.M) break;
+                    const int b = mm / a.T, t = mm - b * a.T;
+                    a.vt[(((int64_t)b * H + h) * 64 + d) * a.Tp + t] = f2h_bits(vv[r] + bias);
+                }
+            }
+        }
+        return;
+    }
+    constexpr int LS = BN + 4, CPR = BN / 4;
+    for (int c = tid; c < BM * CPR; c += 256) {
+        const int row = c / CPR, n = n0 + 4 * (c - row * CPR), m = m0 + row;
+        if (n >= a.N || m >= a.M) continue;
+        const float4 v = *(const float4 *)(stg + row * LS + 4 * (c - row * CPR));
+        float4 bs = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (EPI != EPI_CROSSKV && a.bias) bs = *(const float4 *)(a.bias + n);
+        const float x[4] = {v.x + bs.x, v.y + bs.y, v.z + bs.z, v.w + bs.w};
+        if constexpr (EPI == EPI_F32) {
+            *(float4 *)(a.out32 + (int64_t)m * a.ldo + n) = make_float4(x[0], x[1], x[2], x[3]);
+        } else if constexpr (EPI == EPI_RESID) {
+            float4 *p = (float4 *)(a.out32 + (int64_t)m * a.ldo + n);
+            const float4 o = *p;
+            *p = make_float4(x[0] + o.x, x[1] + o.y, x[2] + o.z, x[3] + o.w);
+        } else if constexpr (EPI == EPI_GELU16 || EPI == EPI_CONV1) {
+            ushort4 g;
+            g.x = a.gelu_tab[f2h_bits(x[0])];
+            g.y = a.gelu_tab[f2h_bits(x[1])];
+            g.z = a.gelu_tab[f2h_bits(x[2])];
+            g.w = a.gelu_tab[f2h_bits(x[3])];
+            int64_t o = (int64_t)m * a.ldo + n;
+            if constexpr (EPI == EPI_CONV1) {
+                const int b = m / a.T, t = m - b * a.T;
+                o = ((int64_t)b * (a.T + 2) + t + 1) * a.ldo + n;
+            }
+            *(ushort4 *)(a.out16 + o) = g;
+        } else if constexpr (EPI == EPI_CONV2PE) {
+            const int t = m - (m / a.T) * a.T;
+            const float4 pe = *(const float4 *)(a.pe + (int64_t)t * a.ldo + n);
+            *(float4 *)(a.out32 + (int64_t)m * a.ldo + n) =
+                make_float4(pe.x + gelu_lookup(a.gelu_tab, x[0]), pe.y + gelu_lookup(a.gelu_tab, x[1]),
+                            pe.z + gelu_lookup(a.gelu_tab, x[2]), pe.w + gelu_lookup(a.gelu_tab, x[3]));
+        } else if constexpr (EPI == EPI_CROSSKV) {
+            const int ns = a.n_state, l = n / (2 * ns), rr = n - l * 2 * ns;
+            const int b = m / a.T, t = m - b * a.T;
+            const int64_t base = (((int64_t)l * a.n_clips + b) * a.T + t) * ns;
+            ushort4 h;
+            if (rr < ns) {
+                h.x = f2h_bits(v.x * a.kscale); h.y = f2h_bits(v.y * a.kscale);
+                h.z = f2h_bits(v.z * a.kscale); h.w = f2h_bits(v.w * a.kscale);
+                *(ushort4 *)(a.ck + base + rr) = h;
+            } else {
+                const float4 bv = a.bias ? *(const float4 *)(a.bias + n) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                h.x = f2h_bits(v.x + bv.x); h.y = f2h_bits(v.y + bv.y);
+                h.z = f2h_bits(v.z + bv.z); h.w = f2h_bits(v.w + bv.w);
+                *(ushort4 *)(a.cv + base + rr - ns) = h;
+            }
+        } else if constexpr (EPI == EPI_QKV) {  // q / k tiles: [b][h][Tp][64]
+            const int ns = a.n_state, H = ns >> 6, which = n / ns, cc = n - which * ns, h = cc >> 6, d = cc & 63;
+            const int b = m / a.T, t = m - b * a.T;
+            ushort4 hv;
+            hv.x = f2h_bits(x[0]); hv.y = f2h_bits(x[1]); hv.z = f2h_bits(x[2]); hv.w = f2h_bits(x[3]);
+            *(ushort4 *)((which == 0 ? a.q : a.k) + (((int64_t)b * H + h) * a.Tp + t) * 64 + d) = hv;
+        }
+    }
+}
+
 // BK = k per LDS stage.  Small tiles (2-4 MFMAs per wave per 32 k) spend
 // their k loop on barriers and LDS round trips, so they take 64 or 128 k per
 // stage; the k steps of 16 still run in order, so the result is bitwise the
@@ -358,6 +499,8 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
     constexpr int CPR = BK / 8;                         // 16-byte chunks per row of a stage
     constexpr int ACH = BM * CPR / 256, BCH = BN * CPR / 256;  // chunks per thread per stage
     __shared__ __attribute__((aligned(16))) f16 smem[2 * (BM + BN) * LD];
+    // the staged epilogue where the k stages' LDS holds the f32 tile
+    constexpr bool STAGED = epi_stage_bytes<BM, BN>() <= sizeof(smem);
     f16 *As = smem;
     f16 *Bs = smem + 2 * BM * LD;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -437,6 +580,12 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs a) {
         }
         sstore(buf ^ 1);  // (after the last stage: a clamped copy, unread)
         __syncthreads();
+    }
+    if constexpr (STAGED) {
+        if (epi_staged_ok<EPI, BN>(a)) {
+            gemm_epi_staged<EPI, BM, BN>(a, acc, (float *)smem, m0, n0);
+            return;
+        }
     }
     // epilogue: lane holds column n, rows (reg&3) + 8(reg>>2) + 4(lane>>5)
 #pragma unroll
@@ -556,6 +705,10 @@ __global__ __launch_bounds__(256) void k_gemm_g(GemmArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
+    if (epi_staged_ok<EPI, 128>(a)) {
+        gemm_epi_staged<EPI, 128, 128>(a, acc, (float *)gsm, m0, n0);
+        return;
+    }
     // epilogue as k_gemm's: lane holds column n, rows (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -574,7 +727,7 @@ __global__ __launch_bounds__(256) void k_gemm_g(GemmArgs a) {
 template <bool CONV>
 static hipError_t gemm_g_dispatch(hipStream_t s, int epi, const GemmArgs &a) {
     const int nwg = ((a.M + 127) / 128) * ((a.N + 127) / 128);
-    constexpr size_t lds = 65536;
+    constexpr size_t lds = epi_stage_bytes<128, 128>();  // (>= the two 32 KB k stages)
 #define GEMMG_CASE(E)                                                                        \
     case E: {                                                                               \
         hipError_t e = allow_lds(k_gemm_g<E, CONV>, lds);                              \
@@ -630,8 +783,10 @@ static hipError_t gemm_dispatch_epi(hipStream_t s, int epi, const GemmArgs &a) {
     return hipGetLastError();
 }
 
-hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a) {
-    if (a.M <= 0 || a.N <= 0) return hipSuccess;
+hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a0) {
+    if (a0.M <= 0 || a0.N <= 0) return hipSuccess;
+    GemmArgs a = a0;
+    a.epi_staged = tune_of(a0.tune).epi_staged;
     if (a.B32) return launch_gemm32(s, epi, a);
     if (a.K % GBK != 0 || a.K <= 0) return hipErrorInvalidValue;
     if (a.conv && a.conv_cp % GBK != 0) return hipErrorInvalidValue;
@@ -729,7 +884,7 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
                     if (TAIL) i = key < T ? i : n_exp;
                     const float e = h2f_bits(tab[i]);  // unguarded read (a guarded one branches per element)
                     if constexpr (PASS == 1) sum += (double)e;
-                    else pa[(r + u) >> 3][(r + u) & 7] = (f16)(e * inv);
+                    else pa[(r + u) >> 3][(r + u) & 7] = f16_rt(e * inv);
                 }
             }
             if constexpr (PASS == 2) {
@@ -1036,7 +1191,7 @@ __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[L], int K, con
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const float t = (float)((double)xx[u] - mean) * scale;
-                dst[e + u] = (f16)(bb4[u] + ww[u] * t);
+                dst[e + u] = f16_rt(bb4[u] + ww[u] * t);
             }
         }
     }
@@ -1312,7 +1467,7 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
                     sacc.z = sacc.z + v[c].z; sacc.w = sacc.w + v[c].w;
                 }
             half4 hv;
-            hv[0] = (f16)sacc.x; hv[1] = (f16)sacc.y; hv[2] = (f16)sacc.z; hv[3] = (f16)sacc.w;
+            hv[0] = f16_rt(sacc.x); hv[1] = f16_rt(sacc.y); hv[2] = f16_rt(sacc.z); hv[3] = f16_rt(sacc.w);
             *(half4 *)(xs + bb * K + k) = hv;
         }
     }
@@ -1672,7 +1827,7 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) acc = dot8(wq[i][kc], *(const half8 *)(xs + kc * 128 + l16 * 8), acc);
         acc = red16_sum(acc);
-        if (l16 == 0) qh[w * 16 + q * 4 + i] = (f16)((acc + bqr[i]) * a.qscale);
+        if (l16 == 0) qh[w * 16 + q * 4 + i] = f16_rt((acc + bqr[i]) * a.qscale);
     }
     __syncthreads();
     trace_phase(a.phase, 2);
@@ -1784,7 +1939,7 @@ __global__ __launch_bounds__(256) void k_dec_xattn_rows(DecAttnArgs a) {
 #pragma unroll
             for (int kc = 0; kc < KC; ++kc) acc = dot8(wq[i][kc], *(const half8 *)(xs[r] + kc * 128 + l16 * 8), acc);
             acc = red16_sum(acc);
-            if (l16 == 0) qh[r][w * 16 + q * 4 + i] = (f16)((acc + bqr[i]) * a.qscale);
+            if (l16 == 0) qh[r][w * 16 + q * 4 + i] = f16_rt((acc + bqr[i]) * a.qscale);
         }
     }
     __syncthreads();
@@ -1955,7 +2110,7 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
         return;
     }
     __shared__ __attribute__((aligned(16))) f16 oh[64];
-    if (tid < 64) oh[tid] = (f16)(((ored[0][tid] + ored[1][tid]) + ored[2][tid]) + ored[3][tid]);  // f16 input of Wo
+    if (tid < 64) oh[tid] = f16_rt(((ored[0][tid] + ored[1][tid]) + ored[2][tid]) + ored[3][tid]);  // f16 input of Wo
     __syncthreads();
     half8 ov[8];
 #pragma unroll

@@ -676,8 +676,8 @@ __device__ __forceinline__ void ln_rows(const float *xf, const LnP<NS> &P, f16 *
                 const float bb[4] = {P.b[i].x, P.b[i].y, P.b[i].z, P.b[i].w};
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    xs[w * NS + e + u] = (f16)(bb[u] + ww[u] * ((float)((double)a4[u] - ma) * ka));
-                    xs[(w + 4) * NS + e + u] = (f16)(bb[u] + ww[u] * ((float)((double)b4[u] - mb) * kb));
+                    xs[w * NS + e + u] = f16_rt(bb[u] + ww[u] * ((float)((double)a4[u] - ma) * ka));
+                    xs[(w + 4) * NS + e + u] = f16_rt(bb[u] + ww[u] * ((float)((double)b4[u] - mb) * kb));
                 }
             }
         }
@@ -712,7 +712,7 @@ __device__ __forceinline__ void ln_rows(const float *xf, const LnP<NS> &P, f16 *
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const float t = (float)((double)xx[u] - mean) * scale;
-                    xs[b * NS + e + u] = (f16)(bb[u] + ww[u] * t);
+                    xs[b * NS + e + u] = f16_rt(bb[u] + ww[u] * t);
                 }
             }
         }
@@ -772,7 +772,7 @@ __device__ __forceinline__ bool ln1_vals(const float (&xv)[Ln1P<NS>::NE], const 
         const int e = tid + PT * u;
         if (e < NS) {
             const float t = (float)((double)xv[u] - mean) * scale;
-            xs[e] = (f16)(P.b[u] + P.w[u] * t);
+            xs[e] = f16_rt(P.b[u] + P.w[u] * t);
         }
     }
     return true;
@@ -1401,7 +1401,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 PSTAMP(l * 32 + 29)
                         wset_dot<1>(S, xs, NS, 1, h * 64, h * 64 + 64, slot, l16,
                                     [&](int row, int, float v, float eb, bool valid) {
-                                        if (valid) qh[row - h * 64] = (f16)((v + eb) * qs);
+                                        if (valid) qh[row - h * 64] = f16_rt((v + eb) * qs);
                                     });
                         __syncthreads();
                 PSTAMP(l * 32 + 30)
