@@ -1493,6 +1493,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     double sum = 0.0;
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
+                        if (256 * u >= T) break;  // workgroup-uniform: no key left (T = 1500: 6 of 8)
                         const int j = tid + 256 * u;
                         const float pj = exp_f16_hash(sv[u] - m, sh.expfb, fbk);
                         if (j < T) sum += (double)pj;
