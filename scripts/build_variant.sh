@@ -1,5 +1,6 @@
 #!/bin/bash
-# Build a variant of libwhisper_mi355x.so for on-GPU A/B runs (scripts/ab_lib.sh):
+# Build a variant of libwhisper_mi355x.so for on-GPU A/B runs (scripts/session.sh ab=WMI_LIB=...,
+# scripts/lib_equal.py):
 #   bash scripts/build_variant.sh NAME "PERSIST_FLAGS" ["EXTRA"]
 # -> whisper.rs_amd/ab/NAME/libwhisper_mi355x.so (select it with WMI_LIB)
 set -e

@@ -554,6 +554,33 @@ def test_multirow_instances_bitwise_independent_of_B(wmi, model_cache):
             np.testing.assert_array_equal(res[nb][1][i], res[8][1][i])
 
 
+def test_encoder_gemm_paths_bitwise(wmi, model_cache):
+    """The 8-clip encoder's GEMMs run on the LDS-DMA kernel (k_gemm_g) with
+    epilogues staged through LDS; WMI_GEMM_G=0 / WMI_GEMM_EPI=0 select the
+    register-staged kernel and the per-lane epilogue stores.  All four give
+    bitwise the same encoder output and cross K / V (one MFMA order; one
+    f32 -> f16 rounding sequence, f16_rt), at 8 clips (k_gemm_g) and one clip
+    (k_gemm's smaller tiles)."""
+    path = synth.model_path("base", model_cache)
+    clips = [synth.synth_pcm_f32(30.0, 1400 + i) for i in range(8)]
+    for nc in (8, 1):
+        ref = None
+        for env in ({}, {"WMI_GEMM_EPI": "0"}, {"WMI_GEMM_G": "0"}, {"WMI_GEMM_G": "0", "WMI_GEMM_EPI": "0"}):
+            ctx = _ctx_with_env(wmi, path, env, max_clips=nc)
+            try:
+                ctx.pcm_to_mel_batch(clips[:nc])
+                ctx.encode(1, 0)
+                got = [(ctx.encoder_out(i), *ctx.cross_kv(i)) for i in range(nc)]
+            finally:
+                ctx.close()
+            if ref is None:
+                ref = got
+                continue
+            for a, b in zip(ref, got):
+                for x, y in zip(a, b):
+                    np.testing.assert_array_equal(x, y)
+
+
 def test_split_grid_equals_full_grid(wmi, model_cache):
     """A block of 8 clips decodes as two concurrent half-grid launches (rows
     0-3 and 4-7 on 128 workgroups each, two streams, separate exchange blocks,
