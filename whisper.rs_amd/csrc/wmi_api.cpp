@@ -1634,7 +1634,7 @@ int ptrace_dump(wmi_context *ctx, int steps) {
         // sub-phase stamps (slots 27..31, when a build sets them): time after
         // the latest poll-done stamp of the same layer
         for (int k = 11; k < 32; ++k) {
-            if (k == 15) k = 27;
+            if (k == 16) k = 27;
             double s = 0;
             int c = 0;
             for (int st = 1; st < steps; ++st)

@@ -636,6 +636,28 @@ __device__ __forceinline__ void ln_params(const float *lw, const float *lb, LnP<
         P.b[i] = *glb((const float4 *)(lb + ec));
     }
 }
+// The multi-row phases' LayerNorm parameters, requested before the phase's
+// poll, pass through an empty asm right there (n <= 512): the compiler
+// otherwise re-issues these invariant loads where ln_rows first uses them,
+// after the poll, and waits for them there with a vmcnt that also covers
+// everything requested since (in the logits phase: the streamed vocabulary
+// tiles).  C4's shard 8 352 -> 8 506 audio-s/s; above n = 512 the settled
+// registers cost more than the late loads (C5 118.1 -> 116.6), and a
+// workgroup-wide multi-row LayerNorm there measured far slower (C5 97)
+// (profiles/r04/ln_settle_ab.txt)
+template <int NS>
+__device__ __forceinline__ void ln_params_early(const float *lw, const float *lb, LnP<NS> &P, int lane) {
+    ln_params<NS>(lw, lb, P, lane);
+    if constexpr (NS <= 512) {
+#pragma unroll
+        for (int i = 0; i < LnP<NS>::V; ++i) {
+            float4 w = P.w[i], b = P.b[i];
+            asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z), "+v"(w.w), "+v"(b.x), "+v"(b.y), "+v"(b.z), "+v"(b.w));
+            P.w[i] = w;
+            P.b[i] = b;
+        }
+    }
+}
 template <int NS>
 __device__ __forceinline__ void ln_rows(const float *xf, const LnP<NS> &P, f16 *xs, int B, int w, int lane) {
     constexpr int LV = LnP<NS>::V;
@@ -1014,7 +1036,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 LnP<NS> lp;
                 Ln1P<NS> l1;
                 if constexpr (BT == 1) ln1_params<NS>(P.ln1_w, P.ln1_b, l1, tid);
-                else ln_params<NS>(P.ln1_w, P.ln1_b, lp, lane);
+                else ln_params_early<NS>(P.ln1_w, P.ln1_b, lp, lane);
                 PREFETCH_ISSUED
                 __syncthreads();
                 if (l == 0) {
@@ -1274,7 +1296,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 LnP<NS> lp;
                 Ln1P<NS> l1;
                 if constexpr (BT == 1) ln1_params<NS>(P.lnc_w, P.lnc_b, l1, tid);
-                else ln_params<NS>(P.lnc_w, P.lnc_b, lp, lane);
+                else ln_params_early<NS>(P.lnc_w, P.lnc_b, lp, lane);
                 PREFETCH_ISSUED
                 __syncthreads();
                 if constexpr (BT == 1) {
@@ -1864,7 +1886,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 LnP<NS> lp;
                 Ln1P<NS> l1;
                 if constexpr (BT == 1) ln1_params<NS>(P.ln2_w, P.ln2_b, l1, tid);
-                else ln_params<NS>(P.ln2_w, P.ln2_b, lp, lane);
+                else ln_params_early<NS>(P.ln2_w, P.ln2_b, lp, lane);
                 PREFETCH_ISSUED
                 __syncthreads();
                 if constexpr (BT == 1) {
@@ -1932,7 +1954,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             LnP<NS> lp;
             Ln1P<NS> l1;
             if constexpr (BT == 1) ln1_params<NS>(a.dln_w, a.dln_b, l1, tid);
-            else ln_params<NS>(a.dln_w, a.dln_b, lp, lane);
+            else ln_params_early<NS>(a.dln_w, a.dln_b, lp, lane);
             PREFETCH_ISSUED
             __syncthreads();
             if constexpr (BT == 1) {
@@ -2033,7 +2055,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             PHASE_IDS
             constexpr int KQ = NS / 4, NKW = KQ / 32, TG = 8;  // k per wave, MFMA steps per wave, tiles per LDS group
             LnP<NS> lp;
-            ln_params<NS>(a.dln_w, a.dln_b, lp, lane);
+            ln_params_early<NS>(a.dln_w, a.dln_b, lp, lane);
             PREFETCH_ISSUED
             __syncthreads();
             {
@@ -2132,7 +2154,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             LnP<NS> lp;
             Ln1P<NS> l1;
             if constexpr (BT == 1) ln1_params<NS>(a.dln_w, a.dln_b, l1, tid);
-            else ln_params<NS>(a.dln_w, a.dln_b, lp, lane);
+            else ln_params_early<NS>(a.dln_w, a.dln_b, lp, lane);
             PREFETCH_ISSUED
             __syncthreads();
             if constexpr (BT == 1) {
