@@ -48,10 +48,10 @@ def test_one_pass_scale_matches_two_pass_within_bound(n):
         assert u <= 1, (ratio, u)
 
 
-def test_one_pass_bound_breaks_only_far_outside_the_data():
+def test_one_pass_bound_ends_at_large_mean_over_std():
     """Where the bound ends: at |mean| / std = 1e5 (mean^2 / var = 1e10) the
-    one-pass scale drifts by many ulps — documenting that the formula is a
-    deliberate trade, safe for decoder activations, not a general identity."""
+    one-pass scale drifts by more than an ulp — the formula is a deliberate
+    trade (one reduction instead of two), not a general identity."""
     rng = np.random.default_rng(11)
     x = (rng.standard_normal(1280) * 1e-2 + 1e3).astype(np.float32)
     assert ulps(scale_one_pass(x), scale_two_pass(x)) > 1
