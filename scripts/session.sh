@@ -68,7 +68,7 @@ import json; d=json.load(open('${O}_bench.json')); print('bench', d['value'], d[
           timeout -k 10 300 env $e python3 bench.py --model ${MODEL:-base} --beam ${BEAM:-0} --clips-per-gpu ${CPG:-1} \
             --steps ${STEPS:-10} --warmup 2 --configs none --no-cpu-baseline 2>/dev/null > ${O}_ab_one.json || exit 1
           python3 -c "
-import json; d=json.load(open('${O}_ab_one.json')); print('$e', d['value'], d['stage_ms']['decode_ms'], d['encoder_ms'])" \
+import json; d=json.load(open('${O}_ab_one.json')); print('$e', d['value'], d['stage_ms']['decode_ms'], d['encoder_ms'], d['stage_ms']['mel_ms'])" \
             | tee -a ${O}_ab.txt
         done
       done ;;

@@ -185,6 +185,8 @@ struct wmi_context {
     size_t model_bytes = 0;
     MelTables *meltabs = nullptr;
     float *filt_t = nullptr;
+    float *filt_c = nullptr;  // compact filterbank (k_mel_frames FG variant), or null when it would not fit
+    int n_fc = 0;             // its floats
     uint16_t *gelu_tab = nullptr, *exp_tab = nullptr;
     uint16_t *conv1_w = nullptr, *conv2_w = nullptr;
     float *conv1_b = nullptr, *conv2_b = nullptr, *e_pe = nullptr, *lnp_w = nullptr, *lnp_b = nullptr;
@@ -294,6 +296,8 @@ struct wmi_context {
     // step: ~17 us each), profiles/r04/coop_launch_ab.txt — and the grid is
     // checked against the occupancy API at context creation instead (grid_nsb)
     bool persist_coop = false;
+    // WMI_VREG=0: stream the one-row logits' non-resident vocabulary tiles every step
+    bool persist_vreg = true;
     bool use_xshare = true;           // WMI_XSHARE=0: beam rows read the cross K / V per row
     // greedy blocks of at least split_rows clips decode as two concurrent
     // half-grid launches (rows [0, B/2) and [B/2, B), each on half the CUs, a
@@ -748,6 +752,21 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
         memcpy(&filt_t[(size_t)201 * C + 2 * (size_t)m], r, 8);
     }
     const size_t o_filt = add(filt_t.data(), filt_t.size() * 4);
+    // compact copy for the LDS-resident filterbank: per mel {k0, k1, offset, 0}
+    // (int32), then each mel's weights k0..k1-1 back to back (a Slaney bank
+    // holds ~2 x 201 non-zeros); past MEL_FC_MAX floats the kernel keeps
+    // the [201][C] layout
+    std::vector<float> filt_c(4 * (size_t)C, 0.0f);
+    for (int m = 0; m < C; ++m) {
+        int32_t r[4];
+        memcpy(r, &filt_t[(size_t)201 * C + 2 * (size_t)m], 8);
+        r[2] = (int32_t)(filt_c.size() - 4 * (size_t)C);
+        r[3] = 0;
+        memcpy(&filt_c[4 * (size_t)m], r, 16);
+        for (int k = r[0]; k < r[1]; ++k) filt_c.push_back(pm.filters[(size_t)m * 201 + k]);
+    }
+    const bool fc_ok = filt_c.size() <= (size_t)MEL_FC_MAX;
+    const size_t o_filc = fc_ok ? add(filt_c.data(), filt_c.size() * 4) : 0;
     const size_t o_gelu = add(gelu.data(), gelu.size() * 2);
     std::vector<uint16_t> expneg(expt.begin() + 0x8000, expt.begin() + 0x8000 + n_exp);
     // whole 16-byte chunks for the LDS copy, and always a 0 at index n_exp
@@ -887,6 +906,8 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
     auto H = [&](size_t o) { return (uint16_t *)(base + o); };
     ctx->meltabs = (MelTables *)(base + o_mt);
     ctx->filt_t = F(o_filt);
+    ctx->filt_c = fc_ok ? F(o_filc) : nullptr;
+    ctx->n_fc = (int)filt_c.size();
     ctx->gelu_tab = H(o_gelu);
     ctx->exp_tab = H(o_exp);
     ctx->conv1_w = H(o_c1w); ctx->conv1_b = F(o_c1b);
@@ -1137,7 +1158,8 @@ int run_mel(wmi_context *ctx) {
     HIPCHK(ctx, hipMemsetAsync(ctx->d_melmax, 0, B * 4, ctx->stream));
     HIPCHK(ctx, launch_mel_frames(ctx->stream, ctx->meltabs, ctx->filt_t, ctx->hp.n_mels,
                                   (const float *const *)ctx->d_pcm_ptrs, ctx->d_nsamp, ctx->d_mel, ctx->mel_stride,
-                                  ctx->d_nlen, ctx->max_len, ctx->d_melmax, B));
+                                  ctx->d_nlen, ctx->max_len, ctx->d_melmax, B, ctx->tune.mel_g ? ctx->filt_c : nullptr,
+                                  ctx->n_fc));
     if (ctx->checksums) {  // clip 0's mel before clamp_and_normalize (main.rs:1645-1647)
         std::vector<float> m((size_t)ctx->hp.n_mels * ctx->n_len_host[0]);
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1693,6 +1715,7 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     a.xg = ctx->d_xg; a.err = ctx->derr;
     a.nres = ctx->persist_nres[B];
     a.coop = ctx->persist_coop ? 1 : 0;
+    a.vreg = ctx->persist_vreg ? 1 : 0;
     a.stall_wg = -1;
     if (ctx->fault_inject == 1) {  // once per context: its first persistent launch
         a.stall_wg = G - 1;
@@ -2215,6 +2238,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (const char *c = getenv("WMI_CHECKSUMS")) ctx->checksums = atoi(c) != 0;
     if (const char *c = getenv("WMI_FAULT_INJECT")) ctx->fault_inject = atoi(c) ? 1 : 0;
     if (const char *c = getenv("WMI_COOP")) ctx->persist_coop = atoi(c) != 0;
+    if (const char *c = getenv("WMI_VREG")) ctx->persist_vreg = atoi(c) != 0;
     if (const char *c = getenv("WMI_XSHARE")) ctx->use_xshare = atoi(c) != 0;
     if (const char *c = getenv("WMI_SPLIT_ROWS")) ctx->split_rows = atoi(c);
     ctx->dec_layers = ctx->hp.n_text_layer;
@@ -2245,6 +2269,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     knob("WMI_ENC_ATTN_NW", tn.enc_attn_nw, 0);
     knob("WMI_GEMM_G", tn.gemm_g, 0);
     knob("WMI_GEMM_EPI", tn.epi_staged, 0);
+    knob("WMI_MEL_G", tn.mel_g, 0);
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_trace, TRACE_SLOTS * 16 + 64 * 16 * 8));

@@ -28,7 +28,9 @@ static_assert(sizeof(MelTables) % 16 == 0, "k_mel_frames copies MelTables in 16-
 // pcm: n_clips pointers (device) with n_samples each (device arrays).
 hipError_t launch_mel_frames(hipStream_t s, const MelTables *tabs, const float *filt_t /*[201][n_mel]*/, int n_mel,
                              const float *const *pcm, const int64_t *n_samples, float *mel, int64_t mel_stride,
-                             const int64_t *n_len, int64_t max_len, uint32_t *mel_max, int n_clips);
+                             const int64_t *n_len, int64_t max_len, uint32_t *mel_max, int n_clips,
+                             const float *filt_c /* compact bank (wmi_api.cpp), or null: LDS copy of filt_t */, int n_fc);
+constexpr int MEL_FC_MAX = 4096;  // floats of the compact filterbank k_mel_frames keeps in LDS
 // clamp_and_normalize in place on mel.
 hipError_t launch_mel_norm(hipStream_t s, float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
                            int64_t max_len, const uint32_t *mel_max, int n_clips);
@@ -68,6 +70,7 @@ struct Tune {
     int graph_steps = 8;    // WMI_GRAPH_STEPS: chain decoder steps per captured graph
     int enc_attn_nw = 0;    // WMI_ENC_ATTN_NW: 32-query blocks (two waves each) per k_attn_enc4 workgroup (0 auto, 1, 2, 4)
     int gemm_g = 1;         // WMI_GEMM_G: large-M encoder GEMMs on k_gemm_g (LDS-DMA staging); 0: k_gemm
+    int mel_g = 1;          // WMI_MEL_G: mel frames as 8 one-frame waves, filterbank from global (0: 4 two-frame waves, LDS copy)
     int epi_staged = 1;     // WMI_GEMM_EPI: GEMM epilogues through LDS, 16 / 8-byte stores (0: per-lane 2 / 4-byte stores)
 };
 extern const Tune kTuneDefault;
@@ -376,6 +379,10 @@ struct PersistArgs {
     // host side: launch through hipLaunchCooperativeKernel (the runtime then
     // checks the grid against the device's co-residency limit at launch)
     int coop;
+    // one-row MFMA logits (n <= 512): the vocabulary tiles that do not fit the
+    // LDS stay in registers for the whole launch instead of streaming every
+    // step (0: streamed; the kernel streams them anyway past 8 tiles)
+    int vreg;
 };
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G);
 // the inputs whose f32 exp is too close to an f16 midpoint, with their table

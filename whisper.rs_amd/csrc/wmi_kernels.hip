@@ -84,38 +84,44 @@ __device__ __forceinline__ void fft_level(const cpx *in, cpx *out, int n, int ns
     }
 }
 
-__global__ __launch_bounds__(256) void k_mel_frames(const MelTables *__restrict__ tabs_g, const float *__restrict__ filt_t,
+// MW waves of FPW frames per workgroup; FG: the compact filterbank (each
+// mel's non-zero weights, wmi_api.cpp filt_c) in LDS instead of the [201][C]
+// copy, so two workgroups of eight one-frame waves fit a CU instead of one of
+// four two-frame waves; the same terms in the same order (bitwise equal)
+template <int MW, int FPW, bool FG>
+__global__ __launch_bounds__(64 * MW) void k_mel_frames(const MelTables *__restrict__ tabs_g, const float *__restrict__ filt_t,
                                                     int n_mel, const float *const *pcm, const int64_t *n_samples,
                                                     float *mel, int64_t mel_stride, const int64_t *n_len,
-                                                    uint32_t *mel_max) {
+                                                    uint32_t *mel_max, int n_fc) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int b = blockIdx.y;
     const int64_t nl = n_len[b];
-    const int64_t frame0 = (int64_t)blockIdx.x * (MEL_WAVES * MEL_FPW);
+    const int64_t frame0 = (int64_t)blockIdx.x * (MW * FPW);
     if (frame0 >= nl) return;
     MelTables *tabs = (MelTables *)sm;
     float *F = sm + sizeof(MelTables) / 4;
-    float *scratch = F + 203 * n_mel;  // after the filterbank and its per-mel ranges
+    const int nfc = FG ? n_fc : 203 * n_mel;  // floats of the bank's LDS copy
+    float *scratch = F + ((nfc + 3) & ~3);
     {
         // tables + filterbank (~74 KB at 80 mels) -> LDS in 16-byte chunks,
         // eight requests in flight per thread before the first store (a
         // one-load-per-iteration copy loop waited one round trip per chunk)
         const float4 *s1 = (const float4 *)tabs_g, *s2 = (const float4 *)filt_t;
         float4 *dst = (float4 *)tabs;  // tabs, then F (contiguous)
-        const int n1 = (int)(sizeof(MelTables) / 16), n2 = 203 * n_mel / 4, nt = n1 + n2;  // + the ranges
-        for (int base = threadIdx.x; base < nt; base += 256 * 8) {
+        const int n1 = (int)(sizeof(MelTables) / 16), n2 = nfc / 4, nt = n1 + n2;  // + the ranges
+        for (int base = threadIdx.x; base < nt; base += 64 * MW * 8) {
             float4 v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const int i = base + 256 * u;
+                const int i = base + 64 * MW * u;
                 const int ic = i < nt ? i : nt - 1;
                 v[u] = ic < n1 ? s1[ic] : s2[ic - n1];
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                if (base + 256 * u < nt) dst[base + 256 * u] = v[u];
+                if (base + 64 * MW * u < nt) dst[base + 64 * MW * u] = v[u];
         }
-        for (int i = 4 * n2 + (int)threadIdx.x; i < 203 * n_mel; i += 256) F[i] = filt_t[i];  // (n_mel % 4 != 0)
+        for (int i = 4 * n2 + (int)threadIdx.x; i < nfc; i += 64 * MW) F[i] = filt_t[i];  // (a size % 4 != 0)
     }
     __syncthreads();
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -126,8 +132,8 @@ __global__ __launch_bounds__(256) void k_mel_frames(const MelTables *__restrict_
     const int64_t ns = n_samples[b];
     float lmax = -INFINITY;
     float *melb = mel + (int64_t)b * mel_stride;
-    for (int f = 0; f < MEL_FPW; ++f) {
-        const int64_t i = frame0 + w * MEL_FPW + f;
+    for (int f = 0; f < FPW; ++f) {
+        const int64_t i = frame0 + w * FPW + f;
         if (i >= nl) break;
         const int64_t off = i * 160;
         // window, zero past the end (main.rs:1594-1601)
@@ -170,11 +176,16 @@ __global__ __launch_bounds__(256) void k_mel_frames(const MelTables *__restrict_
         }
         wave_sync();
         // filterbank, clamp, log10 (main.rs:1620-1634)
-        const int *rng = (const int *)(F + 201 * n_mel);  // per mel: [first, end) of its non-zero weights
+        const int *rng = (const int *)(F + (FG ? 0 : 201 * n_mel));  // per mel: [first, end) of its non-zero weights
         for (int m = lane; m < n_mel; m += 64) {
             float sum = 0.0f;
-            const int k0 = rng[2 * m], k1 = rng[2 * m + 1];  // outside: weight 0 -> exact +0 terms
-            for (int k = k0; k < k1; ++k) sum = sum + fin[k] * F[k * n_mel + m];
+            const int k0 = rng[(FG ? 4 : 2) * m], k1 = rng[(FG ? 4 : 2) * m + 1];  // outside: weight 0 -> exact +0 terms
+            if (FG) {
+                const float *wm = F + 4 * n_mel + rng[4 * m + 2] - k0;
+                for (int k = k0; k < k1; ++k) sum = sum + fin[k] * wm[k];
+            } else {
+                for (int k = k0; k < k1; ++k) sum = sum + fin[k] * F[k * n_mel + m];
+            }
             if (sum < 1e-10f) sum = 1e-10f;
             // glibc's log10f (what Rust's f32::log10 calls) is within an ulp of
             // the correctly rounded result; the double path lands on the same
@@ -222,17 +233,30 @@ __global__ void k_mel_window(const float *mel, int64_t mel_stride, int n_mel, co
     }
 }
 
+template <int MW, int FPW, bool FG>
+static hipError_t mel_frames_launch(hipStream_t s, const MelTables *tabs, const float *filt_t, int n_mel,
+                                    const float *const *pcm, const int64_t *n_samples, float *mel, int64_t mel_stride,
+                                    const int64_t *n_len, int64_t max_len, uint32_t *mel_max, int n_clips, int n_fc) {
+    const size_t lds = sizeof(MelTables) + sizeof(float) * ((((FG ? n_fc : 203 * n_mel) + 3) & ~3) + MW * MEL_SCRATCH);
+    dim3 grid(cdiv(max_len, MW * FPW), n_clips);
+    hipError_t e = allow_lds(k_mel_frames<MW, FPW, FG>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_mel_frames<MW, FPW, FG>), grid, dim3(64 * MW), lds, s, tabs, filt_t, n_mel, pcm, n_samples, mel,
+                       mel_stride, n_len, mel_max, n_fc);
+    return hipGetLastError();
+}
+
 hipError_t launch_mel_frames(hipStream_t s, const MelTables *tabs, const float *filt_t, int n_mel,
                              const float *const *pcm, const int64_t *n_samples, float *mel, int64_t mel_stride,
-                             const int64_t *n_len, int64_t max_len, uint32_t *mel_max, int n_clips) {
-    const size_t lds = sizeof(MelTables) + sizeof(float) * (203 * n_mel + MEL_WAVES * MEL_SCRATCH);
-    dim3 grid(cdiv(max_len, MEL_WAVES * MEL_FPW), n_clips);
+                             const int64_t *n_len, int64_t max_len, uint32_t *mel_max, int n_clips,
+                             const float *filt_c, int n_fc) {
     if (max_len <= 0) return hipSuccess;
-    hipError_t e = allow_lds(k_mel_frames, lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_mel_frames, grid, dim3(256), lds, s, tabs, filt_t, n_mel, pcm, n_samples, mel, mel_stride,
-                       n_len, mel_max);
-    return hipGetLastError();
+    // (each frame's arithmetic is the same in both variants: bitwise equal)
+    if (!filt_c)
+        return mel_frames_launch<MEL_WAVES, MEL_FPW, false>(s, tabs, filt_t, n_mel, pcm, n_samples, mel, mel_stride, n_len,
+                                                            max_len, mel_max, n_clips, 0);
+    return mel_frames_launch<8, 1, true>(s, tabs, filt_c, n_mel, pcm, n_samples, mel, mel_stride, n_len, max_len, mel_max,
+                                         n_clips, n_fc);
 }
 
 hipError_t launch_mel_norm(hipStream_t s, float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
@@ -258,7 +282,9 @@ hipError_t launch_mel_window(hipStream_t s, const float *mel, int64_t mel_stride
 // ============================================================================
 // one wave per row, the row held in registers (n <= 1280, n % 4 == 0): one
 // round trip for the loads instead of one per pass over the row
-constexpr int LNW_V = 5;
+// (LNW_V = n / 256 rounded up, a template constant: no clamped duplicate loads)
+constexpr int LNW_VMAX = 5;
+template <int LNW_V>
 __device__ __forceinline__ void layernorm_wave(const float *x, int n, const float *w, const float *b, uint16_t *y16,
                                                float *y32, int lane) {
     float4 v[LNW_V], gw[LNW_V], gb[LNW_V];
@@ -307,18 +333,26 @@ __device__ __forceinline__ void layernorm_wave(const float *x, int n, const floa
     }
 }
 
+template <int LNW_V>
 __global__ __launch_bounds__(256) void k_layernorm(const float *x, int rows, int n, const float *w, const float *b,
                                                    uint16_t *y16, float *y32) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
-    layernorm_wave(x + (int64_t)row * n, n, w, b, y16 ? y16 + (int64_t)row * n : nullptr,
+    layernorm_wave<LNW_V>(x + (int64_t)row * n, n, w, b, y16 ? y16 + (int64_t)row * n : nullptr,
                    y32 ? y32 + (int64_t)row * n : nullptr, threadIdx.x & 63);
 }
 
 hipError_t launch_layernorm(hipStream_t s, const float *x, int rows, int n, const float *w, const float *b,
                             uint16_t *y16, float *y32) {
-    if (n % 4 || n > 256 * LNW_V) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_layernorm, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, rows, n, w, b, y16, y32);
+    if (n % 4 || n > 256 * LNW_VMAX || n < 4) return hipErrorInvalidValue;
+    const dim3 g(cdiv(rows, 4)), t(256);
+    switch ((n + 255) / 256) {
+        case 1: hipLaunchKernelGGL(k_layernorm<1>, g, t, 0, s, x, rows, n, w, b, y16, y32); break;
+        case 2: hipLaunchKernelGGL(k_layernorm<2>, g, t, 0, s, x, rows, n, w, b, y16, y32); break;
+        case 3: hipLaunchKernelGGL(k_layernorm<3>, g, t, 0, s, x, rows, n, w, b, y16, y32); break;
+        case 4: hipLaunchKernelGGL(k_layernorm<4>, g, t, 0, s, x, rows, n, w, b, y16, y32); break;
+        default: hipLaunchKernelGGL(k_layernorm<5>, g, t, 0, s, x, rows, n, w, b, y16, y32); break;
+    }
     return hipGetLastError();
 }
 
