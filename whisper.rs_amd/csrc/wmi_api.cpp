@@ -1208,13 +1208,14 @@ int run_encode(wmi_context *ctx, int mel_offset) {
         fflush(stdout);
     }
     // mel window -> conv1 input (main.rs:1816-1833)
-    HIPCHK(ctx, launch_mel_window(s, ctx->d_mel, ctx->mel_stride, hp.n_mels, ctx->d_nlen, mel_offset, T2, ctx->Cp1,
-                                  ctx->xconv, B, ctx->xconv32));
     // f32 models: f32 weights and unrounded f32 A operands (GELU outputs g1 /
     // hid stay f16: table values, exact in f32) -> the f32 GEMM
     const bool f32 = ctx->wf32;
     auto W32 = [&](const uint16_t *w) { return f32 ? (const float *)w : nullptr; };
-    HIPCHK(ctx, hipMemsetAsync(ctx->g1, 0, (size_t)B * (T2 + 2) * n * 2, s));
+    // (f16 models: conv2's zero pad rows of g1 are written by the window kernel)
+    HIPCHK(ctx, launch_mel_window(s, ctx->d_mel, ctx->mel_stride, hp.n_mels, ctx->d_nlen, mel_offset, T2, ctx->Cp1,
+                                  ctx->xconv, B, ctx->xconv32, f32 ? nullptr : ctx->g1, n));
+    if (f32) HIPCHK(ctx, hipMemsetAsync(ctx->g1, 0, (size_t)B * (T2 + 2) * n * 2, s));
     GemmArgs g{};
     // conv1 + bias + GELU (main.rs:1834-1855)
     g.A = ctx->xconv; g.B = ctx->conv1_w; g.bias = ctx->conv1_b;
@@ -1761,27 +1762,37 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
                        ctx->hp.n_text_ctx);
     int rc = ensure_decode_buffers(ctx, 8 * np, (size_t)Bt * n_gen);
     if (rc) return rc;
-    std::vector<int32_t> feed(8 * np);
-    for (int b = 0; b < 8; ++b)
-        for (int i = 0; i < np; ++i) feed[b * np + i] = prompt[i];
-    HIPCHK(ctx, hipMemcpyAsync(ctx->dfeed, feed.data(), feed.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     if (host_tokens) host_tokens->assign((size_t)Bt * n_gen, 0);
     if (host_counts) host_counts->assign(Bt, n_gen);
-    HIPCHK(ctx, hipMemsetAsync(ctx->derr, 0, 4, ctx->stream));
     for (int b0 = 0; b0 < Bt; b0 += 8) {
         const int B = Bt - b0 < 8 ? Bt - b0 : 8;
-        HIPCHK(ctx, hipMemsetAsync(ctx->dstate, 0, sizeof(DecState), ctx->stream));
-        HIPCHK(ctx, hipMemsetAsync(ctx->damax, 0, 8 * AMAX_SHARDS * 8, ctx->stream));
-        HIPCHK(ctx, hipMemsetAsync(ctx->dsync, 0, ctx->sync_bytes, ctx->stream));
         const int total_steps = np + n_gen - 1;
         const int G = persist_grid_for(ctx, B);
         const int B1 = B / 2, Gh = G > 0 && ctx->split_rows > 1 && B >= ctx->split_rows
                                        ? persist_split_grid(ctx->hp.n_text_state, G) : 0;
-        if (G > 0) HIPCHK(ctx, hipMemsetAsync(ctx->d_xg, 0, ctx->xg_bytes, ctx->stream));
-        if (Gh > 0) {
-            HIPCHK(ctx, hipMemsetAsync(ctx->d_xg2, 0, ctx->xg_bytes, ctx->stream));
-            HIPCHK(ctx, hipMemsetAsync(ctx->dstate2, 0, sizeof(DecState), ctx->stream));
+        // prompt feed (first block), error word, step state, argmax shards,
+        // chain sync words and exchange blocks: one reset launch
+        ResetArgs ra{};
+        auto zero = [&](void *p, size_t bytes) {
+            ra.ptr[ra.n] = p;
+            ra.bytes[ra.n++] = bytes;
+        };
+        if (b0 == 0) {
+            ra.dfeed = ctx->dfeed;
+            ra.n_feed = 8 * np;
+            for (int b = 0; b < 8; ++b)
+                for (int i = 0; i < np; ++i) ra.feed[b * np + i] = prompt[i];
+            zero(ctx->derr, 4);
         }
+        zero(ctx->dstate, sizeof(DecState));
+        zero(ctx->damax, 8 * AMAX_SHARDS * 8);
+        zero(ctx->dsync, ctx->sync_bytes);
+        if (G > 0) zero(ctx->d_xg, ctx->xg_bytes);
+        if (Gh > 0) {
+            zero(ctx->d_xg2, ctx->xg_bytes);
+            zero(ctx->dstate2, sizeof(DecState));
+        }
+        HIPCHK(ctx, launch_dec_reset(ctx->stream, ra));
         int done_steps = 0;
         while (done_steps < total_steps) {
             int chunk = total_steps - done_steps;

@@ -32,13 +32,25 @@ hipError_t launch_mel_frames(hipStream_t s, const MelTables *tabs, const float *
                              const float *filt_c /* compact bank (wmi_api.cpp), or null: LDS copy of filt_t */, int n_fc);
 constexpr int MEL_FC_MAX = 4096;  // floats of the compact filterbank k_mel_frames keeps in LDS
 // clamp_and_normalize in place on mel.
+// the state a decode run starts from, in one launch instead of a host copy
+// and five memsets (each a separate ~5 us fill kernel): zero `n` byte ranges
+// (4-byte aligned, sizes multiple of 4) and write feed[0..n_feed) to dfeed
+struct ResetArgs {
+    void *ptr[8];
+    size_t bytes[8];
+    int n;
+    int32_t *dfeed;
+    int n_feed;
+    int32_t feed[64];
+};
+hipError_t launch_dec_reset(hipStream_t s, const ResetArgs &a);
 hipError_t launch_mel_norm(hipStream_t s, float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
                            int64_t max_len, const uint32_t *mel_max, int n_clips);
 // mel window (main.rs:1816-1833) -> conv1 input, f16 time-major, zero-padded
 // by one frame at each end and to Cp channels: X[b][T2 + 2][Cp].
 hipError_t launch_mel_window(hipStream_t s, const float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
                              int mel_offset, int T2, int Cp, uint16_t *xconv, int n_clips,
-                             float *xconv32 = nullptr);
+                             float *xconv32 = nullptr, uint16_t *g1 = nullptr, int n = 0);
 
 // ---- LayerNorm (ggml norm + mul(repeat(w)) + add(repeat(b))) ----------------
 hipError_t launch_layernorm(hipStream_t s, const float *x, int rows, int n, const float *w, const float *b,

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "wmi_device.h"
 #include "wmi_internal.h"
 #include "wmi_gemm_epi.h"
@@ -213,8 +215,14 @@ __global__ void k_mel_norm(float *mel, int64_t mel_stride, int n_mel, const int6
 }
 
 __global__ void k_mel_window(const float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len, int mel_offset,
-                             int T2, int Cp, uint16_t *xconv, float *xconv32) {
+                             int T2, int Cp, uint16_t *xconv, float *xconv32, uint16_t *g1, int n) {
     const int b = blockIdx.y;
+    // conv1's output rows 0 and T2 + 1 of this clip are conv2's zero padding
+    // (its epilogue writes rows 1..T2): zeroed here instead of a memset of g1
+    if (g1)
+        for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < 2 * (int64_t)n;
+             idx += (int64_t)gridDim.x * blockDim.x)
+            g1[((int64_t)b * (T2 + 2) + (idx < n ? 0 : T2 + 1)) * n + (idx < n ? idx : idx - n)] = 0;
     const int64_t nl = n_len[b];
     const int64_t tot = (int64_t)(T2 + 2) * Cp;
     const int64_t i0 = mel_offset < nl ? mel_offset : nl;
@@ -259,6 +267,28 @@ hipError_t launch_mel_frames(hipStream_t s, const MelTables *tabs, const float *
                                          n_clips, n_fc);
 }
 
+__global__ __launch_bounds__(256) void k_dec_reset(ResetArgs a) {
+    const size_t gt = (size_t)blockIdx.x * 256 + threadIdx.x, nt = (size_t)gridDim.x * 256;
+    if (gt < (size_t)a.n_feed) a.dfeed[gt] = a.feed[gt];
+    for (int r = 0; r < a.n; ++r) {
+        uint32_t *p = (uint32_t *)a.ptr[r];
+        const size_t nw = a.bytes[r] / 4, n4 = ((uintptr_t)p & 15) ? 0 : nw / 4;
+        for (size_t i = gt; i < n4; i += nt) ((uint4 *)p)[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (size_t i = 4 * n4 + gt; i < nw; i += nt) p[i] = 0u;
+    }
+}
+hipError_t launch_dec_reset(hipStream_t s, const ResetArgs &a) {
+    if (a.n < 0 || a.n > 8 || a.n_feed < 0 || a.n_feed > 64) return hipErrorInvalidValue;
+    size_t mx = 0;
+    for (int r = 0; r < a.n; ++r) {
+        if (((uintptr_t)a.ptr[r] & 3) || (a.bytes[r] & 3)) return hipErrorInvalidValue;
+        mx = a.bytes[r] > mx ? a.bytes[r] : mx;
+    }
+    const int g = (int)std::min<size_t>(1024, std::max<size_t>(1, (mx / 16 + 255) / 256));
+    hipLaunchKernelGGL(k_dec_reset, dim3(g), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_mel_norm(hipStream_t s, float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
                            int64_t max_len, const uint32_t *mel_max, int n_clips) {
     if (max_len <= 0) return hipSuccess;
@@ -269,10 +299,11 @@ hipError_t launch_mel_norm(hipStream_t s, float *mel, int64_t mel_stride, int n_
 
 hipError_t launch_mel_window(hipStream_t s, const float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
                              int mel_offset, int T2, int Cp, uint16_t *xconv, int n_clips,
-                             float *xconv32) {
+                             float *xconv32, uint16_t *g1, int n) {
     const int64_t tot = (int64_t)(T2 + 2) * Cp;
     dim3 grid(cdiv(tot, 1024) < 512 ? cdiv(tot, 1024) : 512, n_clips);
-    hipLaunchKernelGGL(k_mel_window, grid, dim3(256), 0, s, mel, mel_stride, n_mel, n_len, mel_offset, T2, Cp, xconv, xconv32);
+    hipLaunchKernelGGL(k_mel_window, grid, dim3(256), 0, s, mel, mel_stride, n_mel, n_len, mel_offset, T2, Cp, xconv, xconv32,
+                       g1, n);
     return hipGetLastError();
 }
 
