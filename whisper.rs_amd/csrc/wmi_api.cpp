@@ -2281,6 +2281,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     knob("WMI_GEMM_G", tn.gemm_g, 0);
     knob("WMI_GEMM_EPI", tn.epi_staged, 0);
     knob("WMI_MEL_G", tn.mel_g, 0);
+    knob("WMI_GEMM_G_MIN", tn.gemm_g_min, 1);
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_trace, TRACE_SLOTS * 16 + 64 * 16 * 8));

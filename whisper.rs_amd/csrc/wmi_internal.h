@@ -82,6 +82,7 @@ struct Tune {
     int graph_steps = 8;    // WMI_GRAPH_STEPS: chain decoder steps per captured graph
     int enc_attn_nw = 0;    // WMI_ENC_ATTN_NW: 32-query blocks (two waves each) per k_attn_enc4 workgroup (0 auto, 1, 2, 4)
     int gemm_g = 1;         // WMI_GEMM_G: large-M encoder GEMMs on k_gemm_g (LDS-DMA staging); 0: k_gemm
+    int gemm_g_min = 240;   // WMI_GEMM_G_MIN: 128 x 128 tiles from which k_gemm_g takes a GEMM
     int mel_g = 1;          // WMI_MEL_G: mel frames as 8 one-frame waves, filterbank from global (0: 4 two-frame waves, LDS copy)
     int epi_staged = 1;     // WMI_GEMM_EPI: GEMM epilogues through LDS, 16 / 8-byte stores (0: per-lane 2 / 4-byte stores)
 };

@@ -863,7 +863,7 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a0) {
     // large M: the LDS-DMA kernel (bitwise the same outputs)
     // (8-clip encoder 3.10 -> 3.00 ms: conv2 84.6 -> 71.3, Wo 39.7 -> 34.8,
     // mlp.2 77.0 -> 60.2 us; QKV and mlp.0 unchanged)
-    if (t128 >= 240 && tune_of(a.tune).gemm_g && a.K % 64 == 0 && (!a.conv || a.conv_cp % 64 == 0))
+    if (t128 >= tune_of(a.tune).gemm_g_min && tune_of(a.tune).gemm_g && a.K % 64 == 0 && (!a.conv || a.conv_cp % 64 == 0))
         return a.conv ? gemm_g_dispatch<true>(s, epi, a) : gemm_g_dispatch<false>(s, epi, a);
     if (a.conv) {
         if (t128 >= 240) return gemm_dispatch_epi<128, 128, GBK, true>(s, epi, a);
