@@ -1012,6 +1012,12 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             rload(vrB, w + 4);
         }
     }
+    // one-row VALU logits (n = 768): likewise the rows past the LDS-resident
+    // ones (at most 8 per quarter-wave slot) stay in registers for the launch
+    constexpr bool LREG2 = BT == 1 && !LMF && !LMF2 && KC <= 6;
+    const bool lreg2 = LREG2 && a.vreg && rv1 - rs0 <= 128;
+    WSet<LREG2 ? KC : 1, LREG2 ? 8 : 1> SR;
+    if constexpr (LREG2) wset_load(SR, wmat(a.te), nullptr, NS, rs0, lreg2 ? rv1 : rs0, w * 4 + (lane >> 4), lane & 15);
     if (tid == 0) sh.abort_ = 0;
     if (tid < EXPFB) sh.expfb[tid] = a.exp_fb[tid];
     const uint32_t fbk = a.exp_fb[EXPFB + 1];  // the fallback table's hash multiplier
@@ -2211,8 +2217,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             // the streamed rows are requested after the poll, not in front of
             // it in the wave's load queue: the LDS-resident rows cover their
             // latency (logits 6.9 -> 5.8 us a step, profiles/r03/ab_r03c.txt)
-            wset_load(S0, wmat(a.te), nullptr, NS, rs0, rv1, slot, l16);
-            wset_load(S1, wmat(a.te), nullptr, NS, rs0 + RS, rv1, slot, l16);
+            wset_load(S0, wmat(a.te), nullptr, NS, rs0, lreg2 ? rs0 : rv1, slot, l16);
+            wset_load(S1, wmat(a.te), nullptr, NS, rs0 + RS, lreg2 ? rs0 : rv1, slot, l16);
             PREFETCH_ISSUED
             if constexpr (BT > 1) ln_rows<NS>(xf, lp, xs, B, w, lane);
             __syncthreads();
@@ -2272,7 +2278,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 }
             }
             PSTAMP(L * 32 + 2)
-            if (rs0 < rv1)
+            if (lreg2) {  // register-resident rows (LREG2): the same per-row dot chains
+                if constexpr (LREG2) wset_dot<BT>(SR, xs, NS, B, rs0, rv1, slot, l16, epi);
+            } else if (rs0 < rv1)
                 for (int rb = rs0;;) {
                     wset_dot<BT>(S0, xs, NS, B, rb, rv1, slot, l16, epi);
                     wset_load(S0, wmat(a.te), nullptr, NS, rb + 2 * RS, rv1, slot, l16);
