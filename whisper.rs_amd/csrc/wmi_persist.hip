@@ -986,34 +986,12 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             dst[LMF || LMF2 ? j * (NS / 8) + (c ^ (j & 15)) : i] = src[i];
         }
     }
-    // one-row MFMA logits: the vocabulary tiles past the LDS-resident ones
-    // (wave w's tiles w and w + 4 of at most 8) are loaded into registers once
-    // for the whole launch (PersistArgs::vreg) instead of streaming from the
-    // Infinity Cache every step behind the logits poll
-    constexpr bool LREG = BT == 1 && LMF;
-    constexpr int NKL = LREG ? NS / 32 : 1;
-    const int rres_l = rv0 + ((rs0 - rv0) & ~15), nst_l = (rv1 - rres_l + 15) >> 4;
-    const bool lreg = LREG && a.vreg && nst_l <= 8;
-    half8 vrA[NKL], vrB[NKL];
-    {
-        const half8 z8 = {};
-#pragma unroll
-        for (int kk = 0; kk < NKL; ++kk) vrA[kk] = vrB[kk] = z8;
-        if (lreg) {
-            const int lr = lane & 15, lh = lane >> 4;
-            auto rload = [&](half8 (&f)[NKL], int t) {
-                int row = rres_l + 16 * t + lr;
-                row = row < rv1 ? row : rv1 - 1;
-                const f16 *wr = (const f16 *)a.te + (int64_t)row * NS + 8 * lh;
-#pragma unroll
-                for (int kk = 0; kk < NKL; ++kk) f[kk] = t < nst_l ? sld((const half8 *)(wr + 32 * kk)) : z8;
-            };
-            rload(vrA, w);
-            rload(vrB, w + 4);
-        }
-    }
-    // one-row VALU logits (n = 768): likewise the rows past the LDS-resident
-    // ones (at most 8 per quarter-wave slot) stay in registers for the launch
+    // one-row VALU logits (n = 768): the vocabulary rows past the LDS-resident
+    // ones (at most 8 per quarter-wave slot) stay in registers for the whole
+    // launch (PersistArgs::vreg) instead of streaming from the Infinity Cache
+    // every step behind the logits poll.  (The same for the MFMA logits at
+    // n <= 512 — five 16-row tiles — measured no faster at base and slower at
+    // tiny against the streamed build: profiles/r04b/vs_first_session_*.)
     constexpr bool LREG2 = BT == 1 && !LMF && !LMF2 && KC <= 6;
     const bool lreg2 = LREG2 && a.vreg && rv1 - rs0 <= 128;
     WSet<LREG2 ? KC : 1, LREG2 ? 8 : 1> SR;
@@ -2010,7 +1988,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 for (int kk = 0; kk < NK; ++kk) f[kk] = t < nst ? sld((const half8 *)(wr + 32 * kk)) : z8;
             };
             half8 bA[NK], bB[NK];
-            if (!lreg) sload(bA, w);  // (requested after the poll: the resident tiles cover their latency)
+            sload(bA, w);  // (requested after the poll: the resident tiles cover their latency)
             if constexpr (BT > 1) sload(bB, w + 4);  // (one row: behind the resident tiles, measured faster)
             PREFETCH_ISSUED
             if constexpr (BT > 1) ln_rows<NS>(xf, lp, xs, B, w, lane);
@@ -2047,22 +2025,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 epi(d, rv0 + 16 * t, rres);
             }
             PSTAMP(L * 32 + 2)
-            if (lreg) {  // register-resident tiles w and w + 4 (LREG)
-              if constexpr (LREG) {
-                if (w < nst) {
-                    floatx4 d = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int kk = 0; kk < NK; ++kk) d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[kk], vrA[kk], d, 0, 0, 0);
-                    epi(d, rres + 16 * w, rv1);
-                }
-                if (w + 4 < nst) {
-                    floatx4 d = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int kk = 0; kk < NK; ++kk) d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[kk], vrB[kk], d, 0, 0, 0);
-                    epi(d, rres + 16 * (w + 4), rv1);
-                }
-              }
-            } else {
             if constexpr (BT == 1) sload(bB, w + 4);
             PREFETCH_ISSUED
             for (int t = w; t < nst; t += 8) {  // streamed tiles, two register sets in flight
@@ -2079,7 +2041,6 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 epi(d, rres + 16 * (t + 4), rv1);
                 sload(bB, t + 12);
                 PREFETCH_ISSUED
-            }
             }
             PSTAMP(L * 32 + 3)
             // the 16 lanes of a row group hold rows 4 (l >> 4) + r: reduce them
