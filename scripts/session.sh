@@ -12,6 +12,7 @@
 #   trace=MODEL:ROWS   decoder phase trace (WMI_PTRACE) of a greedy run: TAG_trace_MODEL_ROWS.log
 #   prof               rocprofv3 kernel-trace summary of the base bench: TAG_prof/
 #   pmc=MODEL:CLIPS    FETCH_SIZE / WRITE_SIZE passes of the persistent decoder (kernel 14): TAG_pmc_MODEL_CLIPS*
+#   probe=MODEL:CLIPS:NTOK[:beam]  step-logit parity probe (scripts/parity_probe.py): TAG_probe_MODEL_CLIPS.log
 #   ab=ENV1,ENV2,...   bench (base, 1 clip, 10 steps) alternating environments, e.g. ab=WMI_COOP=1,WMI_COOP=0
 #                      (MODEL, CPG, BEAM in the environment select another config): TAG_ab.txt
 # Replaces the one-off drivers of rounds 1-3 (their evidence is under profiles/).
@@ -61,6 +62,10 @@ import json; d=json.load(open('${O}_bench.json')); print('bench', d['value'], d[
           python3 $R/scripts/kernel_probe.py $m 14 3 128 $c > ${O}_pmc_${m}_${c}_trace.log 2>&1) || exit 1
       unset WMI_NO_GRAPH
       cat ${O}_pmc_${m}_${c}_trace.log ;;
+    probe)
+      IFS=: read -ra pa <<< "$arg"
+      timeout -k 10 600 python3 -u scripts/parity_probe.py "${pa[@]}" > ${O}_probe_${pa[0]}_${pa[1]}${pa[3]}.log 2>&1 || exit 1
+      grep "\[probe\]" ${O}_probe_${pa[0]}_${pa[1]}${pa[3]}.log | tail -n 12 ;;
     ab)
       IFS=, read -ra envs <<< "$arg"
       for rep in 1 2; do

@@ -70,10 +70,10 @@ def test_tuning_knobs_are_per_context(wmi, micro_model, monkeypatch):
     thread under a different environment, gets its own."""
     import threading
     monkeypatch.setenv("WMI_LOGITS_CAP", "64")
-    monkeypatch.setenv("WMI_COOP_MAX", "64")
+    monkeypatch.setenv("WMI_GRAPH_STEPS", "4")
     a = wmi.WhisperContext.new(micro_model, 0, max_clips=1)
     monkeypatch.delenv("WMI_LOGITS_CAP")
-    monkeypatch.delenv("WMI_COOP_MAX")
+    monkeypatch.delenv("WMI_GRAPH_STEPS")
     box = {}
     t = threading.Thread(target=lambda: box.update(b=wmi.WhisperContext.new(micro_model, 0, max_clips=1)))
     t.start()
@@ -82,8 +82,8 @@ def test_tuning_knobs_are_per_context(wmi, micro_model, monkeypatch):
     try:
         ka = np.frombuffer(a.debug_read(10, 36), np.int32)
         kb = np.frombuffer(b.debug_read(10, 36), np.int32)
-        assert ka[0] == 64 and ka[5] == 64    # logits_cap, coop_max of the first context
-        assert kb[0] == 512 and kb[5] == 512  # defaults in the second
+        assert ka[0] == 64 and ka[4] == 4    # logits_cap, graph_steps of the first context
+        assert kb[0] == 512 and kb[4] == 8   # defaults in the second
         # and both run to the same numbers
         pcm = synth.synth_pcm_f32(2.0, 5)
         outs = []

@@ -337,6 +337,48 @@ def sharp_hook(name: str, arr: np.ndarray) -> np.ndarray:
     return arr
 
 
+XSHARP_CONV1, XSHARP_PE = 20.0, 3.0
+
+
+def xsharp_hook(name: str, arr: np.ndarray) -> np.ndarray:
+    """The "-xsharp" variants (e.g. "base-xsharp"): a model whose greedy ids
+    follow the audio.  In the plain random model the encoder input is
+    dominated by its sinusoidal positional embedding (conv1 maps the
+    normalised mel to ~0.3 per channel, the embedding is ~0.7), so every
+    clip's encoder output, cross K / V and ids are nearly the same (base,
+    SURVEY clips 1234..1241: 1-2 distinct id sequences).  Here conv1's
+    kernel is x 20, so the mel dominates the encoder, and the decoder's
+    positional embedding x 3 (sigma 0.03) varies the ids along the sequence.
+    With tone clips (synth_pcm_tones) the oracle gives 8 distinct 64-token
+    greedy sequences over seeds 1234..1241 at the plain model's logit noise
+    floor (|ggml order - exact dots| 1.2e-3).  The cross-attention sharpening
+    first tried (query / key x 8, out x 10) made the ids audio-dependent too
+    but chaotic: device and oracle logits 0.2-0.34 apart, free-running ids
+    parting after 2-84 tokens (profiles/r05/xsharp_qk8_probe.log)."""
+    if name == "encoder.conv1.weight":
+        return (arr.astype(np.float32) * XSHARP_CONV1).astype(arr.dtype)
+    if name == "decoder.positional_embedding":
+        return (arr.astype(np.float32) * XSHARP_PE).astype(arr.dtype)
+    return arr
+
+
+LNMEAN_OFFSET = 16.0
+
+
+def lnmean_hook(name: str, arr: np.ndarray) -> np.ndarray:
+    """The "-lnmean" variants: decoder.positional_embedding + 16, so every
+    decoder residual row (token + position embedding, then the layers' sums)
+    has a mean of ~16 over a spread of ~0.02-0.1: |mean| / std up to ~700
+    at the first LayerNorm.  LayerNorm removes the offset, so the model is
+    the plain one up to rounding; it exercises the persistent decoder's
+    one-pass statistics (E[x^2] - mean^2 in double) against the oracle's
+    two-pass ggml norm where cancellation is largest (tests/test_ln_formula.py
+    states the bound, mean^2 / var <= 1e6)."""
+    if name == "decoder.positional_embedding":
+        return (arr.astype(np.float32) + np.float32(LNMEAN_OFFSET)).astype(arr.dtype)
+    return arr
+
+
 def model_path(model: str, cache_dir: str | None = None) -> str:
     """Generate (once) and return the path of a synthetic model file."""
     cache_dir = cache_dir or os.environ.get("WMI_MODEL_CACHE", "/tmp/wmi_models")
@@ -344,7 +386,11 @@ def model_path(model: str, cache_dir: str | None = None) -> str:
     p = os.path.join(cache_dir, f"ggml-synth-{model}.bin")
     if not os.path.exists(p):
         base, _, quant = model.partition("-q")
-        if model.endswith("-sharp"):
+        if model.endswith("-lnmean"):
+            write_ggml(p, model[:-7], tensor_hook=lnmean_hook)
+        elif model.endswith("-xsharp"):
+            write_ggml(p, model[:-7], tensor_hook=xsharp_hook)
+        elif model.endswith("-sharp"):
             write_ggml(p, model[:-6], tensor_hook=sharp_hook)
         elif model.endswith("-f32"):  # e.g. "micro-f32": an ftype-0 (f32) file
             write_ggml(p, model[:-4], quant="f32")
@@ -375,6 +421,20 @@ def pcm_i16_to_f32(s16: np.ndarray) -> np.ndarray:
 
 def synth_pcm_f32(seconds: float = 30.0, seed: int = 1234) -> np.ndarray:
     return pcm_i16_to_f32(synth_pcm_i16(seconds, seed))
+
+
+def synth_pcm_tones(seconds: float = 30.0, seed: int = 1234) -> np.ndarray:
+    """Clips whose content differs with the seed (the SURVEY §8d clips share
+    their tones and differ only in the noise): two tones at seed-drawn
+    frequencies (150-600 Hz, amplitude-modulated at 0.2-2 Hz, and 0.8-3 kHz)
+    plus the same 0.05 N(0, 1) noise; int16-quantised, then s / 32768."""
+    n = int(round(seconds * SAMPLE_RATE))
+    t = np.arange(n, dtype=np.float64) / SAMPLE_RATE
+    rng = np.random.default_rng(seed)
+    f1, f2 = rng.uniform(150, 600), rng.uniform(800, 3000)
+    am = 0.5 + 0.5 * np.sin(2 * np.pi * rng.uniform(0.2, 2) * t)
+    x = 0.4 * np.sin(2 * np.pi * f1 * t) * am + 0.2 * np.sin(2 * np.pi * f2 * t) + 0.05 * rng.standard_normal(n)
+    return pcm_i16_to_f32(np.round(np.clip(x, -1.0, 1.0) * 32767).astype(np.int16))
 
 
 def write_wav(path: str, s16: np.ndarray, sr: int = SAMPLE_RATE) -> None:

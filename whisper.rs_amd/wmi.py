@@ -392,6 +392,14 @@ class WhisperContext:
         _raise(lib().wmi_debug_read(self._h, which, buf, nbytes), self._h)
         return buf.raw
 
+    def step_logits(self, n_pos: int) -> np.ndarray:
+        """Every position's logits of the last persistent greedy decode,
+        [n_pos][8 rows][V] (contexts created with WMI_LOGITS_ALL=1: position
+        p's logits predict the token after the one fed at p)."""
+        V = self.hparams["n_vocab"]
+        raw = self.debug_read(13, n_pos * 8 * V * 4)
+        return np.frombuffer(raw, np.float32).reshape(n_pos, 8, V).copy()
+
     # --- parity getters -----------------------------------------------------
     def mel(self, clip: int = 0) -> np.ndarray:
         nm, nl = C.c_int32(), C.c_int32()
