@@ -273,9 +273,11 @@ def measure_config(wmi, name, model, clips, beam, steps, warmup, n_decode, devic
         ctx.stage([synth.synth_pcm_f32(30.0, sd) for sd in clip_seeds(0, clips)])
         for _ in range(warmup):
             ctx.run_staged(n_decode=n_decode, beam_size=beam)
+            ctx.tokens()
         t0 = time.perf_counter()
         for _ in range(steps):
             ctx.run_staged(n_decode=n_decode, beam_size=beam)
+            ctx.tokens()  # (ids on the host, as the headline step)
         el = time.perf_counter() - t0
         tm = ctx.timings()
         hp = ctx.hparams
@@ -360,7 +362,9 @@ def run_rank(args, rank: int, world: int, local: int) -> None:
         def step():
             ctx.run_staged(n_decode=args.n_decode, beam_size=args.beam)
             if world > 1:
-                ctx.dist_gather_tokens()
+                ctx.dist_gather_tokens()  # every rank's ids to rank 0's host (ncclGather, then D2H)
+            else:
+                ctx.tokens()  # the ids the caller consumes, on the host (wmi_get_tokens: D2H)
 
     for i in range(args.warmup):
         step()
@@ -411,7 +415,8 @@ def run_rank(args, rank: int, world: int, local: int) -> None:
             "parallelism": (f"{world} replicas (one process per GPU), RCCL gather of token ids" if world > 1
                             else "1 GPU"),
             "input": ("PCM staged in HBM before the timed region (wmi_stage_pcm; ~1.9 MB H2D per clip excluded, "
-                      "about 0.03 ms at PCIe Gen5 rates); token ids stay on the device at world 1"),
+                      "about 0.03 ms at PCIe Gen5 rates); every step ends with the token ids on the host "
+                      "(world 1: wmi_get_tokens; world > 1: the RCCL gather to rank 0)"),
         },
         "rank_ms": [round(s * 1e3, 3) for s in rank_s],
         "rendezvous": f"tcp {os.environ.get('MASTER_ADDR', '127.0.0.1')}" if world > 1 else None,

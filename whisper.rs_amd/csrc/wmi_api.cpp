@@ -285,17 +285,13 @@ struct wmi_context {
     bool use_persist = true;          // WMI_PERSIST=0: kernel chain instead
     int persist_q5 = -1;              // WMI_PERSIST_Q5: 0 = decoder GEMVs on the f16 copies (default: q5_1 blocks)
     bool persist_logits = false;      // WMI_PERSIST_LOGITS=1: also store every step's logits (dlogits)
+    // WMI_LOGITS_ALL=1 (parity tests): the persistent greedy launches keep
+    // every position's logits, [n_text_ctx][DEC_ROWS][V] f32 (debug read 13)
+    float *d_lgall = nullptr;
     int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
     int enc_layers = 0;               // WMI_ENC_LAYERS (debug): run only the first encoder layers
     int fault_inject = 0;             // WMI_FAULT_INJECT=1 (test): the first persistent launch runs with one
                                       // workgroup missing (PersistArgs::stall_wg): the device abort path
-    // WMI_COOP=1: launch the persistent grid through hipLaunchCooperativeKernel
-    // (the runtime re-checks co-residency at every launch).  Off by default:
-    // it measured slower — base 1591/1598 vs 1574/1583 audio-s/s (one launch
-    // per decode: ~0.15 ms a launch), C5 116.5 vs 115.5 (one launch per beam
-    // step: ~17 us each), profiles/r04/coop_launch_ab.txt — and the grid is
-    // checked against the occupancy API at context creation instead (grid_nsb)
-    bool persist_coop = false;
     // WMI_VREG=0: stream the one-row logits' non-resident vocabulary tiles every step
     bool persist_vreg = true;
     bool use_xshare = true;           // WMI_XSHARE=0: beam rows read the cross K / V per row
@@ -1702,7 +1698,10 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     // always within the exchange block's task table
     // beam launches of n > 768 (cross q from the D phase) share one task per
     // (head, chunk) among the rows (PersistArgs::xshare): only H * nch tasks
-    const int rows_t = ctx->beam_k > 0 && n > 768 && ctx->use_xshare ? 1 : B;
+    // (the shared tasks run on 128-key chunks, one round of the grid: when
+    // H * ceil(T / 128) exceeds G — a smaller grid, a part with fewer CUs —
+    // the launch takes the per-row tasks instead of a rejected configuration)
+    const int rows_t = ctx->beam_k > 0 && n > 768 && ctx->use_xshare && (int64_t)H * ((T + 127) / 128) <= G ? 1 : B;
     int cl = 128;
     while (cl < 512 && ((int64_t)rows_t * H * ((T + cl - 1) / cl) > G || (int64_t)B * H * ((T + cl - 1) / cl) > PX_TASKS))
         cl += 128;
@@ -1715,14 +1714,14 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     a.cur_tok = ctx->d_curtok; a.suppress_id = suppress_eot ? ctx->sp.eot : -1;
     a.xg = ctx->d_xg; a.err = ctx->derr;
     a.nres = ctx->persist_nres[B];
-    a.coop = ctx->persist_coop ? 1 : 0;
     a.vreg = ctx->persist_vreg ? 1 : 0;
     a.stall_wg = -1;
     if (ctx->fault_inject == 1) {  // once per context: its first persistent launch
         a.stall_wg = G - 1;
         ctx->fault_inject = 2;
     }
-    a.logits_out = ctx->persist_logits ? ctx->dlogits : nullptr;
+    a.logits_out = ctx->d_lgall ? ctx->d_lgall : ctx->persist_logits ? ctx->dlogits : nullptr;
+    a.lg_stride = ctx->d_lgall ? (int64_t)DEC_ROWS * hp.n_vocab : 0;
     // q5_1 blocks in the persistent GEMVs (the ggml dequant x activation
     // product of a q5_1 file), dequantised inside each phase's poll so the
     // VALU overlaps the seam: small q5_1, one clip 43.1 ms decode vs 42.0 ms
@@ -1745,7 +1744,7 @@ void split_second(wmi_context *ctx, PersistArgs &p1, int B1, int Gh) {
     p1.kcache = ctx->kcache + B1 * row;
     p1.vcache = ctx->vcache + B1 * row;
     p1.cur_tok = ctx->d_curtok + B1;
-    if (p1.logits_out) p1.logits_out += (size_t)B1 * ctx->hp.n_vocab;
+    if (p1.logits_out) p1.logits_out += (size_t)B1 * ctx->hp.n_vocab;  // (within each position's slab)
     p1.nres = (ctx->hp.n_vocab + Gh - 1) / Gh;
 }
 
@@ -1921,6 +1920,7 @@ int run_ts_window(wmi_context *ctx, int clip, const std::vector<int32_t> &prompt
                 pa.n_steps = 1;
                 pa.out_stride = 0;
                 pa.logits_out = ctx->dlogits;
+                pa.lg_stride = 0;
                 pa.cur_tok = ctx->dts_tok;
                 HIPCHK(ctx, launch_dec_persist(ctx->stream, pa, G));
                 TsArgs ta{};
@@ -2081,7 +2081,8 @@ int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_st
                     pa.cur_tok = ctx->dbstate->tok;
                     pa.kv_src = ctx->dkvsrc;
                     pa.kv_src_stride = hp.n_text_ctx;
-                    pa.logits_out = ctx->dlogits;
+                    pa.logits_out = ctx->dlogits;  // (the beam kernels read this step's [K][V])
+                    pa.lg_stride = 0;
                     pa.tokens_out = ctx->dtokens;  // (unused: no argmax in beam mode)
                     // WMI_PTRACE: step s of clip 0 stamps slot s (its phase A
                     // then includes the launch gap and the beam kernels)
@@ -2248,7 +2249,6 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (const char *e = getenv("WMI_PERSIST_Q5")) ctx->persist_q5 = atoi(e) ? 1 : 0;
     if (const char *c = getenv("WMI_CHECKSUMS")) ctx->checksums = atoi(c) != 0;
     if (const char *c = getenv("WMI_FAULT_INJECT")) ctx->fault_inject = atoi(c) ? 1 : 0;
-    if (const char *c = getenv("WMI_COOP")) ctx->persist_coop = atoi(c) != 0;
     if (const char *c = getenv("WMI_VREG")) ctx->persist_vreg = atoi(c) != 0;
     if (const char *c = getenv("WMI_XSHARE")) ctx->use_xshare = atoi(c) != 0;
     if (const char *c = getenv("WMI_SPLIT_ROWS")) ctx->split_rows = atoi(c);
@@ -2256,6 +2256,11 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (const char *c = getenv("WMI_DEC_LAYERS")) ctx->dec_layers = std::max(1, std::min(atoi(c), ctx->hp.n_text_layer));
     ctx->enc_layers = ctx->hp.n_audio_layer;
     if (const char *c = getenv("WMI_ENC_LAYERS")) ctx->enc_layers = std::max(0, std::min(atoi(c), ctx->hp.n_audio_layer));
+    if (const char *c = getenv("WMI_LOGITS_ALL"); c && atoi(c)) {
+        const size_t nb = (size_t)ctx->hp.n_text_ctx * DEC_ROWS * ctx->hp.n_vocab * 4;
+        HIPCHK(ctx.get(), hipMalloc(&ctx->d_lgall, nb));
+        HIPCHK(ctx.get(), hipMemset(ctx->d_lgall, 0, nb));
+    }
     if (getenv("WMI_PTRACE")) {
         const size_t nb = (size_t)hp_ptrace_slots(ctx->hp) * 8;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_ptrace, nb));
@@ -2271,17 +2276,12 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     knob("WMI_LOGITS_CAP", tn.logits_cap, 1);
     knob("WMI_LOGITS_G", tn.logits_g, 0);
     knob("WMI_GRAPH_STEPS", tn.graph_steps, 1);
-    knob("WMI_DOWN_NW1_B", tn.down_nw1_b, 0);
-    knob("WMI_LOGITS_CAP2", tn.logits_cap2, 1);
     if (const char *c = getenv("WMI_GEMV_NW")) tn.gemv_nw = atoi(c) == 1 ? 1 : atoi(c) == 0 ? 0 : 4;
-    knob("WMI_COOP_MAX", tn.coop_max, 1);
     knob("WMI_XATTN_ROWS", tn.xattn_rows, 0);
-    knob("WMI_SELF_SPLIT", tn.self_split, 0);
     knob("WMI_ENC_ATTN_NW", tn.enc_attn_nw, 0);
     knob("WMI_GEMM_G", tn.gemm_g, 0);
     knob("WMI_GEMM_EPI", tn.epi_staged, 0);
     knob("WMI_MEL_G", tn.mel_g, 0);
-    knob("WMI_GEMM_G_MIN", tn.gemm_g_min, 1);
     if (getenv("WMI_TRACE")) {
         ctx->trace_on = true;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_trace, TRACE_SLOTS * 16 + 64 * 16 * 8));
@@ -2310,6 +2310,7 @@ void wmi_free(wmi_context *ctx) {
     if (ctx->d_players) (void)hipFree(ctx->d_players);
     if (ctx->d_expfb) (void)hipFree(ctx->d_expfb);
     if (ctx->d_ptrace) (void)hipFree(ctx->d_ptrace);
+    if (ctx->d_lgall) (void)hipFree(ctx->d_lgall);
     for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
@@ -2562,6 +2563,7 @@ static int wmi_decode_logits_impl(wmi_context *ctx, int clip, const int32_t *tok
             PersistArgs pa = persist_args(ctx, clip, 1, G, n_tokens, n_tokens, 0, 1);
             pa.n_steps = 1;
             pa.logits_out = ctx->dlogits;
+            pa.lg_stride = 0;
             pa.out_stride = 0;  // teacher forcing: record no token (dtokens holds staged results)
             HIPCHK(ctx, launch_dec_persist(ctx->stream, pa, G));
         } else {
@@ -2851,11 +2853,14 @@ int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes) {
         case 9: src = ctx->dopart; have = R * (size_t)ctx->n_chunks_max * n * 4; break;
         case 10: {  // host: this context's tuning knobs (struct Tune, int32 fields in order)
             const Tune &t = ctx->tune;
-            const int32_t v[9] = {t.logits_cap, t.logits_g, t.logits_cap2, t.down_nw1_b, t.gemv_nw,
-                                  t.coop_max, t.xattn_rows, t.self_split, t.graph_steps};
+            const int32_t v[9] = {t.logits_cap, t.logits_g, t.gemv_nw, t.xattn_rows, t.graph_steps,
+                                  t.enc_attn_nw, t.gemm_g, t.mel_g, t.epi_staged};
             memcpy(out, v, std::min(sizeof v, bytes));
             return WMI_OK;
         }
+        case 13:  // WMI_LOGITS_ALL: every position's logits [n_text_ctx][8][V]
+            if (!ctx->d_lgall) return WMI_E_INVALID_ARG;
+            src = ctx->d_lgall; have = (size_t)ctx->hp.n_text_ctx * R * ctx->hp.n_vocab * 4; break;
         case 12: src = ctx->h; have = (size_t)ctx->enc_clips * ctx->enc_T * ctx->hp.n_audio_state * 4; break;  // encoder residual stream
         case 11: {  // host: decodes re-run on the kernel chain after a persistent exchange timeout
             const int32_t v = ctx->n_fallbacks;

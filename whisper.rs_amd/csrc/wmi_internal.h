@@ -31,7 +31,6 @@ hipError_t launch_mel_frames(hipStream_t s, const MelTables *tabs, const float *
                              const int64_t *n_len, int64_t max_len, uint32_t *mel_max, int n_clips,
                              const float *filt_c /* compact bank (wmi_api.cpp), or null: LDS copy of filt_t */, int n_fc);
 constexpr int MEL_FC_MAX = 4096;  // floats of the compact filterbank k_mel_frames keeps in LDS
-// clamp_and_normalize in place on mel.
 // the state a decode run starts from, in one launch instead of a host copy
 // and five memsets (each a separate ~5 us fill kernel): zero `n` byte ranges
 // (4-byte aligned, sizes multiple of 4) and write feed[0..n_feed) to dfeed
@@ -44,6 +43,7 @@ struct ResetArgs {
     int32_t feed[64];
 };
 hipError_t launch_dec_reset(hipStream_t s, const ResetArgs &a);
+// clamp_and_normalize in place on mel.
 hipError_t launch_mel_norm(hipStream_t s, float *mel, int64_t mel_stride, int n_mel, const int64_t *n_len,
                            int64_t max_len, const uint32_t *mel_max, int n_clips);
 // mel window (main.rs:1816-1833) -> conv1 input, f16 time-major, zero-padded
@@ -73,19 +73,21 @@ enum GemmEpi {
 struct Tune {
     int logits_cap = 512;   // WMI_LOGITS_CAP: chain logits grid cap
     int logits_g = 2;       // WMI_LOGITS_G: logits rows per lane group
-    int logits_cap2 = 1024; // WMI_LOGITS_CAP2
-    int down_nw1_b = 0;     // WMI_DOWN_NW1_B: MLP-down GEMV with one wave per WG up to this many rows
     int gemv_nw = 4;        // WMI_GEMV_NW: waves per decoder GEMV workgroup (1, 4; 0 auto)
-    int coop_max = 512;     // WMI_COOP_MAX: cooperative cross-attention up to this many workgroups
     int xattn_rows = 1;     // WMI_XATTN_ROWS: beam rows share cross-attention phase A (1 auto, 2 always, 0 never)
-    int self_split = 1;     // WMI_SELF_SPLIT: self-attention output projection over n / 128 WGs per head
     int graph_steps = 8;    // WMI_GRAPH_STEPS: chain decoder steps per captured graph
     int enc_attn_nw = 0;    // WMI_ENC_ATTN_NW: 32-query blocks (two waves each) per k_attn_enc4 workgroup (0 auto, 1, 2, 4)
     int gemm_g = 1;         // WMI_GEMM_G: large-M encoder GEMMs on k_gemm_g (LDS-DMA staging); 0: k_gemm
-    int gemm_g_min = 240;   // WMI_GEMM_G_MIN: 128 x 128 tiles from which k_gemm_g takes a GEMM
-    int mel_g = 1;          // WMI_MEL_G: mel frames as 8 one-frame waves, filterbank from global (0: 4 two-frame waves, LDS copy)
+    // WMI_MEL_G=0: the dense-filterbank mel layout (4 two-frame waves, LDS
+    // copy of the whole [201][n_mel] bank) that a file whose bank has more
+    // than MEL_FC_MAX non-zero weights takes anyway; tested bitwise equal
+    int mel_g = 1;
     int epi_staged = 1;     // WMI_GEMM_EPI: GEMM epilogues through LDS, 16 / 8-byte stores (0: per-lane 2 / 4-byte stores)
 };
+// (fixed since round 5; their alternatives measured slower and are removed:
+// chain logits grid cap at K <= 512, cooperative chain cross-attention up to
+// 512 workgroups, k_gemm_g from 240 128 x 128 tiles)
+constexpr int CHAIN_LOGITS_CAP2 = 1024, CHAIN_COOP_MAX = 512, GEMM_G_MIN_TILES = 240;
 extern const Tune kTuneDefault;
 inline const Tune &tune_of(const Tune *t) { return t ? *t : kTuneDefault; }
 
@@ -372,6 +374,7 @@ struct PersistArgs {
     unsigned long long *ptrace;  // WMI_PTRACE: [n_steps][L + 1][16][2] phase-end clocks, or null
     int nres;                    // vocabulary rows per workgroup resident in LDS
     float *logits_out;           // [B][V] logits of every step (debug / teacher forcing), or null
+    int64_t lg_stride;           // > 0: position p's logits at logits_out + p * lg_stride (all-step capture)
     // beam search (one step per launch; the beam kernels select between launches):
     // rows are the beam slots of clip b0, step 0 feeds cur_tok (the beam state's
     // tokens), self-attention keys j < pos come from cache row kv_src[b][j], and
@@ -389,12 +392,10 @@ struct PersistArgs {
     // poll of its rows runs into the bounded spin, raises the abort word and
     // err bit 3, and the grid drains (-1: none)
     int stall_wg;
-    // host side: launch through hipLaunchCooperativeKernel (the runtime then
-    // checks the grid against the device's co-residency limit at launch)
-    int coop;
-    // one-row MFMA logits (n <= 512): the vocabulary tiles that do not fit the
-    // LDS stay in registers for the whole launch instead of streaming every
-    // step (0: streamed; the kernel streams them anyway past 8 tiles)
+    // one-row VALU logits (n = 768): the vocabulary rows past the LDS-resident
+    // ones stay in registers for the whole launch (an 8-pass WSet per
+    // quarter-wave slot, at most 128 rows a workgroup) instead of streaming
+    // every step (0: streamed; past 128 rows the kernel streams them anyway)
     int vreg;
 };
 hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G);

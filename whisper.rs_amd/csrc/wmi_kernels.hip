@@ -863,7 +863,7 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a0) {
     // large M: the LDS-DMA kernel (bitwise the same outputs)
     // (8-clip encoder 3.10 -> 3.00 ms: conv2 84.6 -> 71.3, Wo 39.7 -> 34.8,
     // mlp.2 77.0 -> 60.2 us; QKV and mlp.0 unchanged)
-    if (t128 >= tune_of(a.tune).gemm_g_min && tune_of(a.tune).gemm_g && a.K % 64 == 0 && (!a.conv || a.conv_cp % 64 == 0))
+    if (t128 >= GEMM_G_MIN_TILES && tune_of(a.tune).gemm_g && a.K % 64 == 0 && (!a.conv || a.conv_cp % 64 == 0))
         return a.conv ? gemm_g_dispatch<true>(s, epi, a) : gemm_g_dispatch<false>(s, epi, a);
     if (a.conv) {
         if (t128 >= 240) return gemm_dispatch_epi<128, 128, GBK, true>(s, epi, a);
@@ -1274,17 +1274,13 @@ __device__ __forceinline__ void ln_regs_to_lds(const float4 (&xv)[L], int K, con
 
 // NC = 128-element K chunks a lane prefetches per row (8 for K <= 1024, 16 for
 // the MLP-down GEMV at K = 4n <= 2048); longer rows loop.
-// decoder weight stream loads: WMI_NT builds use the non-temporal policy
-// (weights each CU reads once per step; MI355X_MICROARCH.md nt-weights)
+// decoder weight stream loads (plain loads: the non-temporal policy was
+// measured and removed in round 5)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 template <typename T>
 __device__ __forceinline__ T wload(const T *p) {
-#ifdef WMI_NT
-    return __builtin_nontemporal_load(p);
-#else
     return *p;
-#endif
 }
 __device__ __forceinline__ uint4 wload(const uint4 *p) {
     const u32x4 v = wload((const u32x4 *)p);
@@ -1611,7 +1607,7 @@ static hipError_t dec_gemv_nw(hipStream_t s, const DecGemvArgs &a) {
         // (128 VGPRs at G = 2: four workgroups per CU, hence the larger cap;
         // a balanced grid of equal row-group counts measured slower)
         const int G = tn.logits_g == 2 ? 2 : 4, ng = cdiv(a.N, 4 * NW * G);
-        const dim3 grid2(ng < tn.logits_cap2 ? ng : tn.logits_cap2);
+        const dim3 grid2(ng < CHAIN_LOGITS_CAP2 ? ng : CHAIN_LOGITS_CAP2);
         if (G == 2) {
             hipError_t e = allow_lds(k_dec_gemv<EPI, IN, 2, 4, 0, NW>, lds);
             if (e != hipSuccess) return e;
@@ -1636,11 +1632,8 @@ static hipError_t dec_gemv_g(hipStream_t s, const DecGemvArgs &a) {
     if constexpr (EPI == DEC_LOGITS) {
         return dec_gemv_nw<EPI, IN, WQ, 4>(s, a);
     } else {
-        // the MLP down projection (K = 4n, no LayerNorm) streams 4x the bytes
-        // per row: one wave per workgroup spreads them over 4x the CUs
         const Tune &tn = tune_of(a.tune);
-        const bool down = EPI == DEC_RESID && IN == 1 && a.K > 1024 && a.B <= tn.down_nw1_b;
-        const bool one = down || tn.gemv_nw == 1 || (tn.gemv_nw == 0 && a.B <= 2);
+        const bool one = tn.gemv_nw == 1 || (tn.gemv_nw == 0 && a.B <= 2);
         return one ? dec_gemv_nw<EPI, IN, WQ, 1>(s, a) : dec_gemv_nw<EPI, IN, WQ, 4>(s, a);
     }
 }
@@ -2245,7 +2238,7 @@ hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
     if (a.M_fixed == 0) {  // self-attention: M = pos + 1 <= 512
         if (a.n_chunks != 1 || (a.Wo && !a.wo_parts)) return hipErrorInvalidValue;
         // fused output projection split over n / 128 workgroups per head
-        const int S = (tn.self_split && a.Wo && a.n % 128 == 0) ? a.n / 128 : 1;
+        const int S = (a.Wo && a.n % 128 == 0) ? a.n / 128 : 1;
         const dim3 grid(a.H, a.B, S);
         switch (a.mk) {
             case 64: hipLaunchKernelGGL(k_dec_self_attn<64>, grid, dim3(256), 0, s, a); break;
@@ -2271,7 +2264,7 @@ hipError_t launch_dec_attn(hipStream_t s, const DecAttnArgs &a) {
     // cooperative single kernel while the grid stays far inside residency
     // (<= 2 workgroups per CU) and the Wq rows fit the register budget;
     // otherwise the two-kernel form
-    const bool coop = a.sync && a.n_chunks * a.H * a.B <= tn.coop_max && a.n <= 768;
+    const bool coop = a.sync && a.n_chunks * a.H * a.B <= CHAIN_COOP_MAX && a.n <= 768;
     // beam rows sharing one clip: phase A once per (chunk, head) for all rows
     // (auto: n > 768, where the head's Wq rows dominate a workgroup's reads —
     // large-v3 x 5 beams 498 -> 448 ms decode; small x 5 beams is faster per

@@ -55,13 +55,17 @@ constexpr uint32_t PSPIN = 1u << 19;    // polls before a seam is declared dead
 constexpr int NPH = 11;                 // phases per decoder layer
 constexpr int PMAXB = 8;                // decoder rows
 constexpr int RNMAX = 16;               // rows of an n-row GEMV per workgroup
-// attention / argmax scratch in LDS: one-row instances use at most ~14.3 KB
-// (LDS K/V self-attention), so they keep 8 KB more vocabulary rows resident
+// attention / argmax scratch in LDS.  One-row instances use at most ~3 KB
+// (a cross task's q and p values, G1's sub-chunk partials, the argmax
+// candidates [G][2]); the multi-row ones also keep the beam-shared task's
+// [B][4][64] P.V partials (from XS_OFF + XS_BYTES) and the MFMA GEMV
+// partials, so the one-row instances keep 8 KB more vocabulary rows resident
 __host__ __device__ constexpr int scr_bytes(int BT) { return BT == 1 ? 16 * 1024 : 24 * 1024; }
 constexpr int NKP = 4;                  // 128-key passes per cross-attention chunk (cl <= 512)
 constexpr int EXPFB = 64;               // exp fallback list entries (exp_f16_fast)
 constexpr int XS_OFF = 1024;            // cross-attention task scores / p in the LDS scratch
-constexpr int XS_BYTES = 8192;          // (workgroup tasks x keys per task x 4 B)
+constexpr int XS_BYTES = 8192;          // (a task's p values: rows x keys x 4 B)
+constexpr int NSUBM = 16;               // 128-key sub-chunks of a row (T <= 2048)
 
 __device__ __forceinline__ uint64_t gld(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -122,8 +126,8 @@ struct PShared {
     int32_t tok[PMAXB];
     float redf[4];
     double redd[4], redd2[4];
-    float redfb[PMAXB][4];   // beam-shared cross tasks: per-row wave maxima
-    double reddb[PMAXB][4];  // and per-row wave sums
+    float redfb[PMAXB][4];   // cross tasks: per (row or sub-chunk, wave) score maxima
+    double reddb[PMAXB][4];  // and exp sums
     unsigned long long best[4][PMAXB];
     float ored[4][64 * 4];  // per wave: up to NKP 64-float partials
     __attribute__((aligned(16))) uint32_t expfb[EXPFB];  // exp fallback list (exp_f16_fast)
@@ -920,12 +924,10 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     // and a tile's B fragments of all of K would not fit the registers)
     constexpr bool LMF2 = !LMF && BT > 1;
     constexpr bool XQF = KC <= 6;  // cross q computed inside the score tasks (registers allow)
-    // cross-attention softmax: several rows (8 clips, beam slots) split it in
-    // two small hand-offs (chunk maxima, then chunk exp sums; each task's
-    // scores stay in LDS) instead of every task sweeping its row's T scores;
-    // one row keeps the single hand-off (one seam fewer: 140.8 vs 142.2 us
-    // per base step, profiles/r03/ptrace_fsplit.log)
-    constexpr bool FSPLIT = BT > 1;
+    // 128-key sub-chunks per cross-attention task: one row runs 128-key
+    // chunks (H * ceil(T / 128) <= G tasks; 256 on a smaller grid), several
+    // rows up to 512 (launch_dec_persist checks)
+    constexpr int NKE = BT == 1 ? 2 : NKP;
     // beam rows share one clip's cross K / V tasks (PersistArgs::xshare)
     const bool xsh = BEAM && !XQF && a.xshare;
     // split-K factors of the GEMV phases (quarter-waves per row), from the
@@ -950,11 +952,11 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
     f16 *vres = (f16 *)(scr + scr_bytes(BT));                              // [nres][NS] resident vocabulary rows
     // exchange offsets as plain scalars (a struct captured by the lambdas
     // below would be kept in scratch memory)
-    int oX1, oX2, oX3, oQ, oK, oV, oO, oXQ, oOC, oH, oS, oM, oP, oA;
+    int oX1, oX2, oX3, oQ, oK, oV, oO, oXQ, oOC, oH, oS, oP, oA;
     {
         const XLayout X = persist_layout(NS, H, T);
         oX1 = X.x1; oX2 = X.x2; oX3 = X.x3; oQ = X.q; oK = X.k; oV = X.v; oO = X.o; oXQ = X.xq;
-        oOC = X.oc; oH = X.h; oS = X.s; oM = X.m; oP = X.p; oA = X.a;
+        oOC = X.oc; oH = X.h; oS = X.s; oP = X.p; oA = X.a;
     }
     uint64_t *xg = a.xg;
     uint32_t *abortw = (uint32_t *)(xg + persist_layout(NS, H, T).ctl);
@@ -1211,24 +1213,24 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     __syncthreads();
                     mx = fmaxf(fmaxf(sh.redf[0], sh.redf[1]), fmaxf(sh.redf[2], sh.redf[3]));
                 PSTAMP(l * 32 + 14)
+                    // p = the ggml exp-table value of f16(s - max) (an f16
+                    // value: stored exactly), and its double sum (exact in any
+                    // order); P.V takes p unnormalised and the sum divides the
+                    // result (ggml rounds f16(p / sum) first: the weights
+                    // differ by that rounding, one barrier fewer)
                     double sum = 0.0;
-                    float p[2];
 #pragma unroll
                     for (int r = 0; r < 2; ++r) {
-                        p[r] = 0.0f;
                         if (tid + 256 * r < M) {
-                            p[r] = exp_f16_hash(sc[r] - mx, sh.expfb, fbk);
-                            sum += (double)p[r];
+                            const float pr = exp_f16_hash(sc[r] - mx, sh.expfb, fbk);
+                            sum += (double)pr;
+                            P16[tid + 256 * r] = f2h_bits(pr);
                         }
                     }
                     sum = wave_sum(sum);
                     if (lane == 0) sh.redd[w] = sum;
                     __syncthreads();
-                    const float inv = (float)(1.0 / (((sh.redd[0] + sh.redd[1]) + sh.redd[2]) + sh.redd[3]));
-#pragma unroll
-                    for (int r = 0; r < 2; ++r)
-                        if (tid + 256 * r < M) P16[tid + 256 * r] = f2h_bits(p[r] * inv);
-                    __syncthreads();
+                    const double inv = 1.0 / (((sh.redd[0] + sh.redd[1]) + sh.redd[2]) + sh.redd[3]);
                 PSTAMP(l * 32 + 31)
                     // P.V in key order: rows past pos are zero registers and
                     // add exact zeros (o is never -0), so this step's row —
@@ -1266,7 +1268,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         const int d = 2 * tid;
                         const float o0 = ((sh.ored[0][d] + sh.ored[1][d]) + sh.ored[2][d]) + sh.ored[3][d];
                         const float o1 = ((sh.ored[0][d + 1] + sh.ored[1][d + 1]) + sh.ored[2][d + 1]) + sh.ored[3][d + 1];
-                        gput(xg + oO + b * (NS / 2) + h * 32 + tid, tag, pack2(o0, o1));
+                        gput(xg + oO + b * (NS / 2) + h * 32 + tid, tag, pack2((float)(o0 * inv), (float)(o1 * inv)));
                     }
                 }
             }
@@ -1328,533 +1330,316 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }
 
             PSTAMP(l * 32 + 3)
-            // beam search (rows = hypotheses of one clip, cross q from D): one
-            // task per (head, key chunk) covers every row, so each K / V chunk
-            // is read once a step (the per-row tasks read it once per row); a
-            // row's arithmetic is the per-row task's, in the same order
-            if (xsh) {
-                PHASE_IDS
-                const uint32_t tag = ptag(pos, L, l, 4);
-                f16 *qb = (f16 *)scr;  // [B][64] this head's cross q of every row
-                const int ntask = H * nch;
-                for (int t = wg, k = 0; t < ntask; t += G) {
-                    const int c = t % nch, h = t / nch;
-                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
-                    float *st = (float *)(scr + XS_OFF) + (k++) * (B * CL);  // [B][CL]
-                    const f16 *Kb = (const f16 *)a.ck + ((int64_t)l * a.Bt + a.b0) * T * NS + h * 64 + (tid & 1) * 32;
-                    half8 kf[NKP][4];
-                    const half8 z8 = {};
-#pragma unroll
-                    for (int p = 0; p < NKP; ++p) {
-                        int key = j0 + 128 * p + (tid >> 1);
-                        key = key < j1 ? key : j1 - 1;
-#pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            kf[p][i] = 128 * p < CL ? sld((const half8 *)(Kb + (int64_t)key * NS + 8 * i)) : z8;
-                    }
-                    PREFETCH_ISSUED
-                    __syncthreads();
-                    const bool ok = gpoll(B * 32, ptag(pos, L, l, 3),
-                                          [=](int i) { return xg + oXQ + (i >> 5) * (NS / 2) + h * 32 + (i & 31); },
-                                          (uint32_t *)qb, abortw, a.err);
-                    if (check(ok)) return;
-                PSTAMP(l * 32 + 20)
-                    // (rows unrolled: their dot chains and max reductions interleave)
-                    float mb[PMAXB];
-#pragma unroll
-                    for (int b = 0; b < PMAXB; ++b) {
-                        mb[b] = -INFINITY;
-                        if (b >= B) continue;
-#pragma unroll
-                        for (int p = 0; p < NKP; ++p)
-                            if (j0 + 128 * p < j1) {
-                                const int key = j0 + 128 * p + (tid >> 1);
-                                float sv = 0.0f;
-#pragma unroll
-                                for (int i = 0; i < 4; ++i)
-                                    sv = dot8(kf[p][i], *(const half8 *)(qb + b * 64 + (tid & 1) * 32 + 8 * i), sv);
-                                sv = xstep<XSum, 1>(sv);
-                                if (key < j1) {
-                                    if ((tid & 1) == 0) st[b * CL + key - j0] = sv;
-                                    mb[b] = fmaxf(mb[b], sv);
-                                }
-                            }
-                    }
-#pragma unroll
-                    for (int b = 0; b < PMAXB; ++b)
-                        if (b < B) {
-                            const float m = wave_max(mb[b]);
-                            if (lane == 0) sh.redfb[b][w] = m;
-                        }
-                    __syncthreads();
-                    if (tid < B)
-                        gput(xg + oM + ((int64_t)tid * H + h) * nch + c, tag,
-                             __float_as_uint(fmaxf(fmaxf(sh.redfb[tid][0], sh.redfb[tid][1]),
-                                                   fmaxf(sh.redfb[tid][2], sh.redfb[tid][3]))));
-                }
-            } else
-            // ---- E: cross scores per (row, head, key chunk) ----------------
-            // the scores stay in this workgroup's LDS (task slot k of the
-            // workgroup's tasks t = wg + k G); only the chunk max is published
+            // ---- E: cross attention of (row, head, key chunk), flash-decoding
+            // form.  Per 128-key sub-chunk: the scores s, their max m, p = the
+            // ggml exp-table value of f16(s - m), the double sum S of p (f16
+            // values in [0, 1]: exact in any order) and the unnormalised
+            // o = sum p V; G1 rescales the sub-chunks to the row's max and
+            // divides by the total sum.  One hand-off (E -> G1) where the global
+            // softmax took two (one row: the scores to F) or three (several rows:
+            // chunk maxima, chunk sums); the attention weights differ from
+            // ggml's f16(p / S) only by the rounding of f16(s - m) against the
+            // sub-chunk's max and the un-rounded division.
+            // A sub-chunk's numbers depend only on its keys (one lane layout
+            // whatever the task's chunk CL), so a row's cross o does not depend
+            // on the row count, the chunking, or beam rows sharing a task.
             {
                 PHASE_IDS
-                const uint32_t tag = ptag(pos, L, l, 4);
-                f16 *qh = (f16 *)scr;
-                const int ntask = B * H * nch;
-                for (int t = wg, k = 0; t < ntask; t += G) {
-                    const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
-                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
-                    float *st = (float *)(scr + XS_OFF) + (k++) * CL;
-                    const f16 *Kb = (const f16 *)a.ck + ((int64_t)l * a.Bt + a.b0 + (a.beam ? 0 : b)) * T * NS + h * 64 + (tid & 1) * 32;
-                    half8 kf[NKP][4];
-                    const half8 z8 = {};
+                const uint32_t tag = ptag(pos, L, l, 6);  // (G1 polls this tag)
+                const int doct = tid & 7, jg = tid >> 3;  // P.V layout: 8 dims x 4 keys a lane
+                if (xsh) {
+                    // beam rows sharing one clip (cross q from D): one task per
+                    // (head, 128-key chunk) covers every row, so a step reads
+                    // each K / V chunk once; a row's arithmetic is the per-row
+                    // task's, in the same order (launch_dec_persist: CL = 128)
+                    f16 *qb = (f16 *)scr;                 // [B][64] this head's cross q of every row
+                    float *st = (float *)(scr + XS_OFF);  // [B][128] p
+                    const int ntask = H * nch;
+                    for (int t = wg; t < ntask; t += G) {
+                        const int c = t % nch, h = t / nch;
+                        const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
+                        const int64_t cb = ((int64_t)l * a.Bt + a.b0) * T * NS + h * 64;
+                        const f16 *Kb = (const f16 *)a.ck + cb + (tid & 1) * 32;
+                        const f16 *Vb = (const f16 *)a.cv + cb + doct * 8;
+                        const int key = j0 + (tid >> 1);
+                        half8 kf[4], vf[4];
 #pragma unroll
-                    for (int p = 0; p < NKP; ++p) {
-                        int key = j0 + 128 * p + (tid >> 1);
-                        key = key < j1 ? key : j1 - 1;
+                        for (int i = 0; i < 4; ++i) kf[i] = sld((const half8 *)(Kb + (int64_t)(key < j1 ? key : j1 - 1) * NS + 8 * i));
 #pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            kf[p][i] = 128 * p < CL ? sld((const half8 *)(Kb + (int64_t)key * NS + 8 * i)) : z8;
-                    }
-                    if constexpr (XQF) {
-                        // this head's cross q from x' directly: LNc(x'_b) and
-                        // Wcq rows h*64 .. h*64+63, the D phase's arithmetic
-                        WSet<KC, 4> S;
-                        wset_load(S, wmat(P.wcq), P.bcq, NS, h * 64, h * 64 + 64, slot, l16);
-                        Ln1P<NS> l1;  // (one row: the whole workgroup's LayerNorm from the poll registers)
-                        ln1_params<NS>(P.lnc_w, P.lnc_b, l1, tid);
+                        for (int u = 0; u < 4; ++u) {
+                            const int kv = j0 + jg * 4 + u;
+                            vf[u] = sld((const half8 *)(Vb + (int64_t)(kv < j1 ? kv : j1 - 1) * NS));
+                        }
                         PREFETCH_ISSUED
                         __syncthreads();
-                        if (!poll_ln1<NS>(xg + oX2 + b * NS, ptag(pos, L, l, 2), l1, xf, xs, abortw, a.err, sh.redd, sh.redd2,
-                                          &sh.abort_))
-                            return;
-                PSTAMP(l * 32 + 20)
-                        __syncthreads();
-                PSTAMP(l * 32 + 29)
-                        wset_dot<1>(S, xs, NS, 1, h * 64, h * 64 + 64, slot, l16,
-                                    [&](int row, int, float v, float eb, bool valid) {
-                                        if (valid) qh[row - h * 64] = f16_rt((v + eb) * qs);
-                                    });
-                        __syncthreads();
-                PSTAMP(l * 32 + 30)
-                    } else {
-                        PREFETCH_ISSUED
-                        __syncthreads();
-                        const bool ok = gpoll(32, ptag(pos, L, l, 3),
-                                              [=](int i) { return xg + oXQ + b * (NS / 2) + h * 32 + i; }, (uint32_t *)qh,
-                                              abortw, a.err);
+                        const bool ok = gpoll(B * 32, ptag(pos, L, l, 3),
+                                              [=](int i) { return xg + oXQ + (i >> 5) * (NS / 2) + h * 32 + (i & 31); },
+                                              (uint32_t *)qb, abortw, a.err);
                         if (check(ok)) return;
                 PSTAMP(l * 32 + 20)
+                        // (rows unrolled: their dot chains and max reductions interleave)
+                        float sc[PMAXB];
+#pragma unroll
+                        for (int b = 0; b < PMAXB; ++b) {
+                            sc[b] = 0.0f;
+                            if (b >= B) continue;
+                            float sv = 0.0f;
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) sv = dot8(kf[i], *(const half8 *)(qb + b * 64 + (tid & 1) * 32 + 8 * i), sv);
+                            sv = xstep<XSum, 1>(sv);
+                            sc[b] = sv;
+                            const float m = wave_max(key < j1 ? sv : -INFINITY);
+                            if (lane == 0) sh.redfb[b][w] = m;
+                        }
+                        __syncthreads();
+                        const bool own = key < j1 && (tid & 1) == 0;
+#pragma unroll
+                        for (int b = 0; b < PMAXB; ++b) {
+                            if (b >= B) continue;
+                            const float m = fmaxf(fmaxf(sh.redfb[b][0], sh.redfb[b][1]), fmaxf(sh.redfb[b][2], sh.redfb[b][3]));
+                            const float pj = exp_f16_hash(sc[b] - m, sh.expfb, fbk);
+                            if (own) st[b * 128 + key - j0] = pj;
+                            const double s = wave_sum(own ? (double)pj : 0.0);
+                            if (lane == 0) sh.reddb[b][w] = s;
+                        }
+                        __syncthreads();
+                        float *ob = (float *)(scr + XS_OFF + XS_BYTES);  // [B][4 waves][64]
+#pragma unroll
+                        for (int b = 0; b < PMAXB; ++b) {
+                            if (b >= B) continue;
+                            float o[8];
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) o[e] = 0.0f;
+                            float sp[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const int kv = j0 + jg * 4 + u;
+                                sp[u] = st[b * 128 + (kv < j1 ? kv : j1 - 1) - j0];
+                            }
+                            // keys past the chunk add p = 0 (o + 0 == o: o is never -0)
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const float pj = j0 + jg * 4 + u < j1 ? sp[u] : 0.0f;
+#pragma unroll
+                                for (int e = 0; e < 8; ++e) o[e] = o[e] + pj * (float)vf[u][e];
+                            }
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) o[e] = red_8_16_32(o[e]);
+                            if (lane < 8)
+#pragma unroll
+                                for (int e = 0; e < 8; ++e) ob[(b * 4 + w) * 64 + lane * 8 + e] = o[e];
+                        }
+                        __syncthreads();
+                        for (int i = tid; i < B * 64; i += PT) {
+                            const int b = i >> 6, d = i & 63;
+                            const float *q4 = ob + b * 256 + d;
+                            gput(xg + oP + (((int64_t)b * H + h) * nsub + c) * 64 + d, tag,
+                                 __float_as_uint(((q4[0] + q4[64]) + q4[128]) + q4[192]));
+                        }
+                        if (tid < B) {
+                            const int64_t sb = ((int64_t)tid * H + h) * nsub + c;
+                            const double s = ((sh.reddb[tid][0] + sh.reddb[tid][1]) + sh.reddb[tid][2]) + sh.reddb[tid][3];
+                            gput(xg + oS + 3 * sb, tag,
+                                 __float_as_uint(fmaxf(fmaxf(sh.redfb[tid][0], sh.redfb[tid][1]),
+                                                       fmaxf(sh.redfb[tid][2], sh.redfb[tid][3]))));
+                            gput(xg + oS + 3 * sb + 1, tag, lo32(s));
+                            gput(xg + oS + 3 * sb + 2, tag, hi32(s));
+                        }
                     }
-                    float m = -INFINITY;
+                } else {
+                    f16 *qh = (f16 *)scr;                 // [64] this task's cross q
+                    float *st = (float *)(scr + XS_OFF);  // [NKE][128] p
+                    const int ntask = B * H * nch;
+                    for (int t = wg; t < ntask; t += G) {
+                        const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
+                        const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
+                        const int64_t cb = ((int64_t)l * a.Bt + a.b0 + (a.beam ? 0 : b)) * T * NS + h * 64;
+                        const f16 *Kb = (const f16 *)a.ck + cb + (tid & 1) * 32;
+                        const f16 *Vb = (const f16 *)a.cv + cb + doct * 8;
+                        half8 kf[NKE][4], vf[NKE][4];
+                        const half8 z8 = {};
 #pragma unroll
-                    for (int p = 0; p < NKP; ++p)
-                        if (j0 + 128 * p < j1) {
-                            const int key = j0 + 128 * p + (tid >> 1);
-                            float s = 0.0f;
+                        for (int p = 0; p < NKE; ++p) {
+                            int key = j0 + 128 * p + (tid >> 1);
+                            key = key < j1 ? key : j1 - 1;
 #pragma unroll
-                            for (int i = 0; i < 4; ++i) s = dot8(kf[p][i], *(const half8 *)(qh + (tid & 1) * 32 + 8 * i), s);
-                            s = xstep<XSum, 1>(s);
-                            if (key < j1) {
-                                if ((tid & 1) == 0) {
-                                    if constexpr (FSPLIT) st[key - j0] = s;
-                                    else gput(xg + oS + (int64_t)bh * T + key, tag, __float_as_uint(s));
-                                }
-                                m = fmaxf(m, s);
+                            for (int i = 0; i < 4; ++i)
+                                kf[p][i] = 128 * p < CL ? sld((const half8 *)(Kb + (int64_t)key * NS + 8 * i)) : z8;
+                        }
+#pragma unroll
+                        for (int p = 0; p < NKE; ++p)
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                int kv = j0 + 128 * p + jg * 4 + u;
+                                kv = kv < j1 ? kv : j1 - 1;
+                                vf[p][u] = 128 * p < CL ? sld((const half8 *)(Vb + (int64_t)kv * NS)) : z8;
+                            }
+                        if constexpr (XQF) {
+                            // this head's cross q from x' directly: LNc(x'_b) and
+                            // Wcq rows h*64 .. h*64+63, the D phase's arithmetic
+                            WSet<KC, 4> S;
+                            wset_load(S, wmat(P.wcq), P.bcq, NS, h * 64, h * 64 + 64, slot, l16);
+                            Ln1P<NS> l1;  // (the whole workgroup's LayerNorm of row b from the poll registers)
+                            ln1_params<NS>(P.lnc_w, P.lnc_b, l1, tid);
+                            PREFETCH_ISSUED
+                            __syncthreads();
+                            if (!poll_ln1<NS>(xg + oX2 + b * NS, ptag(pos, L, l, 2), l1, xf, xs, abortw, a.err, sh.redd,
+                                              sh.redd2, &sh.abort_))
+                                return;
+                PSTAMP(l * 32 + 20)
+                            __syncthreads();
+                PSTAMP(l * 32 + 29)
+                            wset_dot<1>(S, xs, NS, 1, h * 64, h * 64 + 64, slot, l16,
+                                        [&](int row, int, float v, float eb, bool valid) {
+                                            if (valid) qh[row - h * 64] = f16_rt((v + eb) * qs);
+                                        });
+                            __syncthreads();
+                PSTAMP(l * 32 + 30)
+                        } else {
+                            PREFETCH_ISSUED
+                            __syncthreads();
+                            const bool ok = gpoll(32, ptag(pos, L, l, 3),
+                                                  [=](int i) { return xg + oXQ + b * (NS / 2) + h * 32 + i; }, (uint32_t *)qh,
+                                                  abortw, a.err);
+                            if (check(ok)) return;
+                PSTAMP(l * 32 + 20)
+                        }
+                        // scores and the sub-chunk maxima
+                        float sc[NKE];
+#pragma unroll
+                        for (int p = 0; p < NKE; ++p) {
+                            sc[p] = 0.0f;
+                            if (j0 + 128 * p < j1) {  // workgroup-uniform
+                                const int key = j0 + 128 * p + (tid >> 1);
+                                float s = 0.0f;
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) s = dot8(kf[p][i], *(const half8 *)(qh + (tid & 1) * 32 + 8 * i), s);
+                                s = xstep<XSum, 1>(s);
+                                sc[p] = s;
+                                const float m = wave_max(key < j1 ? s : -INFINITY);
+                                if (lane == 0) sh.redfb[p][w] = m;
                             }
                         }
-                    m = wave_max(m);
-                    if (lane == 0) sh.redf[w] = m;
-                    __syncthreads();
-                    if (tid == 0)
-                        gput(xg + oM + t, tag,
-                             __float_as_uint(fmaxf(fmaxf(sh.redf[0], sh.redf[1]), fmaxf(sh.redf[2], sh.redf[3]))));
+                        __syncthreads();
+                        // p against the sub-chunk max, its exact double sum
+#pragma unroll
+                        for (int p = 0; p < NKE; ++p)
+                            if (j0 + 128 * p < j1) {
+                                const int key = j0 + 128 * p + (tid >> 1);
+                                const float m = fmaxf(fmaxf(sh.redfb[p][0], sh.redfb[p][1]), fmaxf(sh.redfb[p][2], sh.redfb[p][3]));
+                                const float pj = exp_f16_hash(sc[p] - m, sh.expfb, fbk);
+                                const bool own = key < j1 && (tid & 1) == 0;
+                                if (own) st[key - j0] = pj;
+                                const double s = wave_sum(own ? (double)pj : 0.0);
+                                if (lane == 0) sh.reddb[p][w] = s;
+                            }
+                        __syncthreads();
+                PSTAMP(l * 32 + 11)
+                        // unnormalised P.V per 128-key sub-chunk
+                        float o[NKE][8];
+#pragma unroll
+                        for (int p = 0; p < NKE; ++p)
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) o[p][e] = 0.0f;
+#pragma unroll
+                        for (int p = 0; p < NKE; ++p)
+                            if (j0 + 128 * p < j1) {  // workgroup-uniform
+                                float sp[4];
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    const int kv = j0 + 128 * p + jg * 4 + u;
+                                    sp[u] = st[(kv < j1 ? kv : j1 - 1) - j0];
+                                }
+                                // keys past the chunk add p = 0 (o + 0 == o: o is never -0)
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    const float pj = j0 + 128 * p + jg * 4 + u < j1 ? sp[u] : 0.0f;
+#pragma unroll
+                                    for (int e = 0; e < 8; ++e) o[p][e] = o[p][e] + pj * (float)vf[p][u][e];
+                                }
+                            }
+#pragma unroll
+                        for (int p = 0; p < NKE; ++p)
+                            if (j0 + 128 * p < j1)
+#pragma unroll
+                                for (int e = 0; e < 8; ++e) o[p][e] = red_8_16_32(o[p][e]);
+                        if (lane < 8)
+#pragma unroll
+                            for (int p = 0; p < NKE; ++p)
+                                if (j0 + 128 * p < j1)
+#pragma unroll
+                                    for (int e = 0; e < 8; ++e) sh.ored[w][p * 64 + lane * 8 + e] = o[p][e];
+                        __syncthreads();
+                PSTAMP(l * 32 + 13)
+                        const int nsp = (j1 - j0 + 127) >> 7;  // sub-chunks of this task
+                        const int64_t sb = (int64_t)bh * nsub + (j0 >> 7);
+                        if (tid < 64 * nsp)
+                            gput(xg + oP + sb * 64 + tid, tag,
+                                 __float_as_uint(((sh.ored[0][tid] + sh.ored[1][tid]) + sh.ored[2][tid]) + sh.ored[3][tid]));
+                        if (tid < nsp) {
+                            const double s = ((sh.reddb[tid][0] + sh.reddb[tid][1]) + sh.reddb[tid][2]) + sh.reddb[tid][3];
+                            gput(xg + oS + 3 * (sb + tid), tag,
+                                 __float_as_uint(fmaxf(fmaxf(sh.redfb[tid][0], sh.redfb[tid][1]),
+                                                       fmaxf(sh.redfb[tid][2], sh.redfb[tid][3]))));
+                            gput(xg + oS + 3 * (sb + tid) + 1, tag, lo32(s));
+                            gput(xg + oS + 3 * (sb + tid) + 2, tag, hi32(s));
+                        }
+                    }
                 }
             }
 
             PSTAMP(l * 32 + 4)
-            if constexpr (!FSPLIT) {
             PSTAMP(l * 32 + 5)
-            // ---- F: exact softmax + P16.V partial per chunk ----------------
-            {
-                PHASE_IDS
-                const uint32_t tag = ptag(pos, L, l, 6);  // (G1 polls the F2 tag)
-                float *cm = (float *)scr;          // [nch]  (nch <= 64)
-                float *Sv = cm + 64;               // [T]    scores, then p
-                const int ntask = B * H * nch;
-                for (int t = wg; t < ntask; t += G) {
-                    const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
-                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
-                    const int doct = tid & 7, jg = tid >> 3;
-                    const f16 *Vb = (const f16 *)a.cv + ((int64_t)l * a.Bt + a.b0 + (a.beam ? 0 : b)) * T * NS + h * 64 + doct * 8;
-                    half8 vf[NKP][4];
-                    const half8 z8 = {};
-#pragma unroll
-                    for (int p = 0; p < NKP; ++p)
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            int key = j0 + 128 * p + jg * 4 + u;
-                            key = key < j1 ? key : j1 - 1;
-                            vf[p][u] = 128 * p < CL ? sld((const half8 *)(Vb + (int64_t)key * NS)) : z8;
-                        }
-                    PREFETCH_ISSUED
-                    __syncthreads();
-                    const uint32_t tg = ptag(pos, L, l, 4);
-                    const bool ok = gpoll<8>(nch + T, tg,  // T <= 2048: one round
-                                          [=](int i) {
-                                              return i < nch ? xg + oM + (int64_t)bh * nch + i
-                                                             : xg + oS + (int64_t)bh * T + (i - nch);
-                                          },
-                                          (uint32_t *)cm, abortw, a.err);
-                    // (cm[0..nch) then the scores: Sv = cm + nch; moved below)
-                    if (check(ok)) return;
-                PSTAMP(l * 32 + 22)
-                    float *Sx = cm + nch;
-                    // (LDS reads are issued unconditionally from clamped
-                    // addresses and selected afterwards: a read under a lane
-                    // guard is waited for on its own, one LDS latency each)
-                    const float m = wave_max(lane < nch ? cm[lane] : -INFINITY);
-                    // exp of every score against the global max; the double
-                    // sum of <= 2048 f16 values in [0, 1] is exact in any order
-                    float sv[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const int j = tid + 256 * u;
-                        sv[u] = Sx[j < T ? j : T - 1];
-                    }
-                    double sum = 0.0;
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        if (256 * u >= T) break;  // workgroup-uniform: no key left (T = 1500: 6 of 8)
-                        const int j = tid + 256 * u;
-                        const float pj = exp_f16_hash(sv[u] - m, sh.expfb, fbk);
-                        if (j < T) sum += (double)pj;
-                        if (j >= j0 && j < j1) Sx[j] = pj;  // (P.V reads only this task's keys)
-                    }
-                    sum = wave_sum(sum);
-                    if (lane == 0) sh.redd[w] = sum;
-                    __syncthreads();
-                PSTAMP(l * 32 + 11)
-                    const float inv = (float)(1.0 / (((sh.redd[0] + sh.redd[1]) + sh.redd[2]) + sh.redd[3]));
-                PSTAMP(l * 32 + 12)
-                    // one partial per 128-key sub-chunk: the grouping of a
-                    // one-row run whatever the task's chunk (CL), so results
-                    // do not depend on how many rows share the launch
-                    float o[NKP][8];
-#pragma unroll
-                    for (int p = 0; p < NKP; ++p)
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) o[p][e] = 0.0f;
-#pragma unroll
-                    for (int p = 0; p < NKP; ++p)
-                        if (j0 + 128 * p < j1) {  // workgroup-uniform
-                            float sp[4];
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                const int key = j0 + 128 * p + jg * 4 + u;
-                                sp[u] = Sx[key < j1 ? key : j1 - 1];
-                            }
-                            // keys past the chunk add pj = 0 (o + 0 == o: o is never -0)
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                const int key = j0 + 128 * p + jg * 4 + u;
-                                const float pj = key < j1 ? h2f_bits(f2h_bits(sp[u] * inv)) : 0.0f;
-#pragma unroll
-                                for (int e = 0; e < 8; ++e) o[p][e] = o[p][e] + pj * (float)vf[p][u][e];
-                            }
-                        }
-#pragma unroll
-                    for (int p = 0; p < NKP; ++p)
-                        if (j0 + 128 * p < j1)
-#pragma unroll
-                            for (int e = 0; e < 8; ++e) o[p][e] = red_8_16_32(o[p][e]);
-                    if (lane < 8)
-#pragma unroll
-                        for (int p = 0; p < NKP; ++p)
-                            if (j0 + 128 * p < j1)
-#pragma unroll
-                                for (int e = 0; e < 8; ++e) sh.ored[w][p * 64 + lane * 8 + e] = o[p][e];
-                PSTAMP(l * 32 + 13)
-                    __syncthreads();
-                    const int nsp = (j1 - j0 + 127) >> 7;  // sub-chunks of this task
-                    if (tid < 64 * nsp)
-                        gput(xg + oP + ((int64_t)bh * nsub + (j0 >> 7)) * 64 + tid, tag,
-                             __float_as_uint(((sh.ored[0][tid] + sh.ored[1][tid]) + sh.ored[2][tid]) + sh.ored[3][tid]));
-                    (void)Sv;
-                }
-            }
-
-            } else {
-            if (xsh) {  // beam rows sharing one clip (see E)
-                PHASE_IDS
-                const uint32_t tag = ptag(pos, L, l, 5);
-                float *cmb = (float *)(scr + XS_OFF + XS_BYTES);  // [B][nch]
-                const int ntask = H * nch;
-                for (int t = wg, k = 0; t < ntask; t += G) {
-                    const int c = t % nch, h = t / nch;
-                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
-                    float *st = (float *)(scr + XS_OFF) + (k++) * (B * CL);
-                    __syncthreads();
-                    const bool ok = gpoll(B * nch, ptag(pos, L, l, 4),
-                                          [=](int i) { return xg + oM + ((int64_t)(i / nch) * H + h) * nch + (i % nch); },
-                                          (uint32_t *)cmb, abortw, a.err);
-                    if (check(ok)) return;
-                PSTAMP(l * 32 + 21)
-                    // wave w takes rows w, w + 4 (each row's keys in one wave:
-                    // no workgroup exchange); the double sum of f16 values in
-                    // [0, 1] is exact in any order, so it equals the per-row task's
-                    for (int b = w; b < B; b += 4) {
-                        const float m = wave_max(cmb[b * nch + (lane < nch ? lane : 0)]);
-                        double sum = 0.0;
-#pragma unroll
-                        for (int u = 0; u < 4 * NKP; ++u) {
-                            const int key = j0 + lane + 64 * u;
-                            if (64 * u < CL) {
-                                const float sv = st[b * CL + (key < j1 ? key : j1 - 1) - j0];
-                                const float pj = exp_f16_hash(sv - m, sh.expfb, fbk);
-                                if (key < j1) {
-                                    sum += (double)pj;
-                                    st[b * CL + key - j0] = pj;
-                                }
-                            }
-                        }
-                        sum = wave_sum(sum);
-                        if (lane == 0) {
-                            const int64_t tb = ((int64_t)b * H + h) * nch + c;
-                            gput(xg + oS + 2 * tb, tag, lo32(sum));
-                            gput(xg + oS + 2 * tb + 1, tag, hi32(sum));
-                        }
-                    }
-                }
-            } else
-            // ---- F1: exp against the global max, chunk sums ----------------
-            // the row max over every chunk of (row, head); p = ggml exp table
-            // value of f16(s - max) replaces the task's scores in LDS; the
-            // chunk's double sum of p (f16 values in [0, 1]: exact in any
-            // order) is published as two granules
-            {
-                PHASE_IDS
-                const uint32_t tag = ptag(pos, L, l, 5);
-                float *cm = (float *)(scr + XS_OFF + XS_BYTES);  // [nch <= 64]
-                const int ntask = B * H * nch;
-                for (int t = wg, k = 0; t < ntask; t += G) {
-                    const int c = t % nch, bh = t / nch;
-                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
-                    float *st = (float *)(scr + XS_OFF) + (k++) * CL;
-                    __syncthreads();
-                    const bool ok = gpoll(nch, ptag(pos, L, l, 4), [=](int i) { return xg + oM + (int64_t)bh * nch + i; },
-                                          (uint32_t *)cm, abortw, a.err);
-                    if (check(ok)) return;
-                PSTAMP(l * 32 + 21)
-                    // (LDS reads issued unconditionally from clamped addresses)
-                    const float m = wave_max(cm[lane < nch ? lane : 0]);
-                    double sum = 0.0;
-#pragma unroll
-                    for (int u = 0; u < NKP; ++u) {
-                        const int key = j0 + tid + 256 * u;
-                        if (256 * u < CL) {
-                            const float sv = st[(key < j1 ? key : j1 - 1) - j0];
-                            const float pj = exp_f16_hash(sv - m, sh.expfb, fbk);
-                            if (key < j1) {
-                                sum += (double)pj;
-                                st[key - j0] = pj;
-                            }
-                        }
-                    }
-                    sum = wave_sum(sum);
-                    if (lane == 0) sh.redd[w] = sum;
-                    __syncthreads();
-                    if (tid == 0) {
-                        const double cs = ((sh.redd[0] + sh.redd[1]) + sh.redd[2]) + sh.redd[3];
-                        gput(xg + oS + 2 * t, tag, lo32(cs));
-                        gput(xg + oS + 2 * t + 1, tag, hi32(cs));
-                    }
-                }
-            }
-
-            PSTAMP(l * 32 + 5)
-            if (xsh) {  // beam rows sharing one clip (see E): V chunk read once, P.V per row
-                // (xshare launches use 128-key chunks: launch_dec_persist checks)
-                PHASE_IDS
-                const uint32_t tag = ptag(pos, L, l, 6);
-                uint32_t *csub = (uint32_t *)(scr + XS_OFF + XS_BYTES + 2048);  // [B][nch][2]
-                float *ob = (float *)(scr + XS_OFF + XS_BYTES + 6144);           // [B][4 waves][64]
-                const int ntask = H * nch;
-                for (int t = wg, k = 0; t < ntask; t += G) {
-                    const int c = t % nch, h = t / nch;
-                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
-                    const float *st = (const float *)(scr + XS_OFF) + (k++) * (B * CL);
-                    const int doct = tid & 7, jg = tid >> 3;
-                    const f16 *Vb = (const f16 *)a.cv + ((int64_t)l * a.Bt + a.b0) * T * NS + h * 64 + doct * 8;
-                    half8 vf[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        int key = j0 + jg * 4 + u;
-                        key = key < j1 ? key : j1 - 1;
-                        vf[u] = sld((const half8 *)(Vb + (int64_t)key * NS));
-                    }
-                    PREFETCH_ISSUED
-                    __syncthreads();
-                    const bool ok = gpoll(B * 2 * nch, ptag(pos, L, l, 5),
-                                          [=](int i) {
-                                              const int b = i / (2 * nch), r = i - b * 2 * nch;
-                                              return xg + oS + 2 * (((int64_t)b * H + h) * nch) + r;
-                                          },
-                                          csub, abortw, a.err);
-                    if (check(ok)) return;
-                PSTAMP(l * 32 + 22)
-                    // lane b < B: row b's exp sum over its chunks (exact in any
-                    // order) -> 1 / sum, read by every lane with readlane
-                    float invl = 0.0f;
-                    if (lane < B) {
-                        double tot = 0.0;
-                        for (int i = 0; i < nch; ++i) tot += mk64(csub[(lane * nch + i) * 2 + 1], csub[(lane * nch + i) * 2]);
-                        invl = (float)(1.0 / tot);
-                    }
-                    // every row's P.V partial at once (each row's keys and
-                    // dims in the per-row task's order), one exchange
-                    float o[PMAXB][8];
-#pragma unroll
-                    for (int b = 0; b < PMAXB; ++b) {
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) o[b][e] = 0.0f;
-                        if (b >= B) continue;
-                        const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(invl), b));
-                        float sp[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int key = j0 + jg * 4 + u;
-                            sp[u] = st[b * CL + (key < j1 ? key : j1 - 1) - j0];
-                        }
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int key = j0 + jg * 4 + u;
-                            const float pj = key < j1 ? h2f_bits(f2h_bits(sp[u] * inv)) : 0.0f;
-#pragma unroll
-                            for (int e = 0; e < 8; ++e) o[b][e] = o[b][e] + pj * (float)vf[u][e];
-                        }
-                    }
-#pragma unroll
-                    for (int b = 0; b < PMAXB; ++b)
-                        if (b < B) {
-#pragma unroll
-                            for (int e = 0; e < 8; ++e) o[b][e] = red_8_16_32(o[b][e]);
-                            if (lane < 8)
-#pragma unroll
-                                for (int e = 0; e < 8; ++e) ob[(b * 4 + w) * 64 + lane * 8 + e] = o[b][e];
-                        }
-                    __syncthreads();
-                    for (int i = tid; i < B * 64; i += PT) {
-                        const int b = i >> 6, d = i & 63;
-                        const float* q4 = ob + b * 256 + d;
-                        gput(xg + oP + (((int64_t)b * H + h) * nsub + (j0 >> 7)) * 64 + d, tag,
-                             __float_as_uint(((q4[0] + q4[64]) + q4[128]) + q4[192]));
-                    }
-                }
-            } else
-            // ---- F2: P16 = f16(p / sum) . V per 128-key sub-chunk -> partials
-            {
-                PHASE_IDS
-                const uint32_t tag = ptag(pos, L, l, 6);
-                uint32_t *csu = (uint32_t *)(scr + XS_OFF + XS_BYTES + 256);  // [nch][2]
-                const int ntask = B * H * nch;
-                for (int t = wg, k = 0; t < ntask; t += G) {
-                    const int c = t % nch, bh = t / nch, h = bh % H, b = bh / H;
-                    const int j0 = c * CL, j1 = j0 + CL < T ? j0 + CL : T;
-                    const float *st = (const float *)(scr + XS_OFF) + (k++) * CL;
-                    const int doct = tid & 7, jg = tid >> 3;
-                    const f16 *Vb = (const f16 *)a.cv + ((int64_t)l * a.Bt + a.b0 + (a.beam ? 0 : b)) * T * NS + h * 64 + doct * 8;
-                    half8 vf[NKP][4];
-                    const half8 z8 = {};
-#pragma unroll
-                    for (int p = 0; p < NKP; ++p)
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            int key = j0 + 128 * p + jg * 4 + u;
-                            key = key < j1 ? key : j1 - 1;
-                            vf[p][u] = 128 * p < CL ? sld((const half8 *)(Vb + (int64_t)key * NS)) : z8;
-                        }
-                    PREFETCH_ISSUED
-                    __syncthreads();
-                    const bool ok = gpoll(2 * nch, ptag(pos, L, l, 5), [=](int i) { return xg + oS + (int64_t)bh * nch * 2 + i; },
-                                          csu, abortw, a.err);
-                    if (check(ok)) return;
-                PSTAMP(l * 32 + 22)
-                    // the row's sum over its chunks (exact: any order)
-                    double tot = 0.0;
-                    for (int i = 0; i < nch; ++i) tot += mk64(csu[2 * i + 1], csu[2 * i]);
-                    const float inv = (float)(1.0 / tot);
-                    // one partial per 128-key sub-chunk: the grouping of a
-                    // one-row run whatever the task's chunk (CL), so results
-                    // do not depend on how many rows share the launch
-                    float o[NKP][8];
-#pragma unroll
-                    for (int p = 0; p < NKP; ++p)
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) o[p][e] = 0.0f;
-#pragma unroll
-                    for (int p = 0; p < NKP; ++p)
-                        if (j0 + 128 * p < j1) {  // workgroup-uniform
-                            float sp[4];
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                const int key = j0 + 128 * p + jg * 4 + u;
-                                sp[u] = st[(key < j1 ? key : j1 - 1) - j0];
-                            }
-                            // keys past the chunk add pj = 0 (o + 0 == o: o is never -0)
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                const int key = j0 + 128 * p + jg * 4 + u;
-                                const float pj = key < j1 ? h2f_bits(f2h_bits(sp[u] * inv)) : 0.0f;
-#pragma unroll
-                                for (int e = 0; e < 8; ++e) o[p][e] = o[p][e] + pj * (float)vf[p][u][e];
-                            }
-                        }
-#pragma unroll
-                    for (int p = 0; p < NKP; ++p)
-                        if (j0 + 128 * p < j1)
-#pragma unroll
-                            for (int e = 0; e < 8; ++e) o[p][e] = red_8_16_32(o[p][e]);
-                    if (lane < 8)
-#pragma unroll
-                        for (int p = 0; p < NKP; ++p)
-                            if (j0 + 128 * p < j1)
-#pragma unroll
-                                for (int e = 0; e < 8; ++e) sh.ored[w][p * 64 + lane * 8 + e] = o[p][e];
-                    __syncthreads();
-                    const int nsp = (j1 - j0 + 127) >> 7;  // sub-chunks of this task
-                    if (tid < 64 * nsp)
-                        gput(xg + oP + ((int64_t)bh * nsub + (j0 >> 7)) * 64 + tid, tag,
-                             __float_as_uint(((sh.ored[0][tid] + sh.ored[1][tid]) + sh.ored[2][tid]) + sh.ored[3][tid]));
-                }
-            }
-
-            }  // FSPLIT
-
             PSTAMP(l * 32 + 6)
-            // ---- G1: chunk partials summed in chunk order -> cross o ---------
+            // ---- G1: the row's sub-chunks combined -> cross o -----------------
+            // M = max m_c, o = (sum_c e^(m_c - M) o_c) / (sum_c e^(m_c - M) S_c),
+            // both sums in one fixed pairwise order (a padded sub-chunk adds 0)
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 7);
-                float *pp = (float *)scr;  // [nsub][64]
+                float *pp = (float *)scr;                        // [nsub][64] partial o
+                const uint32_t *ps = (const uint32_t *)(pp + nsub * 64);  // [nsub][3] m, S lo, S hi
+                const int no = nsub * 64;
                 for (int t = wg; t < B * H; t += G) {
                     const int b = t / H, h = t - b * H;
                     __syncthreads();
-                    const bool ok = gpoll(nsub * 64, ptag(pos, L, l, 6), ptr_u64(xg + oP + (int64_t)t * nsub * 64),
+                    const bool ok = gpoll(no + 3 * nsub, ptag(pos, L, l, 6),
+                                          [=](int i) {
+                                              return i < no ? xg + oP + (int64_t)t * no + i
+                                                            : xg + oS + (int64_t)t * nsub * 3 + (i - no);
+                                          },
                                           (uint32_t *)pp, abortw, a.err);
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 23)
-                    if (tid < 64) {  // in chunk order, 8 LDS reads in flight
-                        float s = 0.0f;
-                        for (int c0 = 0; c0 < nsub; c0 += 8) {
-                            float v[8];
+                    if (tid < 64) {  // (all reads issued from clamped addresses, then selected)
+                        float mc[NSUBM], v[NSUBM];
+                        double sc[NSUBM];
 #pragma unroll
-                            for (int u = 0; u < 8; ++u) v[u] = pp[(c0 + u < nsub ? c0 + u : nsub - 1) * 64 + tid];
-#pragma unroll
-                            for (int u = 0; u < 8; ++u)
-                                if (c0 + u < nsub) s = c0 + u == 0 ? v[u] : s + v[u];
+                        for (int c = 0; c < NSUBM; ++c) {
+                            const int cc = c < nsub ? c : nsub - 1;
+                            mc[c] = __uint_as_float(ps[3 * cc]);
+                            sc[c] = mk64(ps[3 * cc + 2], ps[3 * cc + 1]);
+                            v[c] = pp[cc * 64 + tid];
                         }
-                        sh.ored[0][tid] = s;
+                        float M = mc[0];
+#pragma unroll
+                        for (int c = 1; c < NSUBM; ++c) M = fmaxf(M, mc[c]);  // (padding repeats the last: no effect)
+                        float ov[NSUBM];
+                        double sv[NSUBM];
+#pragma unroll
+                        for (int c = 0; c < NSUBM; ++c) {
+                            const float wc = c < nsub ? expf(mc[c] - M) : 0.0f;
+                            ov[c] = v[c] * wc;
+                            sv[c] = (double)wc * sc[c];
+                        }
+#pragma unroll
+                        for (int st2 = 1; st2 < NSUBM; st2 *= 2)
+#pragma unroll
+                            for (int c = 0; c < NSUBM; c += 2 * st2) {
+                                ov[c] = ov[c] + ov[c + st2];
+                                sv[c] = sv[c] + sv[c + st2];
+                            }
+                        sh.ored[0][tid] = (float)((double)ov[0] / sv[0]);
                     }
                     __syncthreads();
                     if (tid < 32)
@@ -1950,6 +1735,9 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
         // ---- logits: LN_final + vocabulary rows + per-WG argmax -------------
         // rows [rv0, rs0) are resident in LDS (loaded once per launch), the
         // rest [rs0, rv1) stream through two register sets issued before the poll
+        // (logits_out: this step's [B][V] slab; lg_stride > 0 keeps every
+        // position's, for the all-step parity tests)
+        float *const lgo = a.logits_out ? a.logits_out + (int64_t)pos * a.lg_stride : nullptr;
         if constexpr (LMF) {
             // MFMA logits: wave w takes the 16-row tiles w, w + 4, ... of the
             // resident rows (B fragments from the swizzled LDS copy), then of
@@ -2007,7 +1795,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 for (int r = 0; r < 4; ++r) {
                     const int m = 4 * lh + r;
                     const bool valid = m < B && n < nend;
-                    if (a.logits_out && valid) a.logits_out[(int64_t)m * a.V + n] = d[r];
+                    if (lgo && valid) lgo[(int64_t)m * a.V + n] = d[r];
                     const unsigned long long k =
                         ((unsigned long long)ord_f32(d[r]) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)n);
                     if (valid && n != a.suppress_id) best[r] = k > best[r] ? k : best[r];
@@ -2134,7 +1922,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     const float v = ((kp[((tg * 4 + 0) * 16 + rr) * 8 + m] + kp[((tg * 4 + 1) * 16 + rr) * 8 + m]) +
                                      kp[((tg * 4 + 2) * 16 + rr) * 8 + m]) +
                                     kp[((tg * 4 + 3) * 16 + rr) * 8 + m];
-                    if (a.logits_out) a.logits_out[(int64_t)m * a.V + n] = v;
+                    if (lgo) lgo[(int64_t)m * a.V + n] = v;
                     if (n == a.suppress_id) continue;
                     const unsigned long long k =
                         ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)n);
@@ -2186,7 +1974,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             PSTAMP(L * 32 + 1)
             unsigned long long best = 0ull;
             auto epi = [&](int row, int b, float v, float eb, bool valid) {
-                if (a.logits_out && valid) a.logits_out[(int64_t)b * a.V + row] = v;
+                if (lgo && valid) lgo[(int64_t)b * a.V + row] = v;
                 if (!valid || row == a.suppress_id) return;
                 const unsigned long long k =
                     ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)row);
@@ -2311,11 +2099,6 @@ hipError_t launch_nsb(hipStream_t s, const PersistArgs &a, int G) {
     hipError_t e = hipFuncSetAttribute((const void *)k_dec_persist<NS, BT, BEAM, Q5>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    if (b.coop) {
-        void *args[] = {&b};
-        return hipLaunchCooperativeKernel((const void *)k_dec_persist<NS, BT, BEAM, Q5>, dim3(G), dim3(PT), args,
-                                          (unsigned)lds, s);
-    }
     hipLaunchKernelGGL((k_dec_persist<NS, BT, BEAM, Q5>), dim3(G), dim3(PT), lds, s, b);
     return hipGetLastError();
 }
@@ -2450,9 +2233,8 @@ hipError_t launch_dec_persist(hipStream_t s, const PersistArgs &a, int G) {
     if (G < 1 || G > PX_GMAX || a.B < 1 || a.B > PMAXB || a.T > 2048 || a.nch < 1 || a.nch > 64 ||
         a.cl > 128 * NKP || (int64_t)a.nch * a.cl < a.T || (int64_t)a.B * (a.n / 64) * a.nch > PX_TASKS ||
         a.tctx > 512 || a.cl % 128 || (a.beam && a.n_steps != 1) || (a.kv_src && a.kv_src_stride < a.tctx) ||
-        ((int64_t)a.B * (a.n / 64) * a.nch + G - 1) / G * a.cl * 4 > XS_BYTES ||  // task scores in LDS
-        (a.xshare && (!a.beam || a.n <= 768 || a.cl != 128 || ((int64_t)(a.n / 64) * a.nch + G - 1) / G * a.B * a.cl * 4 > XS_BYTES ||
-                      a.B * a.nch * 4 > 2048 || a.B * a.nch * 8 > 4096)))
+        (!a.beam && a.B == 1 && a.cl > 256) ||  // (the one-row instance: two sub-chunks per task)
+        (a.xshare && (!a.beam || a.n <= 768 || a.cl != 128)))
         return hipErrorInvalidValue;
     switch (a.n) {
         case 128: return launch_ns<128>(s, a, G);
