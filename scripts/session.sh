@@ -10,10 +10,11 @@
 #   smoke              __graft_entry__.smoke(): TAG_smoke.log
 #   bench[=ARGS]       bench.py ARGS (default: the driver's line, all configs + CPU baseline): TAG_bench.json
 #   trace=MODEL:ROWS   decoder phase trace (WMI_PTRACE) of a greedy run: TAG_trace_MODEL_ROWS.log
+#   beamtrace=MODEL:K  the same for a K-beam search (16 steps): TAG_beamtrace_MODEL_K.log
 #   prof               rocprofv3 kernel-trace summary of the base bench: TAG_prof/
 #   pmc=MODEL:CLIPS    FETCH_SIZE / WRITE_SIZE passes of the persistent decoder (kernel 14): TAG_pmc_MODEL_CLIPS*
 #   probe=MODEL:CLIPS:NTOK[:beam]  step-logit parity probe (scripts/parity_probe.py): TAG_probe_MODEL_CLIPS.log
-#   ab=ENV1,ENV2,...   bench (base, 1 clip, 10 steps) alternating environments, e.g. ab=WMI_COOP=1,WMI_COOP=0
+#   ab=ENV1,ENV2,...   bench (base, 1 clip, 10 steps) alternating environments, e.g. ab=WMI_LIB=whisper.rs_amd/ab/X/libwhisper_mi355x.so,WMI_LIB=
 #                      (MODEL, CPG, BEAM in the environment select another config): TAG_ab.txt
 # Replaces the one-off drivers of rounds 1-3 (their evidence is under profiles/).
 set -o pipefail
@@ -40,6 +41,10 @@ for step in "$@"; do
       python3 -c "
 import json; d=json.load(open('${O}_bench.json')); print('bench', d['value'], d['stage_ms'], (d.get('roofline') or {}).get('frac'))
 [print(' ', k, v.get('audio_s_per_s'), v.get('decode_ms'), v.get('encoder_ms'), (v.get('roofline') or {}).get('frac')) for k, v in d.get('configs', {}).items()]" ;;
+    beamtrace)
+      m=${arg%%:*}; k=${arg#*:}
+      timeout -k 10 400 python3 -u scripts/diag_persist.py beamtrace $m $k 16 > ${O}_beamtrace_${m}_${k}.log 2>&1 || exit 1
+      grep "wg 0: step" ${O}_beamtrace_${m}_${k}.log ;;
     trace)
       m=${arg%%:*}; rows=${arg#*:}
       timeout -k 10 400 python3 -u scripts/diag_persist.py trace $m $rows > ${O}_trace_${m}_${rows}.log 2>&1 || exit 1

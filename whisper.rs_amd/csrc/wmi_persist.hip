@@ -1593,7 +1593,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             PSTAMP(l * 32 + 6)
             // ---- G1: the row's sub-chunks combined -> cross o -----------------
             // M = max m_c, o = (sum_c e^(m_c - M) o_c) / (sum_c e^(m_c - M) S_c),
-            // both sums in one fixed pairwise order (a padded sub-chunk adds 0)
+            // both sums in one fixed order
             {
                 PHASE_IDS
                 const uint32_t tag = ptag(pos, L, l, 7);
@@ -1611,35 +1611,27 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                                           (uint32_t *)pp, abortw, a.err);
                     if (check(ok)) return;
                 PSTAMP(l * 32 + 23)
-                    if (tid < 64) {  // (all reads issued from clamped addresses, then selected)
-                        float mc[NSUBM], v[NSUBM];
-                        double sc[NSUBM];
+                    if (tid < 64) {
+                        // lane c < nsub: sub-chunk c's max, weight e^(m_c - M)
+                        // and weighted sum (one expf a lane, wave reductions in
+                        // a fixed order); the weights reach every lane through
+                        // readlane; lane d then sums its dimension in chunk order
+                        const int cc = lane < nsub ? lane : nsub - 1;
+                        const float mcl = __uint_as_float(ps[3 * cc]);
+                        const double scl = mk64(ps[3 * cc + 2], ps[3 * cc + 1]);
+                        float v[NSUBM];
+#pragma unroll
+                        for (int c = 0; c < NSUBM; ++c) v[c] = pp[(c < nsub ? c : nsub - 1) * 64 + lane];
+                        const float M = wave_max(lane < nsub ? mcl : -INFINITY);
+                        const float wcl = lane < nsub ? expf(mcl - M) : 0.0f;
+                        const double S = wave_sum(lane < nsub ? (double)wcl * scl : 0.0);
+                        float ov = 0.0f;
 #pragma unroll
                         for (int c = 0; c < NSUBM; ++c) {
-                            const int cc = c < nsub ? c : nsub - 1;
-                            mc[c] = __uint_as_float(ps[3 * cc]);
-                            sc[c] = mk64(ps[3 * cc + 2], ps[3 * cc + 1]);
-                            v[c] = pp[cc * 64 + tid];
+                            const float wc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wcl), c));
+                            ov = ov + v[c] * wc;  // (a padded sub-chunk: weight 0)
                         }
-                        float M = mc[0];
-#pragma unroll
-                        for (int c = 1; c < NSUBM; ++c) M = fmaxf(M, mc[c]);  // (padding repeats the last: no effect)
-                        float ov[NSUBM];
-                        double sv[NSUBM];
-#pragma unroll
-                        for (int c = 0; c < NSUBM; ++c) {
-                            const float wc = c < nsub ? expf(mc[c] - M) : 0.0f;
-                            ov[c] = v[c] * wc;
-                            sv[c] = (double)wc * sc[c];
-                        }
-#pragma unroll
-                        for (int st2 = 1; st2 < NSUBM; st2 *= 2)
-#pragma unroll
-                            for (int c = 0; c < NSUBM; c += 2 * st2) {
-                                ov[c] = ov[c] + ov[c + st2];
-                                sv[c] = sv[c] + sv[c + st2];
-                            }
-                        sh.ored[0][tid] = (float)((double)ov[0] / sv[0]);
+                        sh.ored[0][tid] = (float)((double)ov / S);
                     }
                     __syncthreads();
                     if (tid < 32)
