@@ -190,3 +190,40 @@ def test_rendezvous_rejects_bad_ranks():
     peer.close()
     t.join(30)
     assert res["gather"] == ["hub", "peer"]
+
+
+def test_rendezvous_survives_a_silent_connection():
+    """A connection that sends nothing holds rank 0 for its per-connection
+    handshake timeout; the real peer connecting meanwhile waits longer than
+    that for its ack (dist._HS_PEER > dist._HS_HUB), so it is acked and
+    confirmed once rank 0 gives up on the silent one."""
+    import threading
+    import time
+
+    import dist
+    port = _free_port()
+    res = {}
+    old = dist._HS_HUB
+    dist._HS_HUB = 2.0  # (keeps the test short; the ordering is what matters)
+    try:
+        def hub():
+            g = dist.Group(0, 2, "127.0.0.1", port, timeout=30)
+            res["gather"] = g.all_gather("hub")
+            g.close()
+
+        t = threading.Thread(target=hub)
+        t.start()
+        for _ in range(100):
+            try:
+                silent = socket.create_connection(("127.0.0.1", port), timeout=5)
+                break
+            except OSError:
+                time.sleep(0.05)
+        peer = dist.Group(1, 2, "127.0.0.1", port, timeout=30)
+        assert peer.all_gather("peer") == ["hub", "peer"]
+        peer.close()
+        silent.close()
+        t.join(30)
+        assert res["gather"] == ["hub", "peer"]
+    finally:
+        dist._HS_HUB = old

@@ -20,6 +20,9 @@ _PORT_TRIES = 8     # hub ports MASTER_PORT + 23 + 97 k, k < 8: the first one ra
 _PORT_STRIDE = 97
 _MAX_MSG = 1 << 24  # messages are ids, timings and small token lists
 _MAGIC = b"wmi-rdv1"
+_CONFIRM = b"wmi-rdv1-ok"
+_HS_HUB = 10.0   # rank 0's per-connection handshake reads
+_HS_PEER = 15.0  # a peer's wait for rank 0's ack: longer than _HS_HUB
 
 
 def hub_ports(master_port: int):
@@ -125,17 +128,25 @@ class Group:
                     srv.settimeout(left)
                     c, _ = srv.accept()
                     c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                    c.settimeout(min(timeout, 10.0))
+                    c.settimeout(min(timeout, _HS_HUB))
                     try:
                         msg = _recv(c)
                         r = struct.unpack("<i", msg[-4:])[0] if len(msg) == len(hello) + 4 and msg[:-4] == hello \
                             else -1
+                        if 1 <= r < world:
+                            # ack, then the peer's confirmation: a connection
+                            # its peer abandoned (it gave up waiting and
+                            # reconnected) fails here instead of being kept
+                            _send(c, hello)
+                            if _recv(c) != _CONFIRM:
+                                r = -1
                     except (ConnectionError, OSError):
                         r = -1
-                    if not 1 <= r < world or r in peers:  # foreign, out of range or duplicate: not a peer
+                    if not 1 <= r < world:  # foreign, out of range or abandoned: not a peer
                         c.close()
                         continue
-                    _send(c, hello)  # ack: the peer knows it reached this rendezvous
+                    if r in peers:  # the same rank again: its newer connection wins
+                        peers[r].close()
                     c.settimeout(timeout)
                     peers[r] = c
             except BaseException:
@@ -155,9 +166,10 @@ class Group:
                 try:
                     s = socket.create_connection((addr, p), timeout=5)
                     s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                    s.settimeout(5)
+                    s.settimeout(_HS_PEER)  # (rank 0 may be busy with another connection for up to _HS_HUB)
                     _send(s, hello + struct.pack("<i", rank))
                     if _recv(s) == hello:
+                        _send(s, _CONFIRM)
                         break
                     s.close()
                 except OSError:  # (ConnectionError, socket.timeout are OSErrors)
