@@ -948,11 +948,12 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
                     i = i < n_exp ? i : n_exp;  // v_min: index n_exp holds 0
                     if (TAIL) i = key < T ? i : n_exp;
                     const float e = h2f_bits(tab[i]);  // unguarded read (a guarded one branches per element)
-                    if constexpr (PASS == 1) sum += (double)e;
-                    else pa[(r + u) >> 3][(r + u) & 7] = f16_rt(e * inv);
+                    if constexpr (PASS == 1 || PASS == 3) sum += (double)e;
+                    if constexpr (PASS == 2) pa[(r + u) >> 3][(r + u) & 7] = f16_rt(e * inv);
+                    if constexpr (PASS == 3) pa[(r + u) >> 3][(r + u) & 7] = (f16)e;  // (an f16 value: exact)
                 }
             }
-            if constexpr (PASS == 2) {
+            if constexpr (PASS >= 2) {
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
                     half8 vb[2];
@@ -989,7 +990,7 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
     const int ntiles = (a.T + AT4_KT - 1) / AT4_KT;
     constexpr int NT = 128 * NW;          // threads: NW query blocks x 2 key halves
     constexpr int SCH = 512 / NT;         // 16-byte chunks per thread of an 8 KB tile
-    constexpr int VCH = PASS == 2 ? SCH : 1;
+    constexpr int VCH = PASS >= 2 ? SCH : 1;
     const int kb = (threadIdx.x >> 6) / NW;  // this wave's 32-key half of every tile
     a4vec kA[SCH], vA[VCH], kB[SCH], vB[VCH];
     // this thread's 16-byte chunks of a tile: rows (tid >> 3) + 8 NW i, column (tid & 7) * 8
@@ -1001,7 +1002,7 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
         _Pragma("unroll") for (int i = 0; i < SCH; ++i) {                                       \
             const int row = crow + i * (NT / 8);                                                \
             KR[i] = *(const a4vec *)(K + (int64_t)(key0_ + row) * 64 + ccol);                   \
-            if constexpr (PASS == 2) VR[i] = *(const a4vec *)(Vt + (int64_t)row * Tp + key0_ + ccol); \
+            if constexpr (PASS >= 2) VR[i] = *(const a4vec *)(Vt + (int64_t)row * Tp + key0_ + ccol); \
         }                                                                                       \
     }
 #define ATT4_SSTORE(BUF, KR, VR)                                                                \
@@ -1009,7 +1010,7 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
         _Pragma("unroll") for (int i = 0; i < SCH; ++i) {                                       \
             const int row = crow + i * (NT / 8);                                                \
             *(a4vec *)(Ks + ((BUF) * AT4_KT + row) * AT4_LD + ccol) = KR[i];                    \
-            if constexpr (PASS == 2) *(a4vec *)(Vs + ((BUF) * AT4_KT + row) * AT4_LD + ccol) = VR[i]; \
+            if constexpr (PASS >= 2) *(a4vec *)(Vs + ((BUF) * AT4_KT + row) * AT4_LD + ccol) = VR[i]; \
         }                                                                                       \
     }
     ATT4_GLOAD(0, kA, vA)
@@ -1084,6 +1085,20 @@ __global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
     xm[w * 64 + lane] = mx;
     __syncthreads();
     const float m = fmaxf(mx, xm[partner * 64 + lane]) * a.scale + 0.0f;  // max of the raw scores, scaled once (never -0)
+#ifndef WMI_ATTN3
+    // two sweeps: the second takes p = table exp of f16(S - m) as the P.V
+    // operand (an f16 value, exact) while summing it, and O is divided by the
+    // sum at the end; ggml rounds f16(p / sum) first (the weights differ by
+    // that rounding: one sweep of Q K^T and table reads fewer)
+    __syncthreads();  // (the exchange slots above are V buffers in the sweep)
+    attn4_sweep<NW, 3>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
+    sum = sum + __shfl_xor(sum, 32);
+    xd[w * 64 + lane] = sum;  // (the sweep's last barrier freed the V buffers)
+    __syncthreads();
+    const double dsum = kb ? xd[partner * 64 + lane] + sum : sum + xd[partner * 64 + lane];
+    const float inv = (float)(1.0 / dsum);
+    __syncthreads();  // (the exchange slots are read before the O exchange reuses Ks)
+#else
     attn4_sweep<NW, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
     sum = sum + __shfl_xor(sum, 32);
     xd[w * 64 + lane] = sum;
@@ -1093,6 +1108,7 @@ __global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
     const float inv = (float)(1.0 / (double)(float)d);
     __syncthreads();  // the exchange slots are V buffers again in sweep 2
     attn4_sweep<NW, 2>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, inv, o0, o1);
+#endif
     // second key half's partial O -> LDS (the K / V buffers are free now),
     // added to the first half's in that order
     float *xo = (float *)Ks;  // [NW][32][64]
@@ -1112,6 +1128,17 @@ __global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
         o0[r] = o0[r] + xo[(qw * 32 + qq) * 64 + lr];
         o1[r] = o1[r] + xo[(qw * 32 + qq) * 64 + 32 + lr];
     }
+#ifndef WMI_ATTN3
+    // (inv is per query: lane lr's inv belongs to query lr; row r of the
+    // accumulators holds query (r & 3) + 8 (r >> 2) + 4 lh)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int qq = (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float iq = __shfl(inv, qq);
+        o0[r] = o0[r] * iq;
+        o1[r] = o1[r] * iq;
+    }
+#endif
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int t = q0 + (r & 3) + 8 * (r >> 2) + 4 * lh;

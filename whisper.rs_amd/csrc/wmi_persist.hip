@@ -294,6 +294,22 @@ __device__ __forceinline__ void wset_load(WSet<KCH, NP, Q5> &S, const WMat &m, c
     }
 }
 
+// One row's K chunks c0 .. c0 + N - 1 of xs (lane l16's 8 elements each) in
+// registers, every LDS read issued before the first is waited for: one LDS
+// latency for the N reads instead of one per dot step (the scheduler
+// otherwise interleaves one or two reads with the dots; the values and the
+// dot order are unchanged)
+// (from 6 K chunks, n >= 768: small 37.3 -> 36.0 ms decode; at n = 512 the
+// E tasks' cross-q GEMV measured 0.1 ms slower with it, profiles/r05/preload_*)
+constexpr int PRE_GEMV_MIN = 6;  // K chunks from which a one-row GEMV preloads them
+template <int N>
+__device__ __forceinline__ void xs_chunks(half8 (&xa)[N], const f16 *xs, int c0, int l16) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) xa[c] = *(const half8 *)(xs + (c0 + c) * 128 + l16 * 8);
+#pragma unroll
+    for (int c = 0; c < N; ++c) asm volatile("" : "+v"(xa[c]));
+}
+
 // epi(row, b, v, bias, valid) is called by EVERY lane (pairing shuffles);
 // lane l16 carries the reduced value of row `row` for decoder row b = l16
 template <int BT, int KCH, int NP, bool Q5, typename Epi>
@@ -311,6 +327,14 @@ __device__ __forceinline__ void wset_dot(const WSet<KCH, NP, Q5> &S, const f16 *
         for (int p = 0; p < NP; ++p)
 #pragma unroll
             for (int b = 0; b < BT; ++b) acc[p][b] = 0.0f;
+        if constexpr (BT == 1 && KCH <= 8 && KCH >= PRE_GEMV_MIN) {
+            half8 xa[KCH];
+            xs_chunks(xa, xs, 0, l16);
+#pragma unroll
+            for (int c = 0; c < KCH; ++c)
+#pragma unroll
+                for (int p = 0; p < NP; ++p) acc[p][0] = dot8(wc_h8(S.w[p][c], sh), xa[c], acc[p][0]);
+        } else
 #pragma unroll
         for (int c = 0; c < KCH; ++c) {
             half8 xv[BT];
@@ -446,6 +470,12 @@ __device__ __forceinline__ void wsplit_dot(const WSplit<KCH, KS, Q5> &S, const f
     float acc[BT];
 #pragma unroll
     for (int b = 0; b < BT; ++b) acc[b] = 0.0f;
+    if constexpr (BT == 1 && CQ <= 8 && CQ >= PRE_GEMV_MIN) {
+        half8 xa[CQ];
+        xs_chunks(xa, xs, ks * CQ, l16);
+#pragma unroll
+        for (int c = 0; c < CQ; ++c) acc[0] = dot8(wc_h8(S.w[c], sh), xa[c], acc[0]);
+    } else
 #pragma unroll
     for (int c = 0; c < CQ; ++c) {
         const half8 wv = wc_h8(S.w[c], sh);
@@ -1796,12 +1826,17 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             for (int t = w; 16 * t < rres - rv0; t += 4) {  // resident tiles
                 const int j = 16 * t + lr;                   // row within the resident copy
                 const f16 *wr = vres + j * NS;
+                // every B fragment of the tile requested before the first
+                // MFMA (one LDS latency a tile, not one per MFMA step: the
+                // scheduler otherwise keeps two reads in flight)
+                half8 bv[NK];
+#pragma unroll
+                for (int kk = 0; kk < NK; ++kk) bv[kk] = *(const half8 *)(wr + (((4 * kk + lh) ^ (j & 15)) * 8));
+#pragma unroll
+                for (int kk = 0; kk < NK; ++kk) asm volatile("" : "+v"(bv[kk]));  // (one wait for all of them)
                 floatx4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int kk = 0; kk < NK; ++kk) {
-                    const half8 bv = *(const half8 *)(wr + (((4 * kk + lh) ^ (j & 15)) * 8));
-                    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[kk], bv, d, 0, 0, 0);
-                }
+                for (int kk = 0; kk < NK; ++kk) d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[kk], bv[kk], d, 0, 0, 0);
                 epi(d, rv0 + 16 * t, rres);
             }
             PSTAMP(L * 32 + 2)
@@ -1886,11 +1921,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     if (t < nres_t) {
                         const int j = 16 * t + lr;
                         const f16 *wr = vres + j * NS;
+                        half8 bv[NKW];  // (all requested before the first MFMA, as in the LMF tiles)
 #pragma unroll
-                        for (int i = 0; i < NKW; ++i) {
-                            const half8 bv = *(const half8 *)(wr + ((((k0 >> 3) + 4 * i + lh) ^ (j & 15)) * 8));
-                            d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bv, d, 0, 0, 0);
-                        }
+                        for (int i = 0; i < NKW; ++i) bv[i] = *(const half8 *)(wr + ((((k0 >> 3) + 4 * i + lh) ^ (j & 15)) * 8));
+#pragma unroll
+                        for (int i = 0; i < NKW; ++i) asm volatile("" : "+v"(bv[i]));
+#pragma unroll
+                        for (int i = 0; i < NKW; ++i) d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bv[i], d, 0, 0, 0);
                     } else if (((t - nres_t) & 1) == 0) {
 #pragma unroll
                         for (int i = 0; i < NKW; ++i) d = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bA[i], d, 0, 0, 0);
