@@ -949,12 +949,12 @@ def test_f32_model(wmi, model_cache, model, n_ctx, secs):
         om.close()
 
 
-@pytest.mark.parametrize("nw", ["1", "2", "4"])
+@pytest.mark.parametrize("nw", ["0", "1", "2", "4"])
 def test_enc_attn_nw_parity_and_batch_invariance(wmi, model_cache, nw):
     """k_attn_enc4 with 1, 2 and 4 query blocks per workgroup (WMI_ENC_ATTN_NW;
-    the default picks 2 or 4 by grid size): the encoder bar against the
-    oracle at base's full 1500 frames, and a clip's result bitwise independent
-    of the batch (8 clips vs 1)."""
+    0: the default, 2 at one clip of base and 4 at eight): the encoder bar
+    against the oracle at base's full 1500 frames, and a clip's result bitwise
+    independent of the batch (8 clips vs 1) — across the default's switch too."""
     path = synth.model_path("base", model_cache)
     om = pyoracle.OracleModel(path)
     ctx = _ctx_with_env(wmi, path, {"WMI_ENC_ATTN_NW": nw}, max_clips=8)

@@ -2816,8 +2816,7 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
     } else if (which == 2) {
         out->alg_flops = 4.0 * T * (double)T * n * B;
         out->alg_bytes = 4.0 * (double)M * n * 2;
-        int nw = ctx->tune.enc_attn_nw;  // as launch_attn_enc picks it
-        if (nw != 1 && nw != 2 && nw != 4) nw = (int64_t)((T + 127) / 128) * hp.n_audio_head * B >= 512 ? 4 : 2;
+        const int nw = attn_enc_nw(T, hp.n_audio_head, B, ctx->tune.enc_attn_nw);  // as launch_attn_enc picks it
         snprintf(out->name, sizeof out->name, "k_attn_enc4<%d>", nw);
     } else if (which == 14) {
         int32_t prompt[8];

@@ -76,7 +76,7 @@ struct Tune {
     int gemv_nw = 4;        // WMI_GEMV_NW: waves per decoder GEMV workgroup (1, 4; 0 auto)
     int xattn_rows = 1;     // WMI_XATTN_ROWS: beam rows share cross-attention phase A (1 auto, 2 always, 0 never)
     int graph_steps = 8;    // WMI_GRAPH_STEPS: chain decoder steps per captured graph
-    int enc_attn_nw = 0;    // WMI_ENC_ATTN_NW: 32-query blocks (two waves each) per k_attn_enc4 workgroup (0 auto, 1, 2, 4)
+    int enc_attn_nw = 0;    // WMI_ENC_ATTN_NW: 32-query blocks (four key-part waves each) per k_attn_enc4 workgroup (0 auto, 1, 2, 4)
     int gemm_g = 1;         // WMI_GEMM_G: large-M encoder GEMMs on k_gemm_g (LDS-DMA staging); 0: k_gemm
     // WMI_MEL_G=0: the dense-filterbank mel layout (4 two-frame waves, LDS
     // copy of the whole [201][n_mel] bank) that a file whose bank has more
@@ -133,6 +133,8 @@ struct AttnArgs {
     float scale;
 };
 hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a);
+// k_attn_enc4 query blocks per workgroup, as launch_attn_enc picks them
+int attn_enc_nw(int T, int H, int n_clips, int nw_knob);
 
 // ---- decoder step -----------------------------------------
 struct DecState {          // device-resident, advanced by the kernels

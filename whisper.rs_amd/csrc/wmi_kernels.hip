@@ -884,30 +884,37 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a0) {
 // 8 waves splitting the keys of one 32-query block, scores in registers — is
 // in the git history; k_attn_enc4 replaced it at every batch size.)
 // ============================================================================
-// NW waves x 32 queries per workgroup share every K / V tile
-// through LDS (64-key tiles, double-buffered, one global->LDS copy per tile
-// for the whole workgroup instead of one per 32 queries), and the exact
-// ggml softmax is kept with three sweeps over the keys instead of holding
-// the scores in registers:
-//   sweep 0: S = scale * K Q^T (MFMA) -> row max
-//   sweep 1: S again -> sum of exp_tab[f16(S - max)]  (double)
-//   sweep 2: S again -> P16 = f16(e * (1/sum)); O += P16 V (MFMA)
-// A wave owns its 32 queries over every key, so no cross-wave reduction or
-// partial-O combine exists; recomputing Q K^T twice costs MFMA time the
-// kernel has to spare (enc3 ran at 3 % MFMA busy, bound by its per-32-query
-// K / V streams).
-constexpr int AT4_KT = 64;  // keys per tile
-constexpr int AT4_LD = 72;  // halfs per LDS row (64 + 8 pad: 144-byte rows)
+// NW x 32 queries per workgroup share every K / V tile through LDS
+// (128-key tiles, double-buffered, one global->LDS copy per tile for the
+// whole workgroup instead of one per 32 queries); KQ = 4 waves share a query
+// block, wave kb taking keys kb * 32 .. kb * 32 + 31 of every tile, and the
+// softmax runs in two sweeps over the keys instead of holding the scores in
+// registers:
+//   sweep 0: S = scale * K Q^T (MFMA) -> row max (exact: the parts' maxima
+//            meet in LDS)
+//   sweep 1: S again -> p = exp_tab[f16(S - max)] (an f16 value): double sum
+//            of p, O += p V (MFMA); O / sum at the end (ggml rounds
+//            P16 = f16(p / sum) first: the weights differ by that rounding)
+// The parts' exact double sums and partial O meet in LDS, O added in part
+// order.  Recomputing Q K^T costs MFMA time the kernel has to spare.  (KQ = 2
+// — half the waves, 64-key tiles — was the round-4 kernel: one clip 0.69 vs
+// 0.64 ms; the three-sweep exact-ggml form, f16(p / sum) before P V, is in
+// the git history: 0.78 ms.)
+constexpr int AT4_KQ = 4;
+static_assert(AT4_KQ == 2 || AT4_KQ == 4, "key parts");
+constexpr int AT4_KT = 32 * AT4_KQ;  // keys per tile
+constexpr int AT4_LD = 72;           // halfs per K row in LDS (64 + 8 pad: 144-byte rows)
+constexpr int AT4_VLD = AT4_KT + 8;  // halfs per V^T row in LDS
 
 // 16-byte staging chunks as a native vector (SROA keeps arrays of these in
 // registers; the struct uint4 arrays of the staging loop went to scratch)
 typedef uint32_t a4vec __attribute__((ext_vector_type(4)));
 
-// one 64-key tile from LDS (buffer Kb / Vb) for this wave's 32 queries.
-// TAIL: the tile holds keys >= T (masked); full tiles skip every key test.
+// this wave's 32-key part kb of a tile in LDS (buffer Kb / Vb) for its 32
+// queries.  TAIL: the tile holds keys >= T (masked); full tiles skip every key test.
 // Sweep 0 keeps the max of the raw scores (scale > 0 and rounding are
-// monotone, so fl(max_raw * scale) is the max of the scaled scores); sweeps
-// 1 and 2 clamp the table index to n_exp, where the table holds a 0 (no
+// monotone, so fl(max_raw * scale) is the max of the scaled scores); sweep
+// 1 clamps the table index to n_exp, where the table holds a 0 (no
 // compare / select per element); scale and subtract run as packed f32 pairs,
 // as m - S: fl(m - S) = -fl(S - m), so its f16 bits are the table index
 // f16(|S - m|) with no mask (m is never -0: the caller adds +0).
@@ -920,7 +927,7 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
     const int T = a.T;
     const uint32_t n_exp = (uint32_t)a.n_exp;
     const f2v scale2 = {a.scale, a.scale}, m2 = {m, m};
-    {  // this wave's 32-key half kb of the tile
+    {  // this wave's 32-key part kb of the tile
         floatx16 sc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) sc[r] = 0.0f;
@@ -948,18 +955,17 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
                     i = i < n_exp ? i : n_exp;  // v_min: index n_exp holds 0
                     if (TAIL) i = key < T ? i : n_exp;
                     const float e = h2f_bits(tab[i]);  // unguarded read (a guarded one branches per element)
-                    if constexpr (PASS == 1 || PASS == 3) sum += (double)e;
-                    if constexpr (PASS == 2) pa[(r + u) >> 3][(r + u) & 7] = f16_rt(e * inv);
-                    if constexpr (PASS == 3) pa[(r + u) >> 3][(r + u) & 7] = (f16)e;  // (an f16 value: exact)
+                    sum += (double)e;
+                    pa[(r + u) >> 3][(r + u) & 7] = (f16)e;  // (an f16 value: exact)
                 }
             }
-            if constexpr (PASS >= 2) {
+            {
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
                     half8 vb[2];
 #pragma unroll
                     for (int dt = 0; dt < 2; ++dt) {
-                        const f16 *vp = Vb + (dt * 32 + lr) * AT4_LD + kb * 32 + 16 * s + 4 * lh;
+                        const f16 *vp = Vb + (dt * 32 + lr) * AT4_VLD + kb * 32 + 16 * s + 4 * lh;
                         const half4 v0 = *(const half4 *)vp, v1 = *(const half4 *)(vp + 8);
                         vb[dt][0] = v0[0]; vb[dt][1] = v0[1]; vb[dt][2] = v0[2]; vb[dt][3] = v0[3];
                         vb[dt][4] = v1[0]; vb[dt][5] = v1[1]; vb[dt][6] = v1[2]; vb[dt][7] = v1[3];
@@ -972,7 +978,7 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
     }
 }
 
-// One sweep over the key tiles (PASS 0: max, 1: exp sum, 2: P16 V).  Tiles
+// One sweep over the key tiles (PASS 0: max, 1: exp sum and P V).  Tiles
 // go global -> registers -> LDS with two register stages: while tile kt is
 // computed from LDS, tile kt + 1 sits in one register set (stored to the
 // other LDS buffer after the compute) and tile kt + 2's loads are in flight
@@ -988,29 +994,37 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
     const int tid = threadIdx.x;
     const int Tp = a.Tp;
     const int ntiles = (a.T + AT4_KT - 1) / AT4_KT;
-    constexpr int NT = 128 * NW;          // threads: NW query blocks x 2 key halves
-    constexpr int SCH = 512 / NT;         // 16-byte chunks per thread of an 8 KB tile
-    constexpr int VCH = PASS >= 2 ? SCH : 1;
-    const int kb = (threadIdx.x >> 6) / NW;  // this wave's 32-key half of every tile
+    constexpr int NT = 64 * AT4_KQ * NW;  // threads: NW query blocks x KQ key parts
+    constexpr int SCH = AT4_KT * 8 / NT;  // 16-byte chunks per thread of a K (or V^T) tile
+    constexpr int VCH = PASS >= 1 ? SCH : 1;
+    constexpr int VCPR = AT4_KT / 8;      // 16-byte chunks per V^T tile row
+    const int kb = (threadIdx.x >> 6) / NW;  // this wave's 32-key part of every tile
     a4vec kA[SCH], vA[VCH], kB[SCH], vB[VCH];
-    // this thread's 16-byte chunks of a tile: rows (tid >> 3) + 8 NW i, column (tid & 7) * 8
+    // this thread's 16-byte chunks of a tile: K rows (tid >> 3) + (NT / 8) i,
+    // column (tid & 7) * 8; V^T rows tid / VCPR + (NT / VCPR) i, column (tid % VCPR) * 8.
+    // Keys past Tp (the last tile when T is not a multiple of the tile) are
+    // read clamped: masked scores, finite values
     const int crow = tid >> 3, ccol = (tid & 7) * 8;
+    const int vrow = tid / VCPR, vcol = (tid % VCPR) * 8;
 #define ATT4_GLOAD(KT, KR, VR)                                                                  \
     {                                                                                           \
         const int kt_ = (KT) < ntiles ? (KT) : ntiles - 1;                                      \
         const int key0_ = kt_ * AT4_KT;                                                         \
         _Pragma("unroll") for (int i = 0; i < SCH; ++i) {                                       \
-            const int row = crow + i * (NT / 8);                                                \
-            KR[i] = *(const a4vec *)(K + (int64_t)(key0_ + row) * 64 + ccol);                   \
-            if constexpr (PASS >= 2) VR[i] = *(const a4vec *)(Vt + (int64_t)row * Tp + key0_ + ccol); \
+            const int kr_ = key0_ + crow + i * (NT / 8);                                        \
+            KR[i] = *(const a4vec *)(K + (int64_t)(kr_ < Tp ? kr_ : Tp - 1) * 64 + ccol);       \
+            if constexpr (PASS >= 1) {                                                          \
+                const int vc_ = key0_ + vcol;                                                   \
+                VR[i] = *(const a4vec *)(Vt + (int64_t)(vrow + i * (NT / VCPR)) * Tp + (vc_ < Tp ? vc_ : Tp - 8)); \
+            }                                                                                   \
         }                                                                                       \
     }
 #define ATT4_SSTORE(BUF, KR, VR)                                                                \
     {                                                                                           \
         _Pragma("unroll") for (int i = 0; i < SCH; ++i) {                                       \
-            const int row = crow + i * (NT / 8);                                                \
-            *(a4vec *)(Ks + ((BUF) * AT4_KT + row) * AT4_LD + ccol) = KR[i];                    \
-            if constexpr (PASS >= 2) *(a4vec *)(Vs + ((BUF) * AT4_KT + row) * AT4_LD + ccol) = VR[i]; \
+            *(a4vec *)(Ks + ((BUF) * AT4_KT + crow + i * (NT / 8)) * AT4_LD + ccol) = KR[i];    \
+            if constexpr (PASS >= 1)                                                            \
+                *(a4vec *)(Vs + ((BUF) * 64 + vrow + i * (NT / VCPR)) * AT4_VLD + vcol) = VR[i]; \
         }                                                                                       \
     }
     ATT4_GLOAD(0, kA, vA)
@@ -1022,7 +1036,7 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
         const int buf = kt & 1;
         a4vec kF[SCH], vF[VCH];  // tile kt + 2, requested before this tile's compute
         ATT4_GLOAD(kt + 2, kF, vF)
-        attn4_tile<PASS, false>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * AT4_KT * AT4_LD, kt * AT4_KT, kb, tab, qf,
+        attn4_tile<PASS, false>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * 64 * AT4_VLD, kt * AT4_KT, kb, tab, qf,
                                 mx, sum, m, inv, o0, o1);
         ATT4_SSTORE(buf ^ 1, kB, vB)  // (after the last tile: unread)
         __syncthreads();
@@ -1032,7 +1046,8 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
         for (int i = 0; i < VCH; ++i) vB[i] = vF[i];
     }
     if (nfull < ntiles) {  // the partial tile (stored by the last iteration)
-        attn4_tile<PASS, true>(a, Ks + (nfull & 1) * AT4_KT * AT4_LD, Vs + (nfull & 1) * AT4_KT * AT4_LD, nfull * AT4_KT, kb,
+        const int buf = nfull & 1;
+        attn4_tile<PASS, true>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * 64 * AT4_VLD, nfull * AT4_KT, kb,
                                tab, qf, mx, sum, m, inv, o0, o1);
         __syncthreads();  // (callers reuse the tile buffers: as after every loop tile)
     }
@@ -1040,16 +1055,17 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
 #undef ATT4_SSTORE
 }
 
-// Waves w and w + NW share query block w and split every 64-key tile into
-// its two 32-key halves (twice the waves per query, for one clip's small
-// grid); their maxima, exact double sums and partial P16 V meet in LDS.
+// Waves w, w + NW, .. w + (KQ - 1) NW share query block w and split every
+// tile into its KQ 32-key parts (KQ times the waves per query, for one clip's
+// small grid); their maxima, exact double sums and partial P V meet in LDS,
+// the partial O added in part order.
 template <int NW>
-__global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
+__global__ __launch_bounds__(64 * AT4_KQ * NW) void k_attn_enc4(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
     uint16_t *tab = (uint16_t *)smraw;
     const int tab_bytes = (((a.n_exp + 1) * 2 + 15) / 16) * 16;
-    f16 *Ks = (f16 *)(smraw + tab_bytes);      // [2][64 keys][AT4_LD]
-    f16 *Vs = Ks + 2 * AT4_KT * AT4_LD;        // [2][64 dims][AT4_LD] (V^T tile)
+    f16 *Ks = (f16 *)(smraw + tab_bytes);      // [2][KT keys][AT4_LD]
+    f16 *Vs = Ks + 2 * AT4_KT * AT4_LD;        // [2][64 dims][AT4_VLD] (V^T tile)
     const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int lr = lane & 31, lh = lane >> 5;
@@ -1058,7 +1074,7 @@ __global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
     const f16 *K = (const f16 *)a.k + bh * a.Tp * 64;
     const f16 *Vt = (const f16 *)a.vt + bh * 64 * a.Tp;
     const int T = a.T;
-    const int qw = w % NW, kb = w / NW;  // query block, key half
+    const int qw = w % NW, kb = w / NW;  // query block, key part
     const int q0 = (qb * NW + qw) * 32;  // this wave's queries
     half8 qf[4];
     {
@@ -1069,12 +1085,11 @@ __global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
     {
         const int nch = (a.n_exp + 1 + 7) / 8;  // through the 0 at index n_exp
         const uint4 *tsrc = (const uint4 *)a.exp_tab;
-        for (int i = tid; i < nch; i += 128 * NW) ((uint4 *)tab)[i] = tsrc[i];
+        for (int i = tid; i < nch; i += 64 * AT4_KQ * NW) ((uint4 *)tab)[i] = tsrc[i];
     }
-    // exchange slots for the key-half partner (the V buffers: unused until sweep 2)
-    float *xm = (float *)Vs;                    // [2 NW][64]
-    double *xd = (double *)(xm + 2 * NW * 64);  // [2 NW][64]
-    const int partner = kb ? w - NW : w + NW;
+    // exchange slots for the key-part partners (the V buffers: unused until sweep 2)
+    float *xm = (float *)Vs;                          // [KQ NW][64]
+    double *xd = (double *)(xm + AT4_KQ * NW * 64);  // [KQ NW][64]
     float mx = -INFINITY;
     double sum = 0.0;
     floatx16 o0, o1;
@@ -1084,51 +1099,44 @@ __global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     xm[w * 64 + lane] = mx;
     __syncthreads();
-    const float m = fmaxf(mx, xm[partner * 64 + lane]) * a.scale + 0.0f;  // max of the raw scores, scaled once (never -0)
-#ifndef WMI_ATTN3
-    // two sweeps: the second takes p = table exp of f16(S - m) as the P.V
-    // operand (an f16 value, exact) while summing it, and O is divided by the
-    // sum at the end; ggml rounds f16(p / sum) first (the weights differ by
-    // that rounding: one sweep of Q K^T and table reads fewer)
+#pragma unroll
+    for (int j = 0; j < AT4_KQ; ++j) mx = fmaxf(mx, xm[(qw + NW * j) * 64 + lane]);
+    const float m = mx * a.scale + 0.0f;  // max of the raw scores, scaled once (never -0)
     __syncthreads();  // (the exchange slots above are V buffers in the sweep)
-    attn4_sweep<NW, 3>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
+    attn4_sweep<NW, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
     sum = sum + __shfl_xor(sum, 32);
     xd[w * 64 + lane] = sum;  // (the sweep's last barrier freed the V buffers)
     __syncthreads();
-    const double dsum = kb ? xd[partner * 64 + lane] + sum : sum + xd[partner * 64 + lane];
-    const float inv = (float)(1.0 / dsum);
-    __syncthreads();  // (the exchange slots are read before the O exchange reuses Ks)
-#else
-    attn4_sweep<NW, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
-    sum = sum + __shfl_xor(sum, 32);
-    xd[w * 64 + lane] = sum;
-    __syncthreads();
     // exact double sums of f16 table values: the total is order-independent
-    const double d = kb ? xd[partner * 64 + lane] + sum : sum + xd[partner * 64 + lane];
-    const float inv = (float)(1.0 / (double)(float)d);
-    __syncthreads();  // the exchange slots are V buffers again in sweep 2
-    attn4_sweep<NW, 2>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, inv, o0, o1);
-#endif
-    // second key half's partial O -> LDS (the K / V buffers are free now),
-    // added to the first half's in that order
-    float *xo = (float *)Ks;  // [NW][32][64]
+    double dsum = 0.0;
+#pragma unroll
+    for (int j = 0; j < AT4_KQ; ++j) dsum += xd[(qw + NW * j) * 64 + lane];
+    const float inv = (float)(1.0 / dsum);
+    __syncthreads();  // (the exchange slots are read before the O exchange reuses the LDS)
+    // key parts 1 .. KQ - 1: partial O -> LDS (the K / V buffers are free
+    // now), added to part 0's in part order
+    float *xo = (float *)smraw;  // [KQ - 1][NW][32][64] over the table and tiles (free now)
     if (kb) {
+        float *xp = xo + (size_t)(kb - 1) * NW * 32 * 64;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int qq = (r & 3) + 8 * (r >> 2) + 4 * lh;
-            xo[(qw * 32 + qq) * 64 + lr] = o0[r];
-            xo[(qw * 32 + qq) * 64 + 32 + lr] = o1[r];
+            xp[(qw * 32 + qq) * 64 + lr] = o0[r];
+            xp[(qw * 32 + qq) * 64 + 32 + lr] = o1[r];
         }
     }
     __syncthreads();
     if (kb) return;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int qq = (r & 3) + 8 * (r >> 2) + 4 * lh;
-        o0[r] = o0[r] + xo[(qw * 32 + qq) * 64 + lr];
-        o1[r] = o1[r] + xo[(qw * 32 + qq) * 64 + 32 + lr];
+    for (int j = 1; j < AT4_KQ; ++j) {
+        const float *xp = xo + (size_t)(j - 1) * NW * 32 * 64;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int qq = (r & 3) + 8 * (r >> 2) + 4 * lh;
+            o0[r] = o0[r] + xp[(qw * 32 + qq) * 64 + lr];
+            o1[r] = o1[r] + xp[(qw * 32 + qq) * 64 + 32 + lr];
+        }
     }
-#ifndef WMI_ATTN3
     // (inv is per query: lane lr's inv belongs to query lr; row r of the
     // accumulators holds query (r & 3) + 8 (r >> 2) + 4 lh)
 #pragma unroll
@@ -1138,7 +1146,6 @@ __global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
         o0[r] = o0[r] * iq;
         o1[r] = o1[r] * iq;
     }
-#endif
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int t = q0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -1158,23 +1165,32 @@ __global__ __launch_bounds__(128 * NW) void k_attn_enc4(AttnArgs a) {
 template <int NW>
 static hipError_t attn_enc4_launch(hipStream_t s, const AttnArgs &a) {
     const size_t tabb = (((a.n_exp + 1) * 2 + 15) / 16) * 16;
-    const size_t lds = tabb + (size_t)4 * AT4_KT * AT4_LD * 2;
+    const size_t tiles = (size_t)2 * AT4_KT * AT4_LD * 2 + (size_t)2 * 64 * AT4_VLD * 2;
+    const size_t xob = (size_t)(AT4_KQ - 1) * NW * 32 * 64 * 4;  // the partial-O exchange (over table + tiles)
+    const size_t lds = tabb + tiles > xob ? tabb + tiles : xob;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     hipError_t e = allow_lds(k_attn_enc4<NW>, lds);
     if (e != hipSuccess) return e;
     dim3 grid(cdiv(a.T, 32 * NW), a.H, a.n_clips);
-    hipLaunchKernelGGL(k_attn_enc4<NW>, grid, dim3(128 * NW), lds, s, a);
+    hipLaunchKernelGGL(k_attn_enc4<NW>, grid, dim3(64 * AT4_KQ * NW), lds, s, a);
     return hipGetLastError();
+}
+
+// Query blocks per workgroup, each with KQ = 4 key-part waves: 4 once the
+// grid holds >= 2 workgroups per CU (8 clips of base: 2.38 ms at 2, 2.25-2.30
+// at 4 — 1024 threads, 20 VGPRs spilled — as more waves per CU hide more),
+// else 2.  NW does not change a wave's arithmetic, so a clip's result is
+// batch-independent.  (KQ = 4 against KQ = 2: one clip 0.69 -> 0.64 ms,
+// eight 2.09 -> 2.25-2.30 ms, profiles/r05/enc_kq4_ab.txt)
+int attn_enc_nw(int T, int H, int n_clips, int nw_knob) {
+    if (nw_knob == 1 || nw_knob == 2 || nw_knob == 4) return nw_knob;
+    return (int64_t)cdiv(T, 128) * H * n_clips >= 512 ? 4 : 2;
 }
 
 hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a) {
     const Tune &tn = tune_of(a.tune);
     if (a.T < 1 || a.Tp % 64 || a.Tp < a.T) return hipErrorInvalidValue;
-    // 4 query blocks per workgroup once the grid holds >= 2 workgroups per
-    // CU, else 2 (one clip: 52 vs 62 us at NW 2 / 4); the arithmetic per wave
-    // does not depend on NW, so a clip's result is batch-independent
-    int nw = tn.enc_attn_nw;
-    if (nw != 1 && nw != 2 && nw != 4) nw = (int64_t)cdiv(a.T, 128) * a.H * a.n_clips >= 512 ? 4 : 2;
+    const int nw = attn_enc_nw(a.T, a.H, a.n_clips, tn.enc_attn_nw);
     if (nw == 4) return attn_enc4_launch<4>(s, a);
     if (nw == 2) return attn_enc4_launch<2>(s, a);
     return attn_enc4_launch<1>(s, a);
