@@ -922,7 +922,7 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 template <int PASS, bool TAIL>
 __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, const f16 *Vb, int key0, int kb,
                                            const uint16_t *tab, const half8 (&qf)[4], float &mx, double &sum,
-                                           float m, float inv, floatx16 &o0, floatx16 &o1) {
+                                           float m, floatx16 &o0, floatx16 &o1) {
     const int lane = threadIdx.x & 63, lr = lane & 31, lh = lane >> 5;
     const int T = a.T;
     const uint32_t n_exp = (uint32_t)a.n_exp;
@@ -990,7 +990,7 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
 template <int NW, int PASS>
 __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, const f16 *Vt, f16 *Ks, f16 *Vs,
                                             const uint16_t *tab, const half8 (&qf)[4], float &mx, double &sum,
-                                            float m, float inv, floatx16 &o0, floatx16 &o1) {
+                                            float m, floatx16 &o0, floatx16 &o1) {
     const int tid = threadIdx.x;
     const int Tp = a.Tp;
     const int ntiles = (a.T + AT4_KT - 1) / AT4_KT;
@@ -1037,7 +1037,7 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
         a4vec kF[SCH], vF[VCH];  // tile kt + 2, requested before this tile's compute
         ATT4_GLOAD(kt + 2, kF, vF)
         attn4_tile<PASS, false>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * 64 * AT4_VLD, kt * AT4_KT, kb, tab, qf,
-                                mx, sum, m, inv, o0, o1);
+                                mx, sum, m, o0, o1);
         ATT4_SSTORE(buf ^ 1, kB, vB)  // (after the last tile: unread)
         __syncthreads();
 #pragma unroll
@@ -1048,7 +1048,7 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
     if (nfull < ntiles) {  // the partial tile (stored by the last iteration)
         const int buf = nfull & 1;
         attn4_tile<PASS, true>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * 64 * AT4_VLD, nfull * AT4_KT, kb,
-                               tab, qf, mx, sum, m, inv, o0, o1);
+                               tab, qf, mx, sum, m, o0, o1);
         __syncthreads();  // (callers reuse the tile buffers: as after every loop tile)
     }
 #undef ATT4_GLOAD
@@ -1095,7 +1095,7 @@ __global__ __launch_bounds__(64 * AT4_KQ * NW) void k_attn_enc4(AttnArgs a) {
     floatx16 o0, o1;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { o0[r] = 0.0f; o1[r] = 0.0f; }
-    attn4_sweep<NW, 0>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, 0.0f, 0.0f, o0, o1);
+    attn4_sweep<NW, 0>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, 0.0f, o0, o1);
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     xm[w * 64 + lane] = mx;
     __syncthreads();
@@ -1103,7 +1103,7 @@ __global__ __launch_bounds__(64 * AT4_KQ * NW) void k_attn_enc4(AttnArgs a) {
     for (int j = 0; j < AT4_KQ; ++j) mx = fmaxf(mx, xm[(qw + NW * j) * 64 + lane]);
     const float m = mx * a.scale + 0.0f;  // max of the raw scores, scaled once (never -0)
     __syncthreads();  // (the exchange slots above are V buffers in the sweep)
-    attn4_sweep<NW, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
+    attn4_sweep<NW, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, o0, o1);
     sum = sum + __shfl_xor(sum, 32);
     xd[w * 64 + lane] = sum;  // (the sweep's last barrier freed the V buffers)
     __syncthreads();
