@@ -144,17 +144,22 @@ struct NoPre {
 // pre() runs once in every thread while its first round of loads is in
 // flight (the q5_1 phases dequantise their prefetched weights there, so the
 // VALU work overlaps the seam instead of following it).
-template <int PU = 4, typename F, typename Pre = NoPre>  // PU: granules in flight per thread
+// T0 / NTH: the threads that poll (threads T0 .. T0 + NTH - 1; NTH a
+// multiple of 64: whole waves) — e.g. a wave with few loads of its own queued
+// in front of the poll's, since vmcnt retires in order and a poll round
+// cannot see its granules before every older load of its wave has landed
+template <int PU = 4, int T0 = 0, int NTH = PT, typename F, typename Pre = NoPre>  // PU: granules in flight per thread
 __device__ __forceinline__ bool gpoll(int cnt, uint32_t tag, F addr, uint32_t *dst, uint32_t *abortw, uint32_t *err,
                                       Pre pre = Pre{}) {
     bool ok = true, pre_done = false;
-    int tid = (int)threadIdx.x;
+    int tid = (int)threadIdx.x - T0;
     asm volatile("" : "+v"(tid));
-    for (int base = tid; base < cnt && ok; base += PT * PU) {
+    const bool mine = tid >= 0 && tid < NTH;
+    for (int base = tid; mine && base < cnt && ok; base += NTH * PU) {
         uint64_t v[PU];
 #pragma unroll
         for (int u = 0; u < PU; ++u) {
-            const int i = base + PT * u;
+            const int i = base + NTH * u;
             v[u] = i < cnt ? gld(addr(i)) : ((uint64_t)tag << 32);
         }
         if (!pre_done) {
@@ -167,7 +172,7 @@ __device__ __forceinline__ bool gpoll(int cnt, uint32_t tag, F addr, uint32_t *d
             for (int u = 0; u < PU; ++u)
                 if ((uint32_t)(v[u] >> 32) != tag) {
                     all = false;
-                    v[u] = gld(addr(base + PT * u));
+                    v[u] = gld(addr(base + NTH * u));
                 }
             if (all) break;
             if ((it & 15) == 15) {
@@ -182,7 +187,7 @@ __device__ __forceinline__ bool gpoll(int cnt, uint32_t tag, F addr, uint32_t *d
         }
 #pragma unroll
         for (int u = 0; u < PU; ++u) {
-            const int i = base + PT * u;
+            const int i = base + NTH * u;
             if (i < cnt) dst[i] = (uint32_t)v[u];
         }
     }
@@ -1212,7 +1217,12 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     PREFETCH_ISSUED
                     __syncthreads();
                     const int64_t hq = b * (NS / 2) + h * 32;  // q, k, v granule blocks lie 4 NS apart
-                    const bool ok = gpoll(96, ptag(pos, L, l, 0),
+                    // polled by the last wave: its score lanes hold keys >= 192
+                    // (no cache-row loads before position 192) and its value
+                    // lanes the fewest, so the poll does not wait for the
+                    // cache rows the other waves requested (base 121.6 ->
+                    // 118.6 us a step, profiles/r05/bpoll_lastwave_ab.txt)
+                    const bool ok = gpoll<2, PT - 64, 64>(96, ptag(pos, L, l, 0),
                                           [=](int i) { return xg + oQ + (i >> 5) * (4 * NS) + hq + (i & 31); },
                                           (uint32_t *)qn, abortw, a.err);
                     if (check(ok)) return;
