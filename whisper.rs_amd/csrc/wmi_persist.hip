@@ -1405,16 +1405,19 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         half8 kf[4], vf[4];
 #pragma unroll
                         for (int i = 0; i < 4; ++i) kf[i] = sld((const half8 *)(Kb + (int64_t)(key < j1 ? key : j1 - 1) * NS + 8 * i));
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int kv = j0 + jg * 4 + u;
-                            vf[u] = sld((const half8 *)(Vb + (int64_t)(kv < j1 ? kv : j1 - 1) * NS));
-                        }
                         PREFETCH_ISSUED
                         __syncthreads();
                         const bool ok = gpoll(B * 32, ptag(pos, L, l, 3),
                                               [=](int i) { return xg + oXQ + (i >> 5) * (NS / 2) + h * 32 + (i & 31); },
                                               (uint32_t *)qb, abortw, a.err);
+                        // the value rows (wanted after the scores and the exp
+                        // sums) behind the poll, which then waits for the key
+                        // rows only (vmcnt retires in order)
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int kv = j0 + jg * 4 + u;
+                            vf[u] = sld((const half8 *)(Vb + (int64_t)(kv < j1 ? kv : j1 - 1) * NS));
+                        }
                         if (check(ok)) return;
                 PSTAMP(l * 32 + 20)
                         // (rows unrolled: their dot chains and max reductions interleave)
@@ -1506,14 +1509,21 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                             for (int i = 0; i < 4; ++i)
                                 kf[p][i] = 128 * p < CL ? sld((const half8 *)(Kb + (int64_t)key * NS + 8 * i)) : z8;
                         }
+                        auto v_load = [&] {
 #pragma unroll
-                        for (int p = 0; p < NKE; ++p)
+                            for (int p = 0; p < NKE; ++p)
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                int kv = j0 + 128 * p + jg * 4 + u;
-                                kv = kv < j1 ? kv : j1 - 1;
-                                vf[p][u] = 128 * p < CL ? sld((const half8 *)(Vb + (int64_t)kv * NS)) : z8;
-                            }
+                                for (int u = 0; u < 4; ++u) {
+                                    int kv = j0 + 128 * p + jg * 4 + u;
+                                    kv = kv < j1 ? kv : j1 - 1;
+                                    vf[p][u] = 128 * p < CL ? sld((const half8 *)(Vb + (int64_t)kv * NS)) : z8;
+                                }
+                        };
+                        // (the value rows: with the key rows where the task
+                        // computes its cross q — the q GEMV covers them — else
+                        // behind the poll of q, which then waits for the key
+                        // rows only: vmcnt retires in order)
+                        if constexpr (XQF) v_load();
                         if constexpr (XQF) {
                             // this head's cross q from x' directly: LNc(x'_b) and
                             // Wcq rows h*64 .. h*64+63, the D phase's arithmetic
@@ -1541,6 +1551,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                             const bool ok = gpoll(32, ptag(pos, L, l, 3),
                                                   [=](int i) { return xg + oXQ + b * (NS / 2) + h * 32 + i; }, (uint32_t *)qh,
                                                   abortw, a.err);
+                            v_load();
                             if (check(ok)) return;
                 PSTAMP(l * 32 + 20)
                         }
