@@ -1079,7 +1079,11 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 const uint32_t tag = ptag(pos, L, l, 0);
                 PSet<NS, BT, KC, 2, KS_A, Q5> S;
                 const bool act = ra0 < ra1;
-                S.load(lmat<Q5>(P.wqkv, P.wqkv5, 3 * NS * NS), P.bqkv, NS, ra0, ra1, slot, l16);
+                // (layer 0 of a generated position: requested after the
+                // argmax gather, which then does not wait for them — they are
+                // wanted only after the token's embedding row and its LayerNorm)
+                const bool late_w = l == 0 && pos >= a.feed_len && step > 0;
+                if (!late_w) S.load(lmat<Q5>(P.wqkv, P.wqkv5, 3 * NS * NS), P.bqkv, NS, ra0, ra1, slot, l16);
                 LnP<NS> lp;
                 Ln1P<NS> l1;
                 if constexpr (BT == 1) ln1_params<NS>(P.ln1_w, P.ln1_b, l1, tid);
@@ -1096,6 +1100,7 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         __syncthreads();
                     } else {
                         if (!argmax_gather(pos - 1)) return;
+                        S.load(lmat<Q5>(P.wqkv, P.wqkv5, 3 * NS * NS), P.bqkv, NS, ra0, ra1, slot, l16);
                         if (wg == 0 && tid < B && pos - a.feed_len < a.out_stride)
                             a.tokens_out[tid * a.out_stride + (pos - a.feed_len)] = sh.tok[tid];
                     }
