@@ -1081,8 +1081,11 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                 const bool act = ra0 < ra1;
                 // (layer 0 of a generated position: requested after the
                 // argmax gather, which then does not wait for them — they are
-                // wanted only after the token's embedding row and its LayerNorm)
-                const bool late_w = l == 0 && pos >= a.feed_len && step > 0;
+                // wanted only after the token's embedding row and its LayerNorm:
+                // base 1859 -> 1890 audio-s/s, profiles/r05/l0_weights_after_argmax_ab.txt.
+                // Not the q5_1 instances, whose dequantisation right behind the
+                // loads would then also hold up the embedding loads)
+                const bool late_w = !Q5 && l == 0 && pos >= a.feed_len && step > 0;
                 if (!late_w) S.load(lmat<Q5>(P.wqkv, P.wqkv5, 3 * NS * NS), P.bqkv, NS, ra0, ra1, slot, l16);
                 LnP<NS> lp;
                 Ln1P<NS> l1;
