@@ -55,17 +55,21 @@ constexpr uint32_t PSPIN = 1u << 19;    // polls before a seam is declared dead
 constexpr int NPH = 11;                 // phases per decoder layer
 constexpr int PMAXB = 8;                // decoder rows
 constexpr int RNMAX = 16;               // rows of an n-row GEMV per workgroup
-// attention / argmax scratch in LDS.  One-row instances use at most ~3 KB
-// (a cross task's q and p values, G1's sub-chunk partials, the argmax
-// candidates [G][2]); the multi-row ones also keep the beam-shared task's
-// [B][4][64] P.V partials (from XS_OFF + XS_BYTES) and the MFMA GEMV
-// partials, so the one-row instances keep 8 KB more vocabulary rows resident
-__host__ __device__ constexpr int scr_bytes(int BT) { return BT == 1 ? 16 * 1024 : 24 * 1024; }
+// attention / argmax scratch in LDS.  One-row instances use at most ~4.3 KB
+// (G1's sub-chunk partials [16][64] + stats; a cross task's q and p values
+// 2 KB, the self-attention's q / k / v and P16 1.5 KB, the argmax candidates
+// [G][2] 2 KB); the multi-row ones also keep the beam-shared task's [B][4][64]
+// P.V partials (from XS_OFF + XS_BYTES) and the MFMA GEMV partials, so the
+// one-row instances keep 16 KB more vocabulary rows resident
+__host__ __device__ constexpr int scr_bytes(int BT) { return BT == 1 ? 8 * 1024 : 24 * 1024; }
 constexpr int NKP = 4;                  // 128-key passes per cross-attention chunk (cl <= 512)
 constexpr int EXPFB = 64;               // exp fallback list entries (exp_f16_fast)
 constexpr int XS_OFF = 1024;            // cross-attention task scores / p in the LDS scratch
 constexpr int XS_BYTES = 8192;          // (a task's p values: rows x keys x 4 B)
 constexpr int NSUBM = 16;               // 128-key sub-chunks of a row (T <= 2048)
+static_assert(NSUBM * 64 * 4 + NSUBM * 3 * 4 <= scr_bytes(1) && PX_GMAX * 2 * 4 <= scr_bytes(1) &&
+                  XS_OFF + 2 * 128 * 4 <= scr_bytes(1) && 512 + 512 * 2 <= scr_bytes(1),
+              "one-row scratch: G1 partials, argmax candidates, a cross task's p, P16");
 
 __device__ __forceinline__ uint64_t gld(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
