@@ -247,7 +247,15 @@ int wmi_get_checksums(const wmi_context *ctx, float *out5);
  * decoder fills them only with WMI_PERSIST_LOGITS=1), 3 = the persistent
  * decoder's exchange block (8-byte {tag, value} granules), 4-9 = decoder
  * chain scratch, 10 = this context's tuning knobs (9 int32, host copy; the
- * WMI_* environment is read once per context at wmi_init_from_file). */
+ * WMI_* environment is read once per context at wmi_init_from_file),
+ * 11 = decodes re-run on the kernel chain (int32, host), 12 = the encoder
+ * residual stream, 13 = every position's logits [n_text_ctx][rows][n_vocab]
+ * f32 of the last persistent greedy decode (clip b in row b) or beam search
+ * (slot s in row s; contexts created with WMI_LOGITS_ALL=1), 14 / 15 = the
+ * last beam search's parent slots / tokens [n_text_ctx][8] int32 (its last
+ * clip), 16 = the rows of 13 (int32, host: max(8, max_clips)), 17 = the
+ * persistent decoder's grid per row count (int32 [9], host; -1 = not sized
+ * yet, 0 = kernel chain). */
 int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes);
 
 /* ---- parity getters (copy device results into caller-owned buffers) --- */

@@ -46,7 +46,7 @@ def lib():
         L.or_decode_greedy.argtypes = [vp, hp_, hp_, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.POINTER(i32), fp]
         L.or_dequant.argtypes = [C.c_int, C.c_void_p, C.c_int64, hp_]
         L.or_decode_beam.argtypes = [vp, hp_, hp_, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, ip, C.POINTER(i32),
-                                     C.POINTER(C.c_double), C.POINTER(C.c_float), fp]
+                                     C.POINTER(C.c_double), C.POINTER(C.c_float), fp, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -86,6 +86,7 @@ def tables():
 class OracleModel:
     def __init__(self, path: str):
         self.h = None
+        self.path = path
         L = lib()
         h = C.c_void_p()
         err = C.create_string_buffer(512)
@@ -167,21 +168,28 @@ class OracleModel:
         return toks[:n.value], margins[:n.value]
 
     def decode_beam(self, ck, cv, beam: int, max_tokens: int, suppress_eot: bool = False, n_threads: int = 8,
-                    step_gaps: bool = False):
+                    step_gaps: bool = False, trace: bool = False):
         """Beam search (wmi_oracle.h): (tokens, score, smallest selection margin),
-        plus each step's selection margin when step_gaps."""
+        plus each step's selection margin when step_gaps, plus with trace a
+        dict: "logits" [steps][beam][V] (each active hypothesis' logits before
+        EOT suppression, NaN rows where inactive), "sel" [steps][beam][2]
+        ((parent, token) of the slots after each step, -1 where unfilled)."""
         toks = np.zeros(max_tokens + 1, np.int32)
         n = C.c_int32()
         score = C.c_double()
         gap = C.c_float()
         sg = np.zeros(max_tokens, np.float32)
+        tr = None
+        if trace:
+            tr = {"logits": np.full((max_tokens, beam, self.hp["n_vocab"]), np.nan, np.float32),
+                  "sel": np.full((max_tokens, beam, 2), -1, np.int32)}
         rc = lib().or_decode_beam(self.h, ck, cv, ck.shape[1], beam, max_tokens, int(suppress_eot), n_threads, toks,
-                                  C.byref(n), C.byref(score), C.byref(gap), sg)
+                                  C.byref(n), C.byref(score), C.byref(gap), sg,
+                                  tr["logits"].ctypes.data if trace else None, tr["sel"].ctypes.data if trace else None)
         if rc:
             raise OracleError(rc, "decode_beam")
-        if step_gaps:
-            return toks[:n.value], score.value, gap.value, sg
-        return toks[:n.value], score.value, gap.value
+        out = (toks[:n.value], score.value, gap.value) + ((sg,) if step_gaps else ())
+        return out + (tr,) if trace else out
 
 
 # ---------------------------------------------------------------------------

@@ -1256,7 +1256,7 @@ static double row_lse(const float *lg, int V) {
 
 int or_decode_beam(const or_model *m, const uint16_t *cross_k, const uint16_t *cross_v, int n_ctx, int beam,
                    int max_tokens, int suppress_eot, int nt, int32_t *tokens_out, int32_t *n_out, double *score_out,
-                   float *min_gap, float *step_gap) {
+                   float *min_gap, float *step_gap, float *step_logits, int32_t *step_sel) {
     if (n_ctx <= 0) n_ctx = m->hp[HP_N_AUDIO_CTX];
     if (beam < 1 || beam > 8 || max_tokens < 1) return WMI_E_INVALID_ARG;
     int32_t prompt[8];
@@ -1287,6 +1287,7 @@ int or_decode_beam(const or_model *m, const uint16_t *cross_k, const uint16_t *c
         for (int b = 0; b < n_active; ++b) {
             float *row = lg + (size_t)b * V;
             dec_step(m, &cur[b], cross_k, cross_v, n_ctx, tok[b], pos, row, nt);
+            if (step_logits) memcpy(step_logits + ((size_t)t * K + b) * V, row, sizeof(float) * V);
             if (suppress_eot) row[eot] = -INFINITY;
             const double lse = row_lse(row, V);
             int ids[9];
@@ -1332,6 +1333,10 @@ int or_decode_beam(const or_model *m, const uint16_t *cross_k, const uint16_t *c
                 if (step_gap) step_gap[t] = g;
                 break;
             }
+        for (int s = 0; s < na && step_sel; ++s) {
+            step_sel[((size_t)t * K + s) * 2] = parent[s];
+            step_sel[((size_t)t * K + s) * 2 + 1] = ntok[s];
+        }
         for (int s = 0; s < na; ++s) {
             const int p = parent[s];
             memcpy(nhist + (size_t)s * max_tokens, hist + (size_t)p * max_tokens, 4 * t);

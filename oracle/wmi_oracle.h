@@ -96,10 +96,14 @@ int or_decode_greedy(const or_model *m, const uint16_t *cross_k, const uint16_t 
  * min_gap (optional) the smallest selection margin met (last kept vs first
  * rejected candidate at every step, best vs second in the final choice);
  * step_gap (optional, [max_tokens]) each step's selection margin (INFINITY
- * where none was met). */
+ * where none was met); step_logits (optional, [max_tokens][beam][n_vocab])
+ * active hypothesis b's logits at step t before EOT suppression — the same
+ * dec_step as or_decode_logits on its history, so teacher-forced logits —
+ * and step_sel (optional, [max_tokens][beam][2]) the slots after step t:
+ * (parent hypothesis, appended token); entries of inactive slots untouched. */
 int or_decode_beam(const or_model *m, const uint16_t *cross_k, const uint16_t *cross_v, int n_ctx, int beam,
                    int max_tokens, int suppress_eot, int n_threads, int32_t *tokens_out, int32_t *n_out,
-                   double *score_out, float *min_gap, float *step_gap);
+                   double *score_out, float *min_gap, float *step_gap, float *step_logits, int32_t *step_sel);
 
 #ifdef __cplusplus
 }

@@ -29,7 +29,7 @@ for step in "$@"; do
   case $name in
     tests)
       k=(); [ -n "$arg" ] && k=(-k "$arg")
-      timeout -k 10 1100 python3 -u -m pytest -x -v -s --timeout 700 --timeout-method thread tests/ -m gpu "${k[@]}" \
+      timeout -k 10 1100 python3 -u -m pytest -x -v -s --durations=40 --timeout 700 --timeout-method thread tests/ -m gpu "${k[@]}" \
         > ${O}_tests.log 2>&1; rc=$?
       grep -E "passed|failed|compared over|error" ${O}_tests.log | tail -n 4
       [ $rc -eq 0 ] || exit 1 ;;

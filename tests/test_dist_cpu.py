@@ -227,3 +227,88 @@ def test_rendezvous_survives_a_silent_connection():
         assert res["gather"] == ["hub", "peer"]
     finally:
         dist._HS_HUB = old
+
+
+def test_rendezvous_duplicate_rank_keeps_the_live_peer():
+    """A second process announcing a rank that already joined (with the full
+    handshake) is refused while the first one's socket is open; the first
+    peer stays in the group.  A rank whose first connection died
+    after its handshake is replaced by its reconnect."""
+    import struct
+    import threading
+    import time
+
+    import dist
+
+    def connect(port):
+        for _ in range(100):
+            try:
+                return socket.create_connection(("127.0.0.1", port), timeout=5)
+            except OSError:
+                time.sleep(0.05)
+        raise OSError("hub not listening")
+
+    def handshake(s, port, rank, world):
+        hello = dist._MAGIC + struct.pack("<ii", world, port)
+        dist._send(s, hello + struct.pack("<i", rank))
+        s.settimeout(5)
+        assert dist._recv(s) == hello
+        dist._send(s, dist._CONFIRM)
+
+    # (1) live duplicate: refused, the first rank 1 stays
+    port = _free_port()
+    res = {}
+
+    def hub3():
+        g = dist.Group(0, 3, "127.0.0.1", port, timeout=30)
+        res["gather"] = g.all_gather("hub")
+        g.close()
+
+    t = threading.Thread(target=hub3)
+    t.start()
+    first = {}
+    t1 = threading.Thread(target=lambda: first.setdefault("g", dist.Group(1, 3, "127.0.0.1", port, timeout=30)))
+    t1.start()
+    t1.join(30)
+    imp = connect(port)
+    handshake(imp, port, 1, 3)
+    assert imp.recv(1) == b""  # closed by the hub: rank 1 is taken by a live peer
+    imp.close()
+    out = {}
+    t2 = threading.Thread(target=lambda: out.setdefault("r2", dist.Group(2, 3, "127.0.0.1", port, timeout=30)
+                                                         .all_gather("two")))
+    t2.start()
+    assert first["g"].all_gather("one") == ["hub", "one", "two"]
+    t2.join(30)
+    t.join(30)
+    assert res["gather"] == ["hub", "one", "two"] and out["r2"] == ["hub", "one", "two"]
+    first["g"].close()
+
+    # (2) dead first connection: the reconnect replaces it
+    port = _free_port()
+    res.clear()
+
+    def hub2():
+        g = dist.Group(0, 3, "127.0.0.1", port, timeout=30)
+        res["gather"] = g.all_gather("hub")
+        g.close()
+
+    t = threading.Thread(target=hub2)
+    t.start()
+    dead = connect(port)
+    handshake(dead, port, 1, 3)
+    dead.close()
+    time.sleep(0.2)
+    again = {}
+    t1 = threading.Thread(target=lambda: again.setdefault("g", dist.Group(1, 3, "127.0.0.1", port, timeout=30)))
+    t1.start()
+    t1.join(30)
+    out.clear()
+    t2 = threading.Thread(target=lambda: out.setdefault("r2", dist.Group(2, 3, "127.0.0.1", port, timeout=30)
+                                                         .all_gather("two")))
+    t2.start()
+    assert again["g"].all_gather("one") == ["hub", "one", "two"]
+    t2.join(30)
+    t.join(30)
+    assert res["gather"] == ["hub", "one", "two"]
+    again["g"].close()

@@ -35,6 +35,34 @@ def f16_ulp_ok(a_bits, b_bits, max_ulps=1):
     return np.abs(a - b) <= max_ulps * ulp + 1e-12
 
 
+# The oracle's encoder outputs, memoised per (model file, clip, n_ctx,
+# mel_offset, dot mode): the tests encode the same clips in several places
+# (the floor needs a second, exact-dot encode), and a large-v3 encode takes
+# tens of seconds of the box's 16 host threads.  Oldest entries dropped first.
+_ENC_CACHE = {}
+_ENC_CACHE_MAX = 16
+
+
+def _oracle_encode(om, pcm, n_ctx, mel_offset=0, exact=False):
+    """(enc [n_ctx][n], cross_k, cross_v) of the oracle for pcm; exact: with
+    exact (double) dot products instead of ggml's order (the noise floor)."""
+    import hashlib
+    key = (om.path, hashlib.sha1(np.ascontiguousarray(pcm, np.float32).tobytes()).hexdigest(), n_ctx, mel_offset,
+           exact)
+    hit = _ENC_CACHE.pop(key, None)
+    if hit is None:
+        mel = om.mel(pcm, n_threads=threads())
+        pyoracle.set_dot_mode(exact)
+        try:
+            hit = om.encode(mel, n_ctx=n_ctx, mel_offset=mel_offset, n_threads=threads())
+        finally:
+            pyoracle.set_dot_mode(False)
+        while len(_ENC_CACHE) >= _ENC_CACHE_MAX:
+            _ENC_CACHE.pop(next(iter(_ENC_CACHE)))
+    _ENC_CACHE[key] = hit
+    return hit
+
+
 @pytest.fixture(scope="module")
 def wmi():
     import wmi as w
@@ -75,14 +103,12 @@ def test_mel_empty_and_short(micro_ctx, oracle_micro):
     assert micro_ctx.mel(0).shape == (80, 0)
 
 
-def _check_encoder(ctx, om, pcm, n_ctx, mel_offset=0):
-    mel = om.mel(pcm, n_threads=threads())
-    pyoracle.set_dot_mode(True)
-    try:
-        enc_exact = om.encode(mel, n_ctx=n_ctx, mel_offset=mel_offset, n_threads=threads())[0]
-    finally:
-        pyoracle.set_dot_mode(False)
-    enc_ref, ck_ref, cv_ref = om.encode(mel, n_ctx=n_ctx, mel_offset=mel_offset, n_threads=threads())
+def _check_encoder(ctx, om, pcm, n_ctx, mel_offset=0, pin=None):
+    """Encoder output and cross K / V against the oracle (module docstring's
+    bars); pin: additionally max |device - oracle| <= pin x floor (the
+    round-5 verdict's "back under the floor", base and large-v3)."""
+    enc_exact = _oracle_encode(om, pcm, n_ctx, mel_offset, exact=True)[0]
+    enc_ref, ck_ref, cv_ref = _oracle_encode(om, pcm, n_ctx, mel_offset)
     floor = np.abs(enc_exact - enc_ref).max()
     floor_mean = np.abs(enc_exact - enc_ref).mean()
     ctx.set_audio_ctx(n_ctx)
@@ -96,6 +122,8 @@ def _check_encoder(ctx, om, pcm, n_ctx, mel_offset=0):
           f"(noise floor max {floor:.3e} mean {floor_mean:.3e}; literal 1e-3 {'holds' if err.max() <= 1e-3 else 'exceeded'})")
     assert err.max() <= max(ENC_TOL, 1.25 * floor), (err.max(), floor)
     assert err.mean() <= max(3e-4, 1.25 * floor_mean), (err.mean(), floor_mean)
+    if pin is not None:
+        assert err.max() <= max(ENC_TOL, pin * floor), (err.max(), pin, floor)
     # the device result and the ggml-order oracle are two roundings of the
     # same exact (double-dot) result: the device must be as close to it as
     # ggml's own order is (scripts/enc_layer_err.py: ~1.0x at every layer of
@@ -165,18 +193,21 @@ def test_decoder_logits_full_text_ctx(micro_ctx, oracle_micro):
 GREEDY_GAP = 1e-3  # oracle top-2 margins below this may flip under f32 reordering
 # decoder logits: max |device - oracle| <= max(LOGIT_TOL, 1.25 x the logit
 # noise floor), the floor being |oracle in ggml's order - oracle with exact
-# (double) dots|, encoder included, on the same feed — the encoder bar's rule
+# (double) dots|, encoder included, on the same feed — the encoder bar's rule.
+# Accepted departures from ggml's rounding points in the persistent decoder
+# (they use part of the 1.25x headroom, so the large-v3 margin
+# is pinned at 1.0x its floor in test_step_logits_one_row):
+#  - self-attention: P V from the table values p, divided by the exact sum
+#    afterwards (ggml rounds P16 = f16(p / sum) first);
+#  - cross attention (flash-decoding): max, p and the exact sum per 128-key
+#    sub-chunk, combined in f32 with e^(m - M) (ggml: one row max).
+# The encoder attention keeps ggml's rounding points (P16 before P V).
 LOGIT_TOL = 2e-3
 
 
 def _exact_kv(om, pcm, n_ctx, mel_offset=0):
     """The oracle's cross K / V with exact (double) dot products."""
-    mel = om.mel(pcm, n_threads=threads())
-    pyoracle.set_dot_mode(True)
-    try:
-        return om.encode(mel, n_ctx=n_ctx, mel_offset=mel_offset, n_threads=threads())[1:]
-    finally:
-        pyoracle.set_dot_mode(False)
+    return _oracle_encode(om, pcm, n_ctx, mel_offset, exact=True)[1:]
 
 
 def _logits_ref(om, kv, kv_exact, feed):
@@ -282,6 +313,8 @@ def test_full_size_models(wmi, model_cache, model):
     om = pyoracle.OracleModel(path)
     ctx = wmi.WhisperContext.new(path, 0, max_clips=1)
     try:
+        if model == "base":  # C2's encoder under its floor (pinned)
+            _check_encoder(ctx, om, synth.synth_pcm_f32(30.0, 1234), 1500, pin=1.0)
         _greedy_case(ctx, om, range(1234, 1240), 16, 1500, 30.0, min_len=12)
     finally:
         ctx.close()
@@ -303,8 +336,7 @@ def _beam_case(ctx, om, seeds, K, n_tok, suppress_eot, n_ctx=64, secs=2.0, fail=
     best = None  # (t, seed, pcm)
     for seed in seeds:
         pcm = pcm_fn(secs, seed)
-        mel = om.mel(pcm, n_threads=threads())
-        _, ck, cv = om.encode(mel, n_ctx=n_ctx, n_threads=threads())
+        _, ck, cv = _oracle_encode(om, pcm, n_ctx)
         ref, score, gap, sg = om.decode_beam(ck, cv, K, n_tok, suppress_eot=suppress_eot, n_threads=threads(),
                                              step_gaps=True)
         if gap < BEAM_GAP and min_tok:
@@ -328,7 +360,7 @@ def _beam_case(ctx, om, seeds, K, n_tok, suppress_eot, n_ctx=64, secs=2.0, fail=
         got, got_score = ctx.decode_beam(K, t, suppress_eot=suppress_eot)[0]
         if hyp_logits:  # the winning hypothesis, teacher-forced through the one-row decoder
             feed = np.array(list(om.prompt()) + list(got[:-1]), np.int32)
-            kv = om.encode(om.mel(pcm, n_threads=threads()), n_ctx=n_ctx, n_threads=threads())[1:]
+            kv = _oracle_encode(om, pcm, n_ctx)[1:]
             lr, bar, floor = _logits_ref(om, kv, _exact_kv(om, pcm, n_ctx), feed)
             err = float(np.abs(ctx.decode_logits(feed, 0) - lr).max())
             print(f"[beam parity] K={K}: best hypothesis ({len(got)} tokens) teacher-forced logits max "
@@ -494,22 +526,18 @@ def test_base_batch_of_8_equals_single(wmi, model_cache):
 def test_large_v3(wmi, model_cache):
     """C5's model: 128 mels, vocab 51866 (multilingual specials shifted by one
     more id), n_state 1280 / 20 heads / 32 + 32 layers; encoder at the noise
-    floor, greedy ids (>= 9 of 12 compared), and the 5-beam ids of the first
-    seed whose oracle search has no near-tie selection — always asserted."""
+    floor (pinned: the two-key-part attention, attn_enc_kq), greedy ids
+    (>= 9 of 12 compared) and teacher-forced logits.  (Its 5-beam search meets
+    a near-tie selection within 5-12 steps on every seed, so C5's beam launch
+    is held to the oracle step by step on large-v3-xsharp instead:
+    test_beam_step_logits_large_v3_xsharp.)"""
     path = synth.model_path("large-v3", model_cache)
     om = pyoracle.OracleModel(path)
     ctx = wmi.WhisperContext.new(path, 0, max_clips=1)
     try:
         assert ctx.hparams["n_mels"] == 128 and ctx.hparams["n_vocab"] == 51866
+        _check_encoder(ctx, om, synth.synth_pcm_f32(30.0, 1234), 1500, pin=1.0)
         _greedy_case(ctx, om, range(1234, 1237), 12, 1500, 30.0, min_len=9)
-        # (a random-weight model's beam selections over a 51866-word
-        # vocabulary meet a near-tie within 12 steps on every seed tried: the
-        # longest tie-free prefix, at least 6 steps, is compared)
-        ref, score, got, got_score = _beam_case(ctx, om, range(1234, 1240), 5, 12, True, n_ctx=1500, secs=30.0,
-                                                fail=True, min_tok=6, hyp_logits=True)
-        print(f"large-v3 5-beam ids compared over {len(ref)} tokens")
-        np.testing.assert_array_equal(got, ref)
-        assert abs(got_score - score) < 2e-2
     finally:
         ctx.close()
         om.close()
@@ -539,8 +567,7 @@ def test_long_horizon_greedy_base_sharp(wmi, model_cache):
         got8 = ctx.decode_greedy(n_tok, suppress_eot=True)
         same = 0
         for i, pcm in enumerate(clips):
-            mel = om.mel(pcm, n_threads=threads())
-            _, ck, cv = om.encode(mel, n_ctx=1500, n_threads=threads())
+            _, ck, cv = _oracle_encode(om, pcm, 1500)
             r, m = om.decode_greedy(ck, cv, n_tok, suppress_eot=True, n_threads=threads())
             diff = np.nonzero(got8[i] != r)[0]
             if diff.size:
@@ -974,18 +1001,24 @@ def test_enc_attn_nw_parity_and_batch_invariance(wmi, model_cache, nw):
 # --- every step's logits of the persistent greedy launches (round-4 verdict
 # item 1): the device's own free-running decode, its logits at every position
 # (WMI_LOGITS_ALL), against the oracle teacher-forced on the device's ids -----
-def _step_logits_case(wmi, om, path, clips, n_tok, env=None, tag=""):
-    """Greedy-decode the clips in one call (8 clips: the split 8-row grid;
-    1 clip: the one-row instance) with every position's logits kept.  Per
-    clip: logits at every step within the bar of _logits_ref; the device's
-    ids are the argmax of its own logits (EOT suppressed); the oracle's
-    argmax on the device's history equals the device's id at every decisive
-    step (oracle top-2 margin >= GREEDY_GAP); the oracle's own free-running
-    ids equal the device's up to the first near-tie.  Returns the device ids
-    and the per-clip decisive step counts."""
-    n_ctx = 1500
+def _step_logits_case(wmi, om, path, clips, n_tok, env=None, tag="", floor_clips=None, pin=None, n_ctx=1500):
+    """Greedy-decode the clips in one call (8 clips: the split 8-row grid
+    where the model has one; 2-8 clips: one multi-row launch; 1 clip: the
+    one-row instance) with every position's logits kept.  Per clip: logits
+    at every step within the bar of _logits_ref; the device's ids are the
+    argmax of its own logits (EOT suppressed); the oracle's argmax on the
+    device's history equals the device's id at every decisive step (oracle
+    top-2 margin >= GREEDY_GAP) — so the oracle's own free-running decode
+    gives the device's ids up to its first near-tie (both histories are equal
+    until then).  floor_clips: measure the exact-dot floor on the first
+    floor_clips clips only and hold the others to the largest of those bars
+    (a large-v3 exact encode is ~30 s of host time).  pin: additionally
+    max |device - oracle| <= max(LOGIT_TOL, pin x floor) (the margin the
+    accepted softmax departures leave, LOGIT_TOL's comment).  Returns the
+    device ids and the per-clip decisive step counts."""
     ctx = _ctx_with_env(wmi, path, dict(env or {}, WMI_LOGITS_ALL="1"), max_clips=len(clips))
     try:
+        ctx.set_audio_ctx(n_ctx)
         ctx.pcm_to_mel_batch(clips)
         ctx.encode(1, 0)
         got = ctx.decode_greedy(n_tok, suppress_eot=True)
@@ -995,31 +1028,37 @@ def _step_logits_case(wmi, om, path, clips, n_tok, env=None, tag=""):
     finally:
         ctx.close()
     eot = om.special["eot"]
-    worst, worst_bar, n_dec = 0.0, 0.0, []
+    worst, worst_bar, n_dec, bars = 0.0, 0.0, [], []
+    n_floor = len(clips) if floor_clips is None else floor_clips
     for i, pcm in enumerate(clips):
         g = np.asarray(got[i])
-        kv = om.encode(om.mel(pcm, n_threads=threads()), n_ctx=n_ctx, n_threads=threads())[1:]
+        kv = _oracle_encode(om, pcm, n_ctx)[1:]
         feed = np.array(prompt + list(g[:-1]), np.int32)
-        lr, bar, floor = _logits_ref(om, kv, _exact_kv(om, pcm, n_ctx), feed)
+        if i < n_floor:
+            lr, bar, floor = _logits_ref(om, kv, _exact_kv(om, pcm, n_ctx), feed)
+            bars.append((bar, floor))
+        else:
+            lr = om.decode_logits(kv[0], kv[1], feed, n_threads=threads())
+            bar, floor = max(bars)
         lr = lr[np_ - 1:]
         lg = lg_all[np_ - 1:, i, :]
         err = float(np.abs(lg - lr).max())
         worst, worst_bar = max(worst, err), max(worst_bar, bar)
         assert err <= bar, (tag, i, err, bar, floor)
+        if pin is not None:
+            assert err <= max(LOGIT_TOL, pin * floor), (tag, i, err, pin, floor)
         lg[:, eot] = -np.inf
         np.testing.assert_array_equal(lg.argmax(1), g)  # the ids are the logits' argmax
         lr[:, eot] = -np.inf
         top2 = np.sort(lr, axis=1)[:, -2:]
         decisive = (top2[:, 1] - top2[:, 0]) >= GREEDY_GAP
-        np.testing.assert_array_equal(lr.argmax(1)[decisive], g[decisive])
-        ref, margins = om.decode_greedy(kv[0], kv[1], n_tok, suppress_eot=True, n_threads=threads())
-        diff = np.nonzero(ref != g)[0]
-        if diff.size:
-            assert margins[diff[0]] < GREEDY_GAP, (tag, i, int(diff[0]), float(margins[diff[0]]))
+        ora = lr.argmax(1)
+        np.testing.assert_array_equal(ora[decisive], g[decisive])
+        diff = np.nonzero(ora != g)[0]
         n_dec.append(int(decisive.sum()))
         print(f"[step logits] {tag} clip {i}: {n_tok} steps, max |device - oracle| {err:.3e} (bar {bar:.3e}, "
-              f"floor {floor:.3e}); {n_dec[-1]} decisive; free-running ids = oracle's for "
-              f"{int(diff[0]) if diff.size else n_tok}")
+              f"floor {floor:.3e}{'' if i < n_floor else ' of clip 0'}); {n_dec[-1]} decisive; ids = the oracle's "
+              f"argmax on the same history for {int(diff[0]) if diff.size else n_tok} steps")
     print(f"[step logits] {tag}: worst {worst:.3e} (largest bar {worst_bar:.3e}); "
           f"{len({tuple(x) for x in got})} distinct id sequences over {len(clips)} clips")
     return got, n_dec
@@ -1036,7 +1075,8 @@ def test_step_logits_one_row(wmi, model_cache, model, n_tok, env):
     path = synth.model_path(model, model_cache)
     om = pyoracle.OracleModel(path)
     try:
-        _step_logits_case(wmi, om, path, [synth.synth_pcm_f32(30.0, 1234)], n_tok, env, tag=f"{model} x1")
+        _step_logits_case(wmi, om, path, [synth.synth_pcm_f32(30.0, 1234)], n_tok, env, tag=f"{model} x1",
+                          pin=1.0 if model == "large-v3" else None)
     finally:
         om.close()
 
@@ -1070,7 +1110,7 @@ def _ids_agree_to_near_tie_oracle(om, pcm, a, b, gap=BATCH_GAP):
     if not diff.size:
         return
     d = int(diff[0])
-    kv = om.encode(om.mel(pcm, n_threads=threads()), n_ctx=1500, n_threads=threads())[1:]
+    kv = _oracle_encode(om, pcm, 1500)[1:]
     lg = om.decode_logits(kv[0], kv[1], np.array(list(om.prompt()) + list(a[:d]), np.int32), n_threads=threads())[-1]
     lg[om.special["eot"]] = -np.inf
     top2 = np.sort(lg)[-2:]
@@ -1079,23 +1119,16 @@ def _ids_agree_to_near_tie_oracle(om, pcm, a, b, gap=BATCH_GAP):
 
 @pytest.mark.slow
 def test_xsharp_beam5(wmi, model_cache):
-    """C5's search (5 beams, EOT suppressed) on base-xsharp's tone clips: ids
-    bit-exact with the oracle over the longest near-tie-free prefix of the
-    8 seeds (at least 16 tokens; the oracle's first selection margin below
-    BEAM_GAP comes at step 1-8 on seven seeds, at 25 on seed 1235), and the
-    winning hypothesis' teacher-forced logits within the bar."""
+    """The one-clip beam launch at base (<512,5,beam>, per-row cross tasks
+    with the cross q inside them) on base-xsharp's tone clip 1235, whose
+    oracle search keeps every selection margin >= BEAM_GAP for 25 steps (the
+    other seeds meet one within 1-8): every step's logits of every row and
+    every selection against the oracle's search up to that step."""
     path = synth.model_path("base-xsharp", model_cache)
     om = pyoracle.OracleModel(path)
-    ctx = wmi.WhisperContext.new(path, 0, max_clips=1)
     try:
-        ref, score, got, got_score = _beam_case(ctx, om, range(1234, 1242), 5, 40, True, n_ctx=1500, secs=30.0,
-                                                fail=True, min_tok=16, pcm_fn=synth.synth_pcm_tones,
-                                                hyp_logits=True)
-        print(f"[beam parity] base-xsharp 5-beam ids compared over {len(ref)} tokens")
-        np.testing.assert_array_equal(got, ref)
-        assert abs(got_score - score) < 1e-2
+        _beam_step_logits_case(wmi, om, path, synth.synth_pcm_tones(30.0, 1235), 5, 40, 24, "base-xsharp 5 beams")
     finally:
-        ctx.close()
         om.close()
 
 
@@ -1131,3 +1164,176 @@ def test_mel_dense_filterbank_layout_bitwise(micro_ctx, wmi, micro_model):
             np.testing.assert_array_equal(outs[0], outs[1])
     finally:
         dense.close()
+
+
+# --- the multi-row and beam decoder instances at n > 512 (round-5 verdict
+# item 1): every step's logits of every row against the oracle ---------------
+@pytest.mark.slow
+def test_step_logits_multi_row_small(wmi, model_cache):
+    """<768,4>: small with four tone clips in one multi-row launch (MFMA
+    GEMVs, multi-row LayerNorms, per-row cross tasks with the cross q inside
+    them, MFMA logits above n = 512): every step's logits of every row
+    within the bar against the oracle teacher-forced on that row's own ids."""
+    path = synth.model_path("small", model_cache)
+    om = pyoracle.OracleModel(path)
+    try:
+        clips = [synth.synth_pcm_tones(30.0, 1234 + i) for i in range(4)]
+        _step_logits_case(wmi, om, path, clips, 32, tag="small x4 (<768,4>)", floor_clips=1)
+    finally:
+        om.close()
+
+
+@pytest.mark.slow
+def test_large_v3_xsharp_multi_row_ids_follow_the_audio(wmi, model_cache):
+    """<1280,8>: large-v3-xsharp (synth.xsharp_lv3_hook: the audio drives the
+    ids) on eight tone clips in one 8-row launch — the cross q from the D
+    phase, per-row cross tasks, four waves splitting K in every MFMA GEMV and
+    the logits: every step's logits of every row within the bar against the
+    oracle teacher-forced on that row's ids, the ids = the oracle's argmax at
+    every decisive step, and at least 6 distinct id sequences over the 8
+    clips (a row / clip routing or cross K / V indexing bug changes a
+    compared id or logit)."""
+    path = synth.model_path("large-v3-xsharp", model_cache)
+    om = pyoracle.OracleModel(path)
+    try:
+        clips = [synth.synth_pcm_tones(30.0, 1234 + i) for i in range(8)]
+        got, dec = _step_logits_case(wmi, om, path, clips, 16, tag="large-v3-xsharp x8 (<1280,8>)", floor_clips=1)
+        n_seq = len({tuple(x) for x in got})
+        assert n_seq >= 6, n_seq
+        assert min(dec) >= 12, dec
+    finally:
+        om.close()
+
+
+def test_step_logits_beyond_one_block(wmi, micro_model, oracle_micro):
+    """More clips than one 8-row block: each block's launch keeps
+    its rows' logits at its own offset (rows 0-7: the split 8-row grid, rows
+    8-9: a two-row launch), every row against the oracle."""
+    clips = [synth.synth_pcm_tones(2.0, 500 + i) for i in range(10)]
+    _step_logits_case(wmi, oracle_micro, micro_model, clips, 12, tag="micro x10 (two blocks)", n_ctx=64)
+
+
+def _beam_step_logits_case(wmi, om, path, pcm, K, n_tok, min_steps, tag, n_ctx=1500, env=None):
+    """C5's launch itself: a K-beam search with every step's logits kept
+    (WMI_LOGITS_ALL: the beam launch's [K][V] rows each step) and the beam
+    kernels' selections (parent slot, token per step), against the oracle's
+    search with its per-step hypothesis logits (pyoracle decode_beam trace:
+    the same dec_step as its teacher-forced decoder, so each row's logits are
+    the oracle teacher-forced on that row's own history).  Every step while
+    the two searches keep the same hypotheses, and the step where they part:
+    each active row's logits within the bar; they may part only where the
+    oracle's selection margin is below 2 x the bar (the logits' own noise),
+    and not before min_steps.  The bar's floor is measured on the oracle's
+    winning hypothesis.  Returns the steps with identical selections and the
+    grid the beam launch ran on."""
+    ctx = _ctx_with_env(wmi, path, dict(env or {}, WMI_LOGITS_ALL="1"))
+    try:
+        ctx.set_audio_ctx(n_ctx)
+        ctx.pcm_to_mel_batch([pcm])
+        ctx.encode(1, 0)
+        got, got_score = ctx.decode_beam(K, n_tok, suppress_eot=True)[0]
+        np_ = len(om.prompt())
+        lg = ctx.step_logits(np_ + n_tok - 1)[np_ - 1:]
+        dpar, dtok = ctx.beam_history(n_tok)
+        grid = int(np.frombuffer(ctx.debug_read(17, 9 * 4), np.int32)[K])
+    finally:
+        ctx.close()
+    kv = _oracle_encode(om, pcm, n_ctx)[1:]
+    ref, score, gap, sg, tr = om.decode_beam(kv[0], kv[1], K, n_tok, suppress_eot=True, n_threads=threads(),
+                                             step_gaps=True, trace=True)
+    feed = np.array(list(om.prompt()) + list(ref[:-1]), np.int32)
+    _, bar, floor = _logits_ref(om, kv, _exact_kv(om, pcm, n_ctx), feed)
+    # the rows' histories (token tuples) on both sides: a device row is held
+    # to the oracle hypothesis with the same history (two kept candidates
+    # whose scores are closer than the f32 noise may take each other's slot)
+    hd, ho = [()], [()]
+    worst, rows, swaps, same = 0.0, 0, 0, n_tok
+    for t in range(n_tok):
+        where = {h: j for j, h in enumerate(ho)}
+        for r, h in enumerate(hd):
+            err = float(np.abs(lg[t, r] - tr["logits"][t, where[h]]).max())
+            assert err <= bar, (tag, t, r, err, bar)
+            worst, rows, swaps = max(worst, err), rows + 1, swaps + (where[h] != r)
+        sel = tr["sel"][t]
+        k = int((sel[:, 0] >= 0).sum())
+        nd = [hd[int(p)] + (int(x),) for p, x in zip(dpar[t, :k], dtok[t, :k])]
+        no = [ho[int(p)] + (int(x),) for p, x in sel[:k]]
+        if set(nd) != set(no):
+            # the searches part only where the oracle's selection margin is
+            # within the logits' noise (2 x the bar) — a near-tie
+            assert sg[t] < max(BEAM_GAP, 2 * bar), (tag, t, float(sg[t]), bar)
+            same = t
+            break
+        hd, ho = nd, no
+    print(f"[beam step logits] {tag}: grid {grid}; {min(same + 1, n_tok)} steps ({rows} hypothesis rows, "
+          f"{swaps} in another slot than the oracle's) max |device - oracle| {worst:.3e} (bar {bar:.3e}, floor "
+          f"{floor:.3e}); selections identical for {same} of {n_tok} steps"
+          f"{'' if same == n_tok else f' (step {same}: oracle margin {sg[same]:.2e})'}; smallest oracle margin "
+          f"before: {float(sg[:same].min()) if same else float('nan'):.2e}")
+    assert same >= min_steps, (tag, same, sg[:same + 1])
+    if same == n_tok:
+        np.testing.assert_array_equal(got, ref)
+        assert abs(got_score - score) < 2e-2, (got_score, score)
+    return same, grid
+
+
+@pytest.mark.slow
+def test_beam_step_logits_large_v3_xsharp(wmi, model_cache):
+    """C5's instance, <1280,5,beam> at 1500 frames with the beam rows sharing
+    one cross task per (head, key chunk) (PersistArgs::xshare: 20 heads x 12
+    chunks = 240 tasks within the grid), on an audio-dependent model
+    (large-v3-xsharp, tone clip 1234: the oracle's 40 selection margins all
+    >= BEAM_GAP, scripts/xsharp_probe.py): every step's logits of all five
+    rows and every selection against the oracle over 40 steps, and the final
+    hypothesis and score."""
+    path = synth.model_path("large-v3-xsharp", model_cache)
+    om = pyoracle.OracleModel(path)
+    try:
+        steps, grid = _beam_step_logits_case(wmi, om, path, synth.synth_pcm_tones(30.0, 1234), 5, 40, 32,
+                                             "large-v3-xsharp 5 beams")
+        assert grid >= 240, grid  # (the beam-shared cross tasks: H * ceil(T / 128) <= G)
+    finally:
+        om.close()
+
+
+@pytest.mark.slow
+def test_beam_small_grid_per_row_cross_tasks(wmi, model_cache, tmp_path):
+    """The small-grid fallback of the beam launch (when
+    H * ceil(T / 128) exceeds the grid the rows take per-row cross tasks
+    instead of a rejected configuration): the library built for a
+    192-workgroup grid (variants/g192, WMI_GDESIGN=192; 20 x 12 = 240 > 192)
+    runs large-v3's 5-beam search in a child process and gives bitwise the
+    tokens, score, selections and every step's logits of the default
+    256-workgroup build with shared cross tasks — neither the grid nor the
+    task layout enters a row's arithmetic (MFMA GEMVs in a fixed wave order,
+    test_beam_shared_cross_equals_per_row)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib192 = os.path.join(root, "whisper.rs_amd", "variants", "g192", "libwhisper_mi355x.so")
+    assert os.path.exists(lib192), "build the variants (make -C whisper.rs_amd/csrc)"
+    path = synth.model_path("large-v3", model_cache)
+    out = str(tmp_path / "g192.npz")
+    env = dict(os.environ, WMI_LIB=lib192)
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "beam_worker.py"), path, "1236", "5", "12", out],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    small = np.load(out)
+    ctx = _ctx_with_env(wmi, path, {"WMI_LOGITS_ALL": "1"})
+    try:
+        ctx.pcm_to_mel_batch([synth.synth_pcm_f32(30.0, 1236)])
+        ctx.encode(1, 0)
+        toks, score = ctx.decode_beam(5, 12, suppress_eot=True)[0]
+        par, tok = ctx.beam_history(12)
+        lg = ctx.step_logits(4 + 12 - 1)[3:, :5]
+        grids = np.frombuffer(ctx.debug_read(17, 9 * 4), np.int32)
+    finally:
+        ctx.close()
+    print(f"[small grid] beam grid: g192 build {int(small['grids'][5])}, default {int(grids[5])}")
+    assert int(small["grids"][5]) == 192 and int(grids[5]) >= 240
+    np.testing.assert_array_equal(small["tokens"], toks)
+    assert float(small["score"]) == score
+    np.testing.assert_array_equal(small["par"], par)
+    np.testing.assert_array_equal(small["tok"], tok)
+    np.testing.assert_array_equal(small["logits"], lg)

@@ -233,3 +233,25 @@ def test_xsharp_oracle_ids_follow_the_audio(model_cache):
     print(f"[xsharp] distinct 64-token id sequences over 8 tone clips: {counts}")
     assert counts["base-xsharp"] >= 6, counts
     assert counts["base"] <= 2, counts
+
+
+def test_beam_trace_is_teacher_forced(oracle_micro):
+    """decode_beam's trace (the GPU beam tests' reference): each active
+    hypothesis' logits at step t equal the teacher-forced decoder's last row
+    on that hypothesis' history, bitwise (one dec_step on an identical KV
+    cache), and the recorded selections rebuild the returned hypothesis."""
+    pcm = synth.synth_pcm_f32(2.0, 104)
+    _, ck, cv = oracle_micro.encode(oracle_micro.mel(pcm, n_threads=threads()), n_ctx=64, n_threads=threads())
+    K, n_tok = 3, 6
+    toks, score, gap, tr = oracle_micro.decode_beam(ck, cv, K, n_tok, suppress_eot=True, n_threads=threads(),
+                                                    trace=True)
+    prompt = oracle_micro.prompt()
+    hist = [[]]  # active hypotheses' histories before step t
+    for t in range(n_tok):
+        for b, h in enumerate(hist):
+            want = oracle_micro.decode_logits(ck, cv, np.array(prompt + h, np.int32), n_threads=threads())[-1]
+            np.testing.assert_array_equal(tr["logits"][t, b], want)
+        k = int((tr["sel"][t, :, 0] >= 0).sum())
+        hist = [hist[int(p)] + [int(x)] for p, x in tr["sel"][t, :k]]
+    # suppress_eot: every hypothesis stays active; the result is one of them
+    assert list(toks) in hist

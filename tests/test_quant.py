@@ -97,3 +97,16 @@ def test_dequant_rounding_random_blocks(qtype):
     ref = np_dequant(qtype, raw, nb * 32)
     got = pyoracle.dequant(TYPES[qtype][0], raw, nb * 32)
     np.testing.assert_array_equal(got, ref.view(np.uint16))
+
+
+@pytest.mark.parametrize("hook", ["sharp_hook", "xsharp_hook", "xsharp_lv3_hook", "lnmean_hook"])
+def test_derived_variant_equals_generated(tmp_path, hook):
+    """synth.derive_variant (a copy of the plain file with the hooked tensors
+    rewritten) gives byte for byte the file write_ggml writes with the hook."""
+    import synth
+    plain, gen, der = (str(tmp_path / n) for n in ("plain.bin", "gen.bin", "der.bin"))
+    synth.write_ggml(plain, "micro")
+    synth.write_ggml(gen, "micro", tensor_hook=getattr(synth, hook))
+    synth.derive_variant(plain, der, getattr(synth, hook))
+    with open(gen, "rb") as a, open(der, "rb") as b:
+        assert a.read() == b.read()

@@ -273,11 +273,6 @@ struct wmi_context {
     }
     bool use_graph = true;
     bool use_coop = true;
-    // WMI_TRACE=1: per-launch device timeline of the last decoder step
-    bool trace_on = false;
-    unsigned long long *d_trace = nullptr;
-    std::vector<std::string> trace_names;
-    std::vector<std::string> phase_names = std::vector<std::string>(32);  // phase slots 32.. (layer 0 GEMVs, logits)
     // persistent decoder (wmi_persist.hip): greedy steps in one launch
     Tune tune;                        // WMI_* knobs of this context (wmi_internal.h)
     bool checksums = false;           // WMI_CHECKSUMS=1: the reference's stage sums (debug prints)
@@ -286,13 +281,17 @@ struct wmi_context {
     int persist_q5 = -1;              // WMI_PERSIST_Q5: 0 = decoder GEMVs on the f16 copies (default: q5_1 blocks)
     bool persist_logits = false;      // WMI_PERSIST_LOGITS=1: also store every step's logits (dlogits)
     // WMI_LOGITS_ALL=1 (parity tests): the persistent greedy launches keep
-    // every position's logits, [n_text_ctx][DEC_ROWS][V] f32 (debug read 13)
+    // every position's logits, [n_text_ctx][lg_rows][V] f32 (debug read 13):
+    // clip b's row b (every 8-row block at its own offset); a beam search
+    // keeps each step's [K][V] rows of its last clip, beam slot s in row s
     float *d_lgall = nullptr;
+    int lg_rows = 0;                  // max(DEC_ROWS, max_clips)
     int dec_layers = 0;               // WMI_DEC_LAYERS (debug): run only the first decoder layers
     int enc_layers = 0;               // WMI_ENC_LAYERS (debug): run only the first encoder layers
     int fault_inject = 0;             // WMI_FAULT_INJECT=1 (test): the first persistent launch runs with one
                                       // workgroup missing (PersistArgs::stall_wg): the device abort path
-    // WMI_VREG=0: stream the one-row logits' non-resident vocabulary tiles every step
+    // the one-row logits keep their non-resident vocabulary tiles in registers
+    // (n = 768, PersistArgs::vreg; round 4: small decode 42.3 -> 41.0 ms)
     bool persist_vreg = true;
     bool use_xshare = true;           // WMI_XSHARE=0: beam rows read the cross K / V per row
     // greedy blocks of at least split_rows clips decode as two concurrent
@@ -1286,61 +1285,6 @@ int run_encode(wmi_context *ctx, int mel_offset) {
     return WMI_OK;
 }
 
-constexpr int TRACE_SLOTS = 512;
-
-// phase slot (first / last workgroup timeline inside one launch) for WMI_TRACE
-unsigned long long *pslot(wmi_context *ctx, int i, const char *name) {
-    if (!ctx->trace_on || i < 0 || i >= 32) return nullptr;
-    ctx->phase_names[i] = name;
-    return ctx->d_trace + 2 * 512 + 16 * (32 + i);
-}
-
-unsigned long long *tslot(wmi_context *ctx, const char *name, int l) {
-    if (!ctx->trace_on || ctx->trace_names.size() >= (size_t)TRACE_SLOTS) return nullptr;
-    char buf[64];
-    snprintf(buf, sizeof buf, "%s[%d]", name, l);
-    ctx->trace_names.push_back(buf);
-    return ctx->d_trace + 2 * (ctx->trace_names.size() - 1);
-}
-
-// prints the device timeline recorded for the last traced step to stderr
-int trace_dump(wmi_context *ctx) {
-    const size_t ns = ctx->trace_names.size();
-    std::vector<unsigned long long> t(2 * TRACE_SLOTS + 64 * 16);
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    HIPCHK(ctx, hipMemcpy(t.data(), ctx->d_trace, t.size() * 8, hipMemcpyDeviceToHost));
-    for (int sl = 0; sl < 64; ++sl) {
-        const unsigned long long *ph = t.data() + 2 * TRACE_SLOTS + 16 * sl;
-        std::string nm;
-        if (sl < ctx->hp.n_text_layer && ctx->use_coop) nm = "cross_attn[" + std::to_string(sl) + "]";
-        else if (sl >= 32 && !ctx->phase_names[sl - 32].empty() && ph[0]) nm = ctx->phase_names[sl - 32];
-        if (nm.empty()) continue;
-        for (int wg = 0; wg < 2; ++wg) {
-            fprintf(stderr, "[wmi trace] %-14s %s WG phases:", nm.c_str(), wg ? "last " : "first");
-            for (int i = 1; i < 8; ++i) {
-                const unsigned long long v = ph[8 * wg + i];
-                if (v) fprintf(stderr, " %7.2f", ((double)v - (double)ph[0]) * 0.01);
-                else fprintf(stderr, "       -");
-            }
-            fprintf(stderr, "\n");
-        }
-    }
-    if (!ns) return WMI_OK;
-    const unsigned long long t0 = t[0];
-    unsigned long long prev_end = t0;
-    double busy = 0.0;
-    fprintf(stderr, "[wmi trace] %-22s %9s %9s %9s  (us, 100 MHz clock)\n", "launch", "start", "dur", "gap");
-    for (size_t i = 0; i < ns; ++i) {
-        const unsigned long long st = t[2 * i], en = ~t[2 * i + 1];
-        const double d = (en - st) * 0.01, g = ((double)st - (double)prev_end) * 0.01;
-        busy += d;
-        fprintf(stderr, "[wmi trace] %-22s %9.2f %9.2f %9.2f\n", ctx->trace_names[i].c_str(), (st - t0) * 0.01, d, g);
-        prev_end = en;
-    }
-    fprintf(stderr, "[wmi trace] step span %.2f us, sum of launch durations %.2f us, %zu launches\n",
-            (prev_end - t0) * 0.01, busy, ns);
-    return WMI_OK;
-}
 
 // one decoder step for clips [b0, b0 + B) of the encoded batch
 // beam-step kernel arguments of the current beam search
@@ -1359,7 +1303,6 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     const int n = hp.n_text_state, H = hp.n_text_head, T = ctx->enc_T, Bt = ctx->enc_clips;
     hipStream_t s = ctx->stream;
     const float qs = powf((float)n / (float)H, -0.25f);
-    ctx->trace_names.clear();
     const bool beam = ctx->beam_k > 0;
     // per layer: [LN+QKV (+embed at l=0)] [self-attn] [Wo+res] [LN+Wcq+cross scores]
     //            [cross softmax+PV] [Wco+res] [LN+W0+GELU] [W1+res]; then LN+logits+argmax
@@ -1402,8 +1345,6 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
                 g.beam_tok = ctx->dts_tok;
             }
         }
-        g.trace = tslot(ctx, "qkv", l);
-        if (l == 0) g.phase = pslot(ctx, 0, "qkv[0]");
         HIPCHK(ctx, launch_dec_gemv(s, DEC_QKV, g));
         DecAttnArgs at{}; at.tune = &ctx->tune;
         at.q = ctx->dq16; at.K = kc; at.V = vc; at.clip_stride = (int64_t)hp.n_text_ctx * n; at.M_fixed = 0;
@@ -1421,8 +1362,6 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
             at.Wo = d.wo;
             at.wo_parts = ctx->dwoparts;
         }
-        at.trace = tslot(ctx, "self_attn", l);
-        if (l == 0) at.phase = pslot(ctx, 1, "self_attn[0]");
         HIPCHK(ctx, launch_dec_attn(s, at));
         if (!fuse_wo) {
             g = DecGemvArgs{};
@@ -1430,7 +1369,6 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
             g.Wq5 = q5 ? d.wo5 : nullptr;
             g.W32 = W32(d.wo);
             g.out32 = X[cur];
-            g.trace = tslot(ctx, "wo", l);
             HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
         }
         const int c_cross = (T + 127) / 128;
@@ -1438,7 +1376,6 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
             g = DecGemvArgs{}; g.tune = &ctx->tune;
             g.x = X[cur]; g.ln_w = d.lnc_w; g.ln_b = d.lnc_b; g.W32 = W32(d.wcq); g.bias = d.bcq;
             g.N = n; g.K = n; g.B = B; g.qscale = qs; g.out16 = ctx->dq16; g.ldo = n;
-            g.trace = tslot(ctx, "cross_q", l);
             HIPCHK(ctx, launch_dec_gemv(s, DEC_Q, g));
         }
         at = DecAttnArgs{};
@@ -1456,31 +1393,23 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
             at.res_parts = ctx->dwoparts; at.res_bias = d.bo; at.x_out = X[cur ^ 1];
             cur ^= 1;
         }
-        at.trace = tslot(ctx, "cross_attn", l);
-        at.phase = ctx->trace_on ? ctx->d_trace + 2 * TRACE_SLOTS + 16 * l : nullptr;
         HIPCHK(ctx, launch_dec_attn(s, at));
         g = DecGemvArgs{};
         g.parts = ctx->dopart; g.n_parts = c_cross; g.W = d.wco; g.bias = d.bco; g.N = n; g.K = n; g.B = B;
         g.Wq5 = q5 ? d.wco5 : nullptr;
         g.W32 = W32(d.wco);
         g.out32 = X[cur];
-        g.trace = tslot(ctx, "wco", l);
-        if (l == 0) g.phase = pslot(ctx, 2, "wco[0]");
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
         g = DecGemvArgs{};
         g.x = X[cur]; g.ln_w = d.ln2_w; g.ln_b = d.ln2_b; g.W = d.w0; g.bias = d.b0; g.N = 4 * n; g.K = n; g.B = B;
         g.Wq5 = q5 ? d.w05 : nullptr;
         g.W32 = W32(d.w0);
         g.out16 = ctx->dhid16; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
-        g.trace = tslot(ctx, "mlp0", l);
-        if (l == 0) g.phase = pslot(ctx, 3, "mlp0[0]");
         HIPCHK(ctx, launch_dec_gemv(s, DEC_GELU, g));
         g = DecGemvArgs{};
         g.xin16 = ctx->dhid16; g.W = d.w1; g.bias = d.b1; g.N = n; g.K = 4 * n; g.B = B; g.out32 = X[cur];
         g.Wq5 = q5 ? d.w15 : nullptr;
         g.W32 = W32(d.w1);
-        g.trace = tslot(ctx, "mlp1", l);
-        if (l == 0) g.phase = pslot(ctx, 4, "mlp1[0]");
         HIPCHK(ctx, launch_dec_gemv(s, DEC_RESID, g));
     }
     DecGemvArgs g{}; g.tune = &ctx->tune;
@@ -1489,8 +1418,6 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     g.W32 = W32(ctx->te);
     g.out32 = ctx->dlogits; g.amax = ctx->damax; g.suppress_id = suppress_eot ? ctx->sp.eot : -1;
     g.st_advance = ctx->dstate;
-    g.trace = tslot(ctx, "logits", 0);
-    g.phase = pslot(ctx, 5, "logits");
     if (beam || ctx->ts_mode) g.amax = nullptr;
     HIPCHK(ctx, launch_dec_gemv(s, DEC_LOGITS, g));
     if (ctx->ts_mode) {
@@ -1502,7 +1429,6 @@ int enqueue_dec_step(wmi_context *ctx, int b0, int B, int feed_len, int feed_str
     }
     if (beam) {
         BeamArgs ba = beam_args(ctx, feed_len, suppress_eot);
-        ba.trace = tslot(ctx, "beam", 0);
         HIPCHK(ctx, launch_beam_step(s, ba));
     }
     return WMI_OK;
@@ -1562,7 +1488,6 @@ int run_dec_steps(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride
         ctx->self_mk = mk;
         if (!ctx->use_graph) {
             for (int i = 0; i < n; ++i) {
-                if (ctx->trace_on) HIPCHK(ctx, hipMemsetAsync(ctx->d_trace, 0xff, TRACE_SLOTS * 16, ctx->stream));
                 int rc = enqueue_dec_step(ctx, b0, B, feed_len, feed_stride, suppress_eot, out_stride);
                 if (rc) return rc;
             }
@@ -1594,7 +1519,6 @@ int run_dec_steps(wmi_context *ctx, int b0, int B, int feed_len, int feed_stride
                 it = ctx->graphs.emplace(key, g).first;
             }
             for (; n >= reps; n -= reps, done += reps) {
-                if (ctx->trace_on) HIPCHK(ctx, hipMemsetAsync(ctx->d_trace, 0xff, TRACE_SLOTS * 16, ctx->stream));
                 HIPCHK(ctx, hipGraphLaunch(it->second.exec, ctx->stream));
             }
         }
@@ -1702,8 +1626,12 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     // H * ceil(T / 128) exceeds G — a smaller grid, a part with fewer CUs —
     // the launch takes the per-row tasks instead of a rejected configuration)
     const int rows_t = ctx->beam_k > 0 && n > 768 && ctx->use_xshare && (int64_t)H * ((T + 127) / 128) <= G ? 1 : B;
+    // (the one-row instance's tasks hold two 128-key sub-chunks: cl <= 256;
+    // more tasks than workgroups then take several rounds of the grid)
+    const int cl_max = B == 1 && ctx->beam_k == 0 ? 256 : 512;
     int cl = 128;
-    while (cl < 512 && ((int64_t)rows_t * H * ((T + cl - 1) / cl) > G || (int64_t)B * H * ((T + cl - 1) / cl) > PX_TASKS))
+    while (cl < cl_max &&
+           ((int64_t)rows_t * H * ((T + cl - 1) / cl) > G || (int64_t)B * H * ((T + cl - 1) / cl) > PX_TASKS))
         cl += 128;
     a.cl = cl;
     a.nch = (T + cl - 1) / cl;
@@ -1720,8 +1648,9 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
         a.stall_wg = G - 1;
         ctx->fault_inject = 2;
     }
-    a.logits_out = ctx->d_lgall ? ctx->d_lgall : ctx->persist_logits ? ctx->dlogits : nullptr;
-    a.lg_stride = ctx->d_lgall ? (int64_t)DEC_ROWS * hp.n_vocab : 0;
+    // (all-step capture: rows b0.. of each position's [lg_rows][V] slab)
+    a.logits_out = ctx->d_lgall ? ctx->d_lgall + (size_t)b0 * hp.n_vocab : ctx->persist_logits ? ctx->dlogits : nullptr;
+    a.lg_stride = ctx->d_lgall ? (int64_t)ctx->lg_rows * hp.n_vocab : 0;
     // q5_1 blocks in the persistent GEMVs (the ggml dequant x activation
     // product of a q5_1 file), dequantised inside each phase's poll so the
     // VALU overlaps the seam: small q5_1, one clip 43.1 ms decode vs 42.0 ms
@@ -1744,7 +1673,7 @@ void split_second(wmi_context *ctx, PersistArgs &p1, int B1, int Gh) {
     p1.kcache = ctx->kcache + B1 * row;
     p1.vcache = ctx->vcache + B1 * row;
     p1.cur_tok = ctx->d_curtok + B1;
-    if (p1.logits_out) p1.logits_out += (size_t)B1 * ctx->hp.n_vocab;  // (within each position's slab)
+    if (ctx->persist_logits && !ctx->d_lgall) p1.logits_out += (size_t)B1 * ctx->hp.n_vocab;  // (dlogits rows B1..)
     p1.nres = (ctx->hp.n_vocab + Gh - 1) / Gh;
 }
 
@@ -1854,10 +1783,6 @@ int run_greedy(wmi_context *ctx, int n_gen, int suppress_eot, bool early_stop, s
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         if (persist_fallback(ctx, err)) return run_greedy(ctx, n_gen, suppress_eot, early_stop, host_tokens, host_counts);
         if (err) return dec_err(ctx, err);
-    }
-    if (ctx->trace_on) {
-        const int rc2 = trace_dump(ctx);
-        if (rc2) return rc2;
     }
     if (host_tokens) {
         HIPCHK(ctx, hipMemcpyAsync(host_tokens->data(), ctx->dtokens, host_tokens->size() * 4, hipMemcpyDeviceToHost,
@@ -2090,6 +2015,10 @@ int run_beam(wmi_context *ctx, int K, int n_gen, int suppress_eot, bool early_st
                     if (ctx->d_ptrace && clip == 0 && s_all < hp.n_text_ctx)
                         pa.ptrace = ctx->d_ptrace + (size_t)s_all * (hp.n_text_layer + 1) * 32 * 2;
                     HIPCHK(ctx, launch_dec_persist(ctx->stream, pa, G));
+                    if (ctx->d_lgall && s_all < hp.n_text_ctx)  // WMI_LOGITS_ALL: this step's [K][V]
+                        HIPCHK(ctx, hipMemcpyAsync(ctx->d_lgall + (size_t)s_all * ctx->lg_rows * hp.n_vocab,
+                                                   ctx->dlogits, (size_t)K * hp.n_vocab * 4,
+                                                   hipMemcpyDeviceToDevice, ctx->stream));
                     HIPCHK(ctx, launch_beam_step(ctx->stream, beam_args(ctx, np, suppress_eot)));
                 }
             } else {
@@ -2249,7 +2178,6 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     if (const char *e = getenv("WMI_PERSIST_Q5")) ctx->persist_q5 = atoi(e) ? 1 : 0;
     if (const char *c = getenv("WMI_CHECKSUMS")) ctx->checksums = atoi(c) != 0;
     if (const char *c = getenv("WMI_FAULT_INJECT")) ctx->fault_inject = atoi(c) ? 1 : 0;
-    if (const char *c = getenv("WMI_VREG")) ctx->persist_vreg = atoi(c) != 0;
     if (const char *c = getenv("WMI_XSHARE")) ctx->use_xshare = atoi(c) != 0;
     if (const char *c = getenv("WMI_SPLIT_ROWS")) ctx->split_rows = atoi(c);
     ctx->dec_layers = ctx->hp.n_text_layer;
@@ -2257,7 +2185,8 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     ctx->enc_layers = ctx->hp.n_audio_layer;
     if (const char *c = getenv("WMI_ENC_LAYERS")) ctx->enc_layers = std::max(0, std::min(atoi(c), ctx->hp.n_audio_layer));
     if (const char *c = getenv("WMI_LOGITS_ALL"); c && atoi(c)) {
-        const size_t nb = (size_t)ctx->hp.n_text_ctx * DEC_ROWS * ctx->hp.n_vocab * 4;
+        ctx->lg_rows = std::max(DEC_ROWS, max_clips);
+        const size_t nb = (size_t)ctx->hp.n_text_ctx * ctx->lg_rows * ctx->hp.n_vocab * 4;
         HIPCHK(ctx.get(), hipMalloc(&ctx->d_lgall, nb));
         HIPCHK(ctx.get(), hipMemset(ctx->d_lgall, 0, nb));
     }
@@ -2274,19 +2203,12 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
         }
     };
     knob("WMI_LOGITS_CAP", tn.logits_cap, 1);
-    knob("WMI_LOGITS_G", tn.logits_g, 0);
     knob("WMI_GRAPH_STEPS", tn.graph_steps, 1);
-    if (const char *c = getenv("WMI_GEMV_NW")) tn.gemv_nw = atoi(c) == 1 ? 1 : atoi(c) == 0 ? 0 : 4;
     knob("WMI_XATTN_ROWS", tn.xattn_rows, 0);
     knob("WMI_ENC_ATTN_NW", tn.enc_attn_nw, 0);
     knob("WMI_GEMM_G", tn.gemm_g, 0);
     knob("WMI_GEMM_EPI", tn.epi_staged, 0);
     knob("WMI_MEL_G", tn.mel_g, 0);
-    if (getenv("WMI_TRACE")) {
-        ctx->trace_on = true;
-        HIPCHK(ctx.get(), hipMalloc(&ctx->d_trace, TRACE_SLOTS * 16 + 64 * 16 * 8));
-        HIPCHK(ctx.get(), hipMemset(ctx->d_trace, 0, TRACE_SLOTS * 16 + 64 * 16 * 8));
-    }
     *out = ctx.release();
     return WMI_OK;
 }
@@ -2305,7 +2227,6 @@ void wmi_free(wmi_context *ctx) {
     if (ctx->d_dsend) (void)hipFree(ctx->d_dsend);
     if (ctx->d_dctl) (void)hipFree(ctx->d_dctl);
     if (ctx->d_ws) (void)hipFree(ctx->d_ws);
-    if (ctx->d_trace) (void)hipFree(ctx->d_trace);
     if (ctx->d_model) (void)hipFree(ctx->d_model);
     if (ctx->d_players) (void)hipFree(ctx->d_players);
     if (ctx->d_expfb) (void)hipFree(ctx->d_expfb);
@@ -2817,7 +2738,7 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
         out->alg_flops = 4.0 * T * (double)T * n * B;
         out->alg_bytes = 4.0 * (double)M * n * 2;
         const int nw = attn_enc_nw(T, hp.n_audio_head, B, ctx->tune.enc_attn_nw);  // as launch_attn_enc picks it
-        snprintf(out->name, sizeof out->name, "k_attn_enc4<%d>", nw);
+        snprintf(out->name, sizeof out->name, "k_attn_enc4<%d,%d>", nw, attn_enc_kq(T, hp.n_audio_head));
     } else if (which == 14) {
         int32_t prompt[8];
         const int np = prompt_tokens(ctx, prompt), steps = np + ctx->staged_n_decode - 1;
@@ -2857,9 +2778,24 @@ int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes) {
             memcpy(out, v, std::min(sizeof v, bytes));
             return WMI_OK;
         }
-        case 13:  // WMI_LOGITS_ALL: every position's logits [n_text_ctx][8][V]
+        case 13:  // WMI_LOGITS_ALL: every position's logits [n_text_ctx][lg_rows][V]
             if (!ctx->d_lgall) return WMI_E_INVALID_ARG;
-            src = ctx->d_lgall; have = (size_t)ctx->hp.n_text_ctx * R * ctx->hp.n_vocab * 4; break;
+            src = ctx->d_lgall; have = (size_t)ctx->hp.n_text_ctx * ctx->lg_rows * ctx->hp.n_vocab * 4; break;
+        case 14:  // the last beam search's history of its last clip: parent slots [n_text_ctx][BEAM_MAX]
+            if (!ctx->dhist_par) return WMI_E_INVALID_ARG;
+            src = ctx->dhist_par; have = (size_t)ctx->hp.n_text_ctx * BEAM_MAX * 4; break;
+        case 15:  // ... and the slots' tokens [n_text_ctx][BEAM_MAX]
+            if (!ctx->dhist_tok) return WMI_E_INVALID_ARG;
+            src = ctx->dhist_tok; have = (size_t)ctx->hp.n_text_ctx * BEAM_MAX * 4; break;
+        case 17: {  // host: the persistent grid per row count, int32 [9] (-1: not sized yet, 0: chain)
+            memcpy(out, ctx->persist_G, std::min(sizeof ctx->persist_G, bytes));
+            return WMI_OK;
+        }
+        case 16: {  // host: rows of each position's slab of debug read 13
+            const int32_t v = ctx->lg_rows;
+            memcpy(out, &v, std::min(sizeof v, bytes));
+            return WMI_OK;
+        }
         case 12: src = ctx->h; have = (size_t)ctx->enc_clips * ctx->enc_T * ctx->hp.n_audio_state * 4; break;  // encoder residual stream
         case 11: {  // host: decodes re-run on the kernel chain after a persistent exchange timeout
             const int32_t v = ctx->n_fallbacks;

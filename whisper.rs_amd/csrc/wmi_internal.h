@@ -72,8 +72,8 @@ enum GemmEpi {
 // context's copy; a null pointer means the defaults below.
 struct Tune {
     int logits_cap = 512;   // WMI_LOGITS_CAP: chain logits grid cap
-    int logits_g = 2;       // WMI_LOGITS_G: logits rows per lane group
-    int gemv_nw = 4;        // WMI_GEMV_NW: waves per decoder GEMV workgroup (1, 4; 0 auto)
+    int logits_g = 2;       // (fixed) chain logits rows per lane group
+    int gemv_nw = 4;        // (fixed) waves per chain decoder GEMV workgroup
     int xattn_rows = 1;     // WMI_XATTN_ROWS: beam rows share cross-attention phase A (1 auto, 2 always, 0 never)
     int graph_steps = 8;    // WMI_GRAPH_STEPS: chain decoder steps per captured graph
     int enc_attn_nw = 0;    // WMI_ENC_ATTN_NW: 32-query blocks (four key-part waves each) per k_attn_enc4 workgroup (0 auto, 1, 2, 4)
@@ -135,6 +135,7 @@ struct AttnArgs {
 hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a);
 // k_attn_enc4 query blocks per workgroup, as launch_attn_enc picks them
 int attn_enc_nw(int T, int H, int n_clips, int nw_knob);
+int attn_enc_kq(int T, int H);
 
 // ---- decoder step -----------------------------------------
 struct DecState {          // device-resident, advanced by the kernels
@@ -177,8 +178,6 @@ struct DecGemvArgs {
     int out_stride;
     float *x_out;               // residual stream written by block 0
     const int32_t *beam_tok;    // beam search: token of row b past the prompt (BeamState::tok), else null
-    unsigned long long *trace;  // WMI_TRACE: {min start, ~max end} s_memrealtime of this launch
-    unsigned long long *phase;  // WMI_TRACE: [2][8] phase times of the first and last workgroup
     // f32 models: W32 = f32 weights [N][K] (W / Wq5 unused), te32 = f32 token
     // embedding for IN = 3; activations stay f32 into the dot (wmi_f32.hip)
     const float *W32, *te32;
@@ -228,8 +227,6 @@ struct DecAttnArgs {
     // then LN(x_out); block (0, 0, b) stores x_out[b] (x_out != x: ping-pong)
     const float *res_parts, *res_bias;
     float *x_out;
-    unsigned long long *trace;  // WMI_TRACE slot (see DecGemvArgs)
-    unsigned long long *phase;  // WMI_TRACE: [2][8] phase times of the first and last chunk of (head 0, clip 0)
 };
 // exchange words of one (layer, clip, head) for the cooperative kernel
 struct XSync {
@@ -262,7 +259,6 @@ struct BeamArgs {
     BeamState *bs;
     int32_t *kv_src;         // [K][tctx]
     int32_t *hist_parent, *hist_tok;  // [max_tokens][BEAM_MAX]
-    unsigned long long *trace;
 };
 hipError_t launch_beam_step(hipStream_t s, const BeamArgs &a);
 
@@ -321,7 +317,7 @@ struct PersistLayer {          // decoder layer weights (device pointers)
 
 // exchange block layout in granules (host and device agree)
 struct XLayout {
-    int x1, x2, x3, q, k, v, o, xq, oc, h, s, m, p, a, ctl, total;
+    int x1, x2, x3, q, k, v, o, xq, oc, h, s, p, a, ctl, total;
 };
 constexpr int PX_TASKS = 2048;   // cross-attention (row, head, chunk) tasks
 constexpr int PX_GMAX = 256;     // workgroups
@@ -339,9 +335,9 @@ __host__ __device__ inline XLayout persist_layout(int n, int H, int T) {
     L.xq = o; o += R * n / 2;
     L.oc = o; o += R * n / 2;
     L.h = o; o += R * 2 * n;
-    // one row: the cross scores [R][H][T]; several rows: per task its chunk's exp sum (double as lo, hi)
-    L.s = o; o += R * H * T > 2 * PX_TASKS ? R * H * T : 2 * PX_TASKS;
-    L.m = o; o += PX_TASKS;
+    // per (row, head, 128-key sub-chunk) of the cross attention: its max m and
+    // its exact exp sum S (a double as lo, hi): [R][H][ceil(T / 128)][3]
+    L.s = o; o += 3 * R * H * ((T + 127) / 128);
     L.p = o; o += R * H * ((T + 127) / 128) * 64;  // 128-key P.V partials
     L.a = o; o += R * PX_GMAX * 2;
     L.ctl = o; o += 16;             // ctl[0] low word: abort flag

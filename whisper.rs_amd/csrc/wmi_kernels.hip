@@ -888,23 +888,22 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a0) {
 // (128-key tiles, double-buffered, one global->LDS copy per tile for the
 // whole workgroup instead of one per 32 queries); KQ = 4 waves share a query
 // block, wave kb taking keys kb * 32 .. kb * 32 + 31 of every tile, and the
-// softmax runs in two sweeps over the keys instead of holding the scores in
+// softmax runs in three sweeps over the keys instead of holding the scores in
 // registers:
 //   sweep 0: S = scale * K Q^T (MFMA) -> row max (exact: the parts' maxima
 //            meet in LDS)
-//   sweep 1: S again -> p = exp_tab[f16(S - max)] (an f16 value): double sum
-//            of p, O += p V (MFMA); O / sum at the end (ggml rounds
-//            P16 = f16(p / sum) first: the weights differ by that rounding)
-// The parts' exact double sums and partial O meet in LDS, O added in part
-// order.  Recomputing Q K^T costs MFMA time the kernel has to spare.  (KQ = 2
-// — half the waves, 64-key tiles — was the round-4 kernel: one clip 0.69 vs
-// 0.64 ms; the three-sweep exact-ggml form, f16(p / sum) before P V, is in
-// the git history: 0.78 ms.)
-constexpr int AT4_KQ = 4;
-static_assert(AT4_KQ == 2 || AT4_KQ == 4, "key parts");
-constexpr int AT4_KT = 32 * AT4_KQ;  // keys per tile
-constexpr int AT4_LD = 72;           // halfs per K row in LDS (64 + 8 pad: 144-byte rows)
-constexpr int AT4_VLD = AT4_KT + 8;  // halfs per V^T row in LDS
+//   sweep 1: S again -> p = exp_tab[f16(S - max)]: double sum of p (exact,
+//            so the parts' sums meet in LDS in any order)
+//   sweep 2: S again -> P16 = f16(p * (1 / sum)) -> O += P16 V (MFMA)
+// — ggml's rounding points (flash_attn_f16: P16 rounded before P V).  The
+// parts' partial O meet in LDS, added in part order.  Recomputing Q K^T costs
+// MFMA time the kernel has to spare.  (Round 5's two-sweep form — p V
+// unnormalised, O / sum at the end — saved one sweep, 0.69 vs 0.78 ms a clip
+// at KQ = 2, but moved the encoder output past its noise floor against the
+// oracle: base 1.41e-3 vs floor 1.34e-3; it is in the git history.)
+// KQ (2 or 4) key parts per query block: tiles of KT = 32 KQ keys, V^T tile
+// rows of KT + 8 halfs in LDS (attn_enc_kq picks KQ per model)
+constexpr int AT4_LD = 72;  // halfs per K row in LDS (64 + 8 pad: 144-byte rows)
 
 // 16-byte staging chunks as a native vector (SROA keeps arrays of these in
 // registers; the struct uint4 arrays of the staging loop went to scratch)
@@ -913,16 +912,17 @@ typedef uint32_t a4vec __attribute__((ext_vector_type(4)));
 // this wave's 32-key part kb of a tile in LDS (buffer Kb / Vb) for its 32
 // queries.  TAIL: the tile holds keys >= T (masked); full tiles skip every key test.
 // Sweep 0 keeps the max of the raw scores (scale > 0 and rounding are
-// monotone, so fl(max_raw * scale) is the max of the scaled scores); sweep
-// 1 clamps the table index to n_exp, where the table holds a 0 (no
+// monotone, so fl(max_raw * scale) is the max of the scaled scores); sweeps
+// 1 and 2 clamp the table index to n_exp, where the table holds a 0 (no
 // compare / select per element); scale and subtract run as packed f32 pairs,
 // as m - S: fl(m - S) = -fl(S - m), so its f16 bits are the table index
 // f16(|S - m|) with no mask (m is never -0: the caller adds +0).
 typedef float f2v __attribute__((ext_vector_type(2)));
-template <int PASS, bool TAIL>
+template <int KQ, int PASS, bool TAIL>
 __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, const f16 *Vb, int key0, int kb,
                                            const uint16_t *tab, const half8 (&qf)[4], float &mx, double &sum,
-                                           float m, floatx16 &o0, floatx16 &o1) {
+                                           float m, float inv, floatx16 &o0, floatx16 &o1) {
+    constexpr int VLD = 32 * KQ + 8;
     const int lane = threadIdx.x & 63, lr = lane & 31, lh = lane >> 5;
     const int T = a.T;
     const uint32_t n_exp = (uint32_t)a.n_exp;
@@ -955,17 +955,17 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
                     i = i < n_exp ? i : n_exp;  // v_min: index n_exp holds 0
                     if (TAIL) i = key < T ? i : n_exp;
                     const float e = h2f_bits(tab[i]);  // unguarded read (a guarded one branches per element)
-                    sum += (double)e;
-                    pa[(r + u) >> 3][(r + u) & 7] = (f16)e;  // (an f16 value: exact)
+                    if constexpr (PASS == 1) sum += (double)e;
+                    else pa[(r + u) >> 3][(r + u) & 7] = f16_rt(e * inv);  // P16 = f16(p * (1 / sum))
                 }
             }
-            {
+            if constexpr (PASS == 2) {
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
                     half8 vb[2];
 #pragma unroll
                     for (int dt = 0; dt < 2; ++dt) {
-                        const f16 *vp = Vb + (dt * 32 + lr) * AT4_VLD + kb * 32 + 16 * s + 4 * lh;
+                        const f16 *vp = Vb + (dt * 32 + lr) * VLD + kb * 32 + 16 * s + 4 * lh;
                         const half4 v0 = *(const half4 *)vp, v1 = *(const half4 *)(vp + 8);
                         vb[dt][0] = v0[0]; vb[dt][1] = v0[1]; vb[dt][2] = v0[2]; vb[dt][3] = v0[3];
                         vb[dt][4] = v1[0]; vb[dt][5] = v1[1]; vb[dt][6] = v1[2]; vb[dt][7] = v1[3];
@@ -978,7 +978,7 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
     }
 }
 
-// One sweep over the key tiles (PASS 0: max, 1: exp sum and P V).  Tiles
+// One sweep over the key tiles (PASS 0: max, 1: exp sum, 2: P16 V).  Tiles
 // go global -> registers -> LDS with two register stages: while tile kt is
 // computed from LDS, tile kt + 1 sits in one register set (stored to the
 // other LDS buffer after the compute) and tile kt + 2's loads are in flight
@@ -987,16 +987,17 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
 // unconditional from a clamped tile, so no undef phi reaches scratch).  The
 // partial last tile runs after the loop: a full / tail branch inside it made
 // the compiler copy both MFMA accumulators every iteration (32 v_mov a tile).
-template <int NW, int PASS>
+template <int NW, int KQ, int PASS>
 __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, const f16 *Vt, f16 *Ks, f16 *Vs,
                                             const uint16_t *tab, const half8 (&qf)[4], float &mx, double &sum,
-                                            float m, floatx16 &o0, floatx16 &o1) {
+                                            float m, float inv, floatx16 &o0, floatx16 &o1) {
+    constexpr int AT4_KT = 32 * KQ, AT4_VLD = AT4_KT + 8;
     const int tid = threadIdx.x;
     const int Tp = a.Tp;
     const int ntiles = (a.T + AT4_KT - 1) / AT4_KT;
-    constexpr int NT = 64 * AT4_KQ * NW;  // threads: NW query blocks x KQ key parts
+    constexpr int NT = 64 * KQ * NW;  // threads: NW query blocks x KQ key parts
     constexpr int SCH = AT4_KT * 8 / NT;  // 16-byte chunks per thread of a K (or V^T) tile
-    constexpr int VCH = PASS >= 1 ? SCH : 1;
+    constexpr int VCH = PASS == 2 ? SCH : 1;
     constexpr int VCPR = AT4_KT / 8;      // 16-byte chunks per V^T tile row
     const int kb = (threadIdx.x >> 6) / NW;  // this wave's 32-key part of every tile
     a4vec kA[SCH], vA[VCH], kB[SCH], vB[VCH];
@@ -1013,7 +1014,7 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
         _Pragma("unroll") for (int i = 0; i < SCH; ++i) {                                       \
             const int kr_ = key0_ + crow + i * (NT / 8);                                        \
             KR[i] = *(const a4vec *)(K + (int64_t)(kr_ < Tp ? kr_ : Tp - 1) * 64 + ccol);       \
-            if constexpr (PASS >= 1) {                                                          \
+            if constexpr (PASS == 2) {                                                          \
                 const int vc_ = key0_ + vcol;                                                   \
                 VR[i] = *(const a4vec *)(Vt + (int64_t)(vrow + i * (NT / VCPR)) * Tp + (vc_ < Tp ? vc_ : Tp - 8)); \
             }                                                                                   \
@@ -1023,7 +1024,7 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
     {                                                                                           \
         _Pragma("unroll") for (int i = 0; i < SCH; ++i) {                                       \
             *(a4vec *)(Ks + ((BUF) * AT4_KT + crow + i * (NT / 8)) * AT4_LD + ccol) = KR[i];    \
-            if constexpr (PASS >= 1)                                                            \
+            if constexpr (PASS == 2)                                                            \
                 *(a4vec *)(Vs + ((BUF) * 64 + vrow + i * (NT / VCPR)) * AT4_VLD + vcol) = VR[i]; \
         }                                                                                       \
     }
@@ -1036,8 +1037,8 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
         const int buf = kt & 1;
         a4vec kF[SCH], vF[VCH];  // tile kt + 2, requested before this tile's compute
         ATT4_GLOAD(kt + 2, kF, vF)
-        attn4_tile<PASS, false>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * 64 * AT4_VLD, kt * AT4_KT, kb, tab, qf,
-                                mx, sum, m, o0, o1);
+        attn4_tile<KQ, PASS, false>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * 64 * AT4_VLD, kt * AT4_KT, kb, tab, qf,
+                                mx, sum, m, inv, o0, o1);
         ATT4_SSTORE(buf ^ 1, kB, vB)  // (after the last tile: unread)
         __syncthreads();
 #pragma unroll
@@ -1047,8 +1048,8 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
     }
     if (nfull < ntiles) {  // the partial tile (stored by the last iteration)
         const int buf = nfull & 1;
-        attn4_tile<PASS, true>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * 64 * AT4_VLD, nfull * AT4_KT, kb,
-                               tab, qf, mx, sum, m, o0, o1);
+        attn4_tile<KQ, PASS, true>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * 64 * AT4_VLD, nfull * AT4_KT, kb,
+                               tab, qf, mx, sum, m, inv, o0, o1);
         __syncthreads();  // (callers reuse the tile buffers: as after every loop tile)
     }
 #undef ATT4_GLOAD
@@ -1059,8 +1060,9 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
 // tile into its KQ 32-key parts (KQ times the waves per query, for one clip's
 // small grid); their maxima, exact double sums and partial P V meet in LDS,
 // the partial O added in part order.
-template <int NW>
-__global__ __launch_bounds__(64 * AT4_KQ * NW) void k_attn_enc4(AttnArgs a) {
+template <int NW, int KQ>
+__global__ __launch_bounds__(64 * KQ * NW) void k_attn_enc4(AttnArgs a) {
+    constexpr int AT4_KT = 32 * KQ;
     extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
     uint16_t *tab = (uint16_t *)smraw;
     const int tab_bytes = (((a.n_exp + 1) * 2 + 15) / 16) * 16;
@@ -1085,34 +1087,38 @@ __global__ __launch_bounds__(64 * AT4_KQ * NW) void k_attn_enc4(AttnArgs a) {
     {
         const int nch = (a.n_exp + 1 + 7) / 8;  // through the 0 at index n_exp
         const uint4 *tsrc = (const uint4 *)a.exp_tab;
-        for (int i = tid; i < nch; i += 64 * AT4_KQ * NW) ((uint4 *)tab)[i] = tsrc[i];
+        for (int i = tid; i < nch; i += 64 * KQ * NW) ((uint4 *)tab)[i] = tsrc[i];
     }
     // exchange slots for the key-part partners (the V buffers: unused until sweep 2)
     float *xm = (float *)Vs;                          // [KQ NW][64]
-    double *xd = (double *)(xm + AT4_KQ * NW * 64);  // [KQ NW][64]
+    double *xd = (double *)(xm + KQ * NW * 64);  // [KQ NW][64]
     float mx = -INFINITY;
     double sum = 0.0;
     floatx16 o0, o1;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { o0[r] = 0.0f; o1[r] = 0.0f; }
-    attn4_sweep<NW, 0>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, 0.0f, o0, o1);
+    attn4_sweep<NW, KQ, 0>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, 0.0f, 0.0f, o0, o1);
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     xm[w * 64 + lane] = mx;
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < AT4_KQ; ++j) mx = fmaxf(mx, xm[(qw + NW * j) * 64 + lane]);
+    for (int j = 0; j < KQ; ++j) mx = fmaxf(mx, xm[(qw + NW * j) * 64 + lane]);
     const float m = mx * a.scale + 0.0f;  // max of the raw scores, scaled once (never -0)
-    __syncthreads();  // (the exchange slots above are V buffers in the sweep)
-    attn4_sweep<NW, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, o0, o1);
+    attn4_sweep<NW, KQ, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
     sum = sum + __shfl_xor(sum, 32);
-    xd[w * 64 + lane] = sum;  // (the sweep's last barrier freed the V buffers)
+    xd[w * 64 + lane] = sum;  // (xd and xm are disjoint: no barrier after the max reads)
     __syncthreads();
-    // exact double sums of f16 table values: the total is order-independent
+    // exact double sums of f16 table values: the total is order-independent;
+    // ggml's float sum, then 1 / sum in double rounded to float (the oracle's
+    // flash_attn_row)
     double dsum = 0.0;
 #pragma unroll
-    for (int j = 0; j < AT4_KQ; ++j) dsum += xd[(qw + NW * j) * 64 + lane];
-    const float inv = (float)(1.0 / dsum);
-    __syncthreads();  // (the exchange slots are read before the O exchange reuses the LDS)
+    for (int j = 0; j < KQ; ++j) dsum += xd[(qw + NW * j) * 64 + lane];
+    const float inv = (float)(1.0 / (double)(float)dsum);
+    // (lane lr's inv belongs to query lr; the P16 operand of lane (lr, lh)
+    // row r is query lr too: the score tile is K Q^T, keys in rows)
+    __syncthreads();  // (the exchange slots are V buffers in sweep 2)
+    attn4_sweep<NW, KQ, 2>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, inv, o0, o1);
     // key parts 1 .. KQ - 1: partial O -> LDS (the K / V buffers are free
     // now), added to part 0's in part order
     float *xo = (float *)smraw;  // [KQ - 1][NW][32][64] over the table and tiles (free now)
@@ -1128,7 +1134,7 @@ __global__ __launch_bounds__(64 * AT4_KQ * NW) void k_attn_enc4(AttnArgs a) {
     __syncthreads();
     if (kb) return;
 #pragma unroll
-    for (int j = 1; j < AT4_KQ; ++j) {
+    for (int j = 1; j < KQ; ++j) {
         const float *xp = xo + (size_t)(j - 1) * NW * 32 * 64;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -1136,15 +1142,6 @@ __global__ __launch_bounds__(64 * AT4_KQ * NW) void k_attn_enc4(AttnArgs a) {
             o0[r] = o0[r] + xp[(qw * 32 + qq) * 64 + lr];
             o1[r] = o1[r] + xp[(qw * 32 + qq) * 64 + 32 + lr];
         }
-    }
-    // (inv is per query: lane lr's inv belongs to query lr; row r of the
-    // accumulators holds query (r & 3) + 8 (r >> 2) + 4 lh)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int qq = (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const float iq = __shfl(inv, qq);
-        o0[r] = o0[r] * iq;
-        o1[r] = o1[r] * iq;
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -1162,61 +1159,56 @@ __global__ __launch_bounds__(64 * AT4_KQ * NW) void k_attn_enc4(AttnArgs a) {
     }
 }
 
-template <int NW>
+template <int NW, int KQ>
 static hipError_t attn_enc4_launch(hipStream_t s, const AttnArgs &a) {
+    constexpr int AT4_KT = 32 * KQ, AT4_VLD = AT4_KT + 8;
     const size_t tabb = (((a.n_exp + 1) * 2 + 15) / 16) * 16;
     const size_t tiles = (size_t)2 * AT4_KT * AT4_LD * 2 + (size_t)2 * 64 * AT4_VLD * 2;
-    const size_t xob = (size_t)(AT4_KQ - 1) * NW * 32 * 64 * 4;  // the partial-O exchange (over table + tiles)
+    const size_t xob = (size_t)(KQ - 1) * NW * 32 * 64 * 4;  // the partial-O exchange (over table + tiles)
     const size_t lds = tabb + tiles > xob ? tabb + tiles : xob;
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    hipError_t e = allow_lds(k_attn_enc4<NW>, lds);
+    hipError_t e = allow_lds(k_attn_enc4<NW, KQ>, lds);
     if (e != hipSuccess) return e;
     dim3 grid(cdiv(a.T, 32 * NW), a.H, a.n_clips);
-    hipLaunchKernelGGL(k_attn_enc4<NW>, grid, dim3(64 * AT4_KQ * NW), lds, s, a);
+    hipLaunchKernelGGL((k_attn_enc4<NW, KQ>), grid, dim3(64 * KQ * NW), lds, s, a);
     return hipGetLastError();
 }
 
-// Query blocks per workgroup, each with KQ = 4 key-part waves: 4 once the
-// grid holds >= 2 workgroups per CU (8 clips of base: 2.38 ms at 2, 2.25-2.30
-// at 4 — 1024 threads, 20 VGPRs spilled — as more waves per CU hide more),
-// else 2.  NW does not change a wave's arithmetic, so a clip's result is
-// batch-independent.  (KQ = 4 against KQ = 2: one clip 0.69 -> 0.64 ms,
-// eight 2.09 -> 2.25-2.30 ms, profiles/r05/enc_kq4_ab.txt)
+// Query blocks per workgroup: 4 once the grid holds >= 2 workgroups per CU
+// (8 clips of base: 2.38 ms at 2, 2.25-2.30 at 4 — 1024 threads, 20 VGPRs
+// spilled — as more waves per CU hide more), else 2.  NW does not change a
+// wave's arithmetic, so a clip's result is batch-independent.
 int attn_enc_nw(int T, int H, int n_clips, int nw_knob) {
     if (nw_knob == 1 || nw_knob == 2 || nw_knob == 4) return nw_knob;
     return (int64_t)cdiv(T, 128) * H * n_clips >= 512 ? 4 : 2;
 }
 
+// Key parts per query block, per model (never per batch: the P V partials'
+// order is the arithmetic, so a clip's output stays batch-independent):
+// four where one clip's query blocks leave the SIMDs idle (base: 8 heads x
+// 47 blocks = 376 -> four-part waves, one clip 0.69 -> 0.645 ms in the
+// two-sweep form, profiles/r05/enc_kq4_ab.txt), two where they fill the chip
+// by themselves (small: 564, large-v3: 940 blocks).
+int attn_enc_kq(int T, int H) { return (int64_t)cdiv(T, 32) * H >= 512 ? 2 : 4; }
+
 hipError_t launch_attn_enc(hipStream_t s, const AttnArgs &a) {
     const Tune &tn = tune_of(a.tune);
     if (a.T < 1 || a.Tp % 64 || a.Tp < a.T) return hipErrorInvalidValue;
     const int nw = attn_enc_nw(a.T, a.H, a.n_clips, tn.enc_attn_nw);
-    if (nw == 4) return attn_enc4_launch<4>(s, a);
-    if (nw == 2) return attn_enc4_launch<2>(s, a);
-    return attn_enc4_launch<1>(s, a);
+    if (attn_enc_kq(a.T, a.H) == 2) {
+        if (nw == 4) return attn_enc4_launch<4, 2>(s, a);
+        if (nw == 2) return attn_enc4_launch<2, 2>(s, a);
+        return attn_enc4_launch<1, 2>(s, a);
+    }
+    if (nw == 4) return attn_enc4_launch<4, 4>(s, a);
+    if (nw == 2) return attn_enc4_launch<2, 4>(s, a);
+    return attn_enc4_launch<1, 4>(s, a);
 }
 
 // ============================================================================
 // decoder step kernels (batch B <= 8 clips), latency-oriented
 // ============================================================================
 constexpr int DG_MAXB = 8;
-
-// WMI_TRACE timeline: thread 0 of every workgroup folds its start time into
-// slot[0] (min) and its end time into slot[1] (min of the complement = max);
-// s_memrealtime is the 100 MHz device-wide reference clock.
-__device__ __forceinline__ void trace_begin(unsigned long long *slot) {
-    if (slot && threadIdx.x == 0) atomicMin(slot, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-}
-__device__ __forceinline__ void trace_phase(unsigned long long *ph, int i) {
-    if (ph && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 &&
-        (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
-        ph[(blockIdx.x ? 8 : 0) + i] = __builtin_amdgcn_s_memrealtime();
-}
-__device__ __forceinline__ void trace_end(unsigned long long *slot) {
-    if (slot && threadIdx.x == 0) atomicMin(slot + 1, ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
-}
-
-
 
 // y[b][o] = W[o] . in[b]  for B <= 8 input rows.  A quarter-wave (16 lanes)
 // owns one output row; a wave owns 4*G rows, a workgroup 16*G.  Latency is
@@ -1340,8 +1332,6 @@ __device__ __forceinline__ uint2 wload(const uint2 *p) {
 // chip bandwidth, bound a 2 MiB GEMV spread over 32-128 workgroups)
 template <int EPI, int IN, int G, int NC, int WQ, int NW>
 __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
-    trace_begin(a.trace);
-    trace_phase(a.phase, 0);
     // chunk geometry: a quarter-wave covers CW consecutive weights of its row
     // per chunk, a lane LW of them (f16: 8 = one 16-byte load; q5_1: 32 = one
     // block, its 16 nibble bytes + an 8-byte {5th bits, d/m} word)
@@ -1505,7 +1495,6 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
         load_set(S1, rbase(rgB), 0);
         load_epi(S1, rbase(rgB));
     }
-    trace_phase(a.phase, 1);
     if (IN == 0 || IN == 3) {
         // each wave normalises rows w, w + NW, ...
         const int pos = (IN == 3) ? a.st->pos : 0;
@@ -1577,7 +1566,6 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
     }
     if (EPI == DEC_LOGITS && tid < DG_MAXB) amax_s[tid] = 0ull;
     __syncthreads();
-    trace_phase(a.phase, 2);
     float acc[G][DG_MAXB];
     if constexpr (PIPE) {  // K <= DG_KB (checked by the launcher)
         for (;;) {
@@ -1604,25 +1592,20 @@ __global__ __launch_bounds__(64 * NW) void k_dec_gemv(DecGemvArgs a) {
             if (k0 > 0) load_set(S0, rbase(rgA), k0);
             dot_set(S0, k0, acc);
         }
-        trace_phase(a.phase, 3);
         finish(rbase(rgA), acc, S0);
-        trace_phase(a.phase, 4);
     }
     if (EPI == DEC_LOGITS) {
         __syncthreads();
         if (a.amax && tid < B && amax_s[tid]) atomicMax(&a.amax[tid * AMAX_SHARDS + (blockIdx.x & (AMAX_SHARDS - 1))], amax_s[tid]);
         if (blockIdx.x == 0 && tid == 0) a.st_advance->pos += 1;
     }
-    trace_phase(a.phase, 7);
-    trace_end(a.trace);
 }
 
-// waves per workgroup of the per-layer GEMVs (WMI_GEMV_NW=1 / 0 = one wave /
-// one wave at B <= 2): 4 measured fastest at base, B = 1 (one wave per
-// workgroup: mlp0 4.6 -> 10 us, every workgroup repeating the LayerNorm)
-// row groups per register set of the vocabulary GEMV at K <= 512 (WMI_LOGITS_G
-// = 1 / 2 / 4) and its persistent grid cap (WMI_LOGITS_CAP2): base 13.9 us at
-// G = 1 -> 12.1 us at G = 2 over 1024 workgroups
+// waves per workgroup of the per-layer GEMVs (Tune::gemv_nw, fixed at 4: one
+// wave per workgroup measured mlp0 4.6 -> 10 us at base, B = 1, every
+// workgroup repeating the LayerNorm); row groups per register set of the
+// vocabulary GEMV at K <= 512 (Tune::logits_g, fixed at 2: base 13.9 us at
+// G = 1 -> 12.1 us at G = 2 over 1024 workgroups)
 
 template <int EPI, int IN, int WQ, int NW>
 static hipError_t dec_gemv_nw(hipStream_t s, const DecGemvArgs &a) {
@@ -1838,8 +1821,6 @@ __device__ __forceinline__ void xattn_load_v(const DecAttnArgs &a, int c, int h,
 // head) replaces the kernel boundary, then phase B runs in the same launch.
 template <int KC, int MODE>
 __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
-    trace_begin(a.trace);
-    trace_phase(a.phase, 0);
     constexpr bool COH = MODE == 1;
     const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1921,7 +1902,6 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
         ln_regs_to_lds(xv, n, gw, gb, xs, lane);
     }
     __syncthreads();
-    trace_phase(a.phase, 1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         float acc = 0.0f;
@@ -1931,7 +1911,6 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
         if (l16 == 0) qh[w * 16 + q * 4 + i] = f16_rt((acc + bqr[i]) * a.qscale);
     }
     __syncthreads();
-    trace_phase(a.phase, 2);
     float s = 0.0f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) s = dot8(kf[i], *(const half8 *)(qh + half * 32 + 8 * i), s);
@@ -1945,13 +1924,11 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
     if (tid == 0)
         st_x<COH>(a.cmax + ((int64_t)b * a.H + h) * a.n_chunks + c, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
     if (MODE == 0) {
-        trace_end(a.trace);
         return;
     }
     // ---- arrival: this chunk's scores and max are globally visible ----
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    trace_phase(a.phase, 3);
     if (tid == 0) {
         XSync *sy = a.sync + ((int64_t)b * a.H + h);
         const uint32_t epoch = (uint32_t)a.st->pos + 1u;
@@ -1959,10 +1936,7 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
         spin_until(&sy->cnt, epoch * (uint32_t)a.n_chunks, a.err);
     }
     __syncthreads();
-    trace_phase(a.phase, 4);
     xattn_pv<COH>(a, c, h, b, M, vf);
-    trace_phase(a.phase, 7);
-    trace_end(a.trace);
 }
 
 // Phase A of cross-attention for beam rows, which all read one clip's cross
@@ -1973,7 +1947,6 @@ __global__ __launch_bounds__(256) void k_dec_xattn(DecAttnArgs a) {
 // and cmax are bit-identical; k_dec_attn_pv follows as in the two-kernel form.
 template <int KC>
 __global__ __launch_bounds__(256) void k_dec_xattn_rows(DecAttnArgs a) {
-    trace_begin(a.trace);
     const int c = blockIdx.x, h = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int q = lane >> 4, l16 = lane & 15;
@@ -2059,17 +2032,14 @@ __global__ __launch_bounds__(256) void k_dec_xattn_rows(DecAttnArgs a) {
     if (tid < B)
         a.cmax[((int64_t)tid * a.H + h) * a.n_chunks + c] =
             fmaxf(fmaxf(red[tid][0], red[tid][1]), fmaxf(red[tid][2], red[tid][3]));
-    trace_end(a.trace);
 }
 
 __global__ __launch_bounds__(256) void k_dec_attn_pv(DecAttnArgs a) {
-    trace_begin(a.trace);
     const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
     const int M = a.M_fixed;
     half8 vf[4];
     xattn_load_v(a, c, h, b, M, vf);
     xattn_pv<false>(a, c, h, b, M, vf);
-    trace_end(a.trace);
 }
 
 // self-attention over the KV cache (M = pos + 1 <= 512 keys): one workgroup
@@ -2078,8 +2048,6 @@ __global__ __launch_bounds__(256) void k_dec_attn_pv(DecAttnArgs a) {
 template <int MK>  // keys covered: M = pos + 1 <= MK (64, 128, 256 or 512)
 __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     constexpr int RK = MK > 256 ? 2 : 1, NVI = MK / 32;
-    trace_begin(a.trace);
-    trace_phase(a.phase, 0);
     const int h = blockIdx.x, b = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int M = a.st->pos + 1;
@@ -2154,7 +2122,6 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
             for (int i = 0; i < 8; ++i) wov[r][i] = wload((const half8 *)(a.Wo + (int64_t)orow * n + h * 64 + 8 * i));
         }
     }
-    trace_phase(a.phase, 1);
     float sc[RK];
     float mx = -INFINITY;
 #pragma unroll
@@ -2187,7 +2154,6 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
     for (int r = 0; r < RK; ++r)
         if (tid + 256 * r < MK) P[tid + 256 * r] = f2h_bits(tid + 256 * r < M ? p[r] * inv : 0.0f);
     __syncthreads();
-    trace_phase(a.phase, 2);
     float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < NVI; ++i) {
@@ -2204,10 +2170,8 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) ored[w][lane * 8 + e] = o[e];
     __syncthreads();
-    trace_phase(a.phase, 3);
     if (!a.Wo) {
         if (tid < 64) a.opart[(int64_t)b * n + h * 64 + tid] = ((ored[0][tid] + ored[1][tid]) + ored[2][tid]) + ored[3][tid];
-        trace_end(a.trace);
         return;
     }
     __shared__ __attribute__((aligned(16))) f16 oh[64];
@@ -2224,8 +2188,6 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
         for (int i = 0; i < 4; ++i) acc = dot8(wov[0][i], part ? ov[4 + i] : ov[i], acc);
         const float other = __uint_as_float(dpp_xor1(__float_as_uint(acc)));
         if (part == 0) dst[blockIdx.z * 128 + (tid >> 1)] = acc + other;  // summed by the next kernel's prologue
-        trace_phase(a.phase, 7);
-        trace_end(a.trace);
         return;
     }
     for (int r = 0; r * 256 < n; ++r) {
@@ -2244,7 +2206,6 @@ __global__ __launch_bounds__(256) void k_dec_self_attn(DecAttnArgs a) {
         for (int i = 0; i < 8; ++i) acc = dot8(wr[i], ov[i], acc);
         if (orow < n) dst[orow] = acc;  // summed by the next kernel's prologue
     }
-    trace_end(a.trace);
 }
 
 
@@ -2461,10 +2422,8 @@ __device__ __forceinline__ unsigned long long beam_key(float v, int id) {
 // one vocabulary split of one row: split max, sum exp(logit - max) (double)
 // and the split's top-(K+1)
 __global__ __launch_bounds__(256) void k_beam_topk(BeamArgs a) {
-    trace_begin(a.trace);
     const int sp = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (a.st->pos < a.feed_len || a.bs->done || b >= a.bs->n_active) {
-        trace_end(a.trace);
         return;
     }
     __shared__ float redf[4];
@@ -2526,7 +2485,6 @@ __global__ __launch_bounds__(256) void k_beam_topk(BeamArgs a) {
         out->m = m;
         out->sum = ((redd[0] + redd[1]) + redd[2]) + redd[3];
     }
-    trace_end(a.trace);
 }
 
 // candidate i before candidate j in the ranking (score desc, beam asc, rank asc)
@@ -2539,11 +2497,9 @@ __device__ __forceinline__ bool cand_before(double si, int bi, int ri, double sj
 // one workgroup: merge the splits, rank the K x (K+1) candidates, fill the
 // next hypotheses, record finished ones, and re-point the KV history table
 __global__ __launch_bounds__(256) void k_beam_select(BeamArgs a) {
-    trace_begin(a.trace);
     BeamState *bs = a.bs;
     const int pos = a.st->pos;
     if (pos < a.feed_len || bs->done) {
-        trace_end(a.trace);
         return;
     }
     const int t = pos - a.feed_len, K = a.K, TK = K + 1;
@@ -2646,7 +2602,6 @@ __global__ __launch_bounds__(256) void k_beam_select(BeamArgs a) {
         const int sl = i / pos, j = i - sl * pos, p = sel_parent[sl];
         a.kv_src[sl * a.tctx + j] = j < pos - 1 ? src_old[p][j] : p;
     }
-    trace_end(a.trace);
 }
 
 hipError_t launch_beam_step(hipStream_t s, const BeamArgs &a) {

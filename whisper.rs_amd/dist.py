@@ -21,8 +21,28 @@ _PORT_STRIDE = 97
 _MAX_MSG = 1 << 24  # messages are ids, timings and small token lists
 _MAGIC = b"wmi-rdv1"
 _CONFIRM = b"wmi-rdv1-ok"
-_HS_HUB = 10.0   # rank 0's per-connection handshake reads
+_HS_HUB = 10.0   # rank 0's handshake deadline per connection (hello + confirm together)
 _HS_PEER = 15.0  # a peer's wait for rank 0's ack: longer than _HS_HUB
+
+
+def _alive(sock) -> bool:
+    """A registered peer's socket still open (a zero-timeout peek: EOF or an
+    error means its process went away; no data pending means it waits)."""
+    t = sock.gettimeout()
+    try:
+        sock.setblocking(False)
+        return sock.recv(1, socket.MSG_PEEK) != b""
+    except BlockingIOError:
+        return True
+    except OSError:
+        return False
+    finally:
+        sock.settimeout(t)
+
+
+def _recv_by(sock, deadline: float) -> bytes:
+    sock.settimeout(max(0.01, deadline - time.time()))
+    return _recv(sock)
 
 
 def hub_ports(master_port: int):
@@ -128,9 +148,12 @@ class Group:
                     srv.settimeout(left)
                     c, _ = srv.accept()
                     c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                    c.settimeout(min(timeout, _HS_HUB))
+                    # one deadline for the whole handshake of this connection
+                    # (hello + confirm): rank 0 is held at most _HS_HUB by any
+                    # one connection, less than a peer waits for its ack
+                    hs = time.time() + min(timeout, _HS_HUB)
                     try:
-                        msg = _recv(c)
+                        msg = _recv_by(c, hs)
                         r = struct.unpack("<i", msg[-4:])[0] if len(msg) == len(hello) + 4 and msg[:-4] == hello \
                             else -1
                         if 1 <= r < world:
@@ -138,14 +161,20 @@ class Group:
                             # its peer abandoned (it gave up waiting and
                             # reconnected) fails here instead of being kept
                             _send(c, hello)
-                            if _recv(c) != _CONFIRM:
+                            if _recv_by(c, hs) != _CONFIRM:
                                 r = -1
                     except (ConnectionError, OSError):
                         r = -1
                     if not 1 <= r < world:  # foreign, out of range or abandoned: not a peer
                         c.close()
                         continue
-                    if r in peers:  # the same rank again: its newer connection wins
+                    if r in peers:
+                        # the same rank again: a reconnect replaces a peer whose
+                        # socket is dead; a second live process claiming the
+                        # rank (a misconfiguration) is refused, the first kept
+                        if _alive(peers[r]):
+                            c.close()
+                            continue
                         peers[r].close()
                     c.settimeout(timeout)
                     peers[r] = c

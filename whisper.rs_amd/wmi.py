@@ -393,12 +393,22 @@ class WhisperContext:
         return buf.raw
 
     def step_logits(self, n_pos: int) -> np.ndarray:
-        """Every position's logits of the last persistent greedy decode,
-        [n_pos][8 rows][V] (contexts created with WMI_LOGITS_ALL=1: position
-        p's logits predict the token after the one fed at p)."""
+        """Every position's logits of the last persistent greedy decode or
+        beam search, [n_pos][rows][V] with rows = max(8, max_clips) (contexts
+        created with WMI_LOGITS_ALL=1: position p's logits predict the token
+        after the one fed at p; greedy: clip b in row b; beam: slot s)."""
         V = self.hparams["n_vocab"]
-        raw = self.debug_read(13, n_pos * 8 * V * 4)
-        return np.frombuffer(raw, np.float32).reshape(n_pos, 8, V).copy()
+        rows = int(np.frombuffer(self.debug_read(16, 4), np.int32)[0])
+        raw = self.debug_read(13, n_pos * rows * V * 4)
+        return np.frombuffer(raw, np.float32).reshape(n_pos, rows, V).copy()
+
+    def beam_history(self, n_steps: int):
+        """The last beam search's selections (its last clip): (parent slot,
+        token) arrays [n_steps][8] — slot s after generation step t came from
+        slot parent[t][s] of step t - 1 and appended token[t][s]."""
+        par = np.frombuffer(self.debug_read(14, n_steps * 8 * 4), np.int32).reshape(n_steps, 8).copy()
+        tok = np.frombuffer(self.debug_read(15, n_steps * 8 * 4), np.int32).reshape(n_steps, 8).copy()
+        return par, tok
 
     # --- parity getters -----------------------------------------------------
     def mel(self, clip: int = 0) -> np.ndarray:
