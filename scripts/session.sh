@@ -13,6 +13,7 @@
 #   beamtrace=MODEL:K  the same for a K-beam search (16 steps): TAG_beamtrace_MODEL_K.log
 #   prof               rocprofv3 kernel-trace summary of the base bench: TAG_prof/
 #   pmc=MODEL:CLIPS    FETCH_SIZE / WRITE_SIZE passes of the persistent decoder (kernel 14): TAG_pmc_MODEL_CLIPS*
+#   encpmc=MODEL:CLIPS per-kernel MFMA utilisation of the encoder: TAG_encpmc_MODEL_CLIPS.txt
 #   probe=MODEL:CLIPS:NTOK[:beam]  step-logit parity probe (scripts/parity_probe.py): TAG_probe_MODEL_CLIPS.log
 #   ab=ENV1,ENV2,...   bench (base, 1 clip, 10 steps) alternating environments, e.g. ab=WMI_LIB=whisper.rs_amd/ab/X/libwhisper_mi355x.so,WMI_LIB=
 #                      (MODEL, CPG, BEAM in the environment select another config): TAG_ab.txt
@@ -67,6 +68,17 @@ import json; d=json.load(open('${O}_bench.json')); print('bench', d['value'], d[
           python3 $R/scripts/kernel_probe.py $m 14 3 128 $c > ${O}_pmc_${m}_${c}_trace.log 2>&1) || exit 1
       unset WMI_NO_GRAPH
       cat ${O}_pmc_${m}_${c}_trace.log ;;
+    encpmc)
+      # per-kernel MFMA utilisation of the encoder: a kernel-trace pass and a
+      # SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE pass over the same encodes
+      m=${arg%%:*}; c=${arg#*:}
+      (cd /tmp && export TMPDIR=/tmp && \
+        timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d ${O}_encpmc_${m}_${c}_trace -o run -- \
+          python3 $R/scripts/encode_probe.py $m $c 5 > ${O}_encpmc_${m}_${c}_trace.log 2>&1 && \
+        timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
+          -d ${O}_encpmc_${m}_${c}_pmc -o run -- python3 $R/scripts/encode_probe.py $m $c 5 \
+          > ${O}_encpmc_${m}_${c}_pmc.log 2>&1) || exit 1
+      python3 scripts/enc_mfma_summary.py ${O}_encpmc_${m}_${c}_trace ${O}_encpmc_${m}_${c}_pmc ${O}_encpmc_${m}_${c}.txt ;;
     probe)
       IFS=: read -ra pa <<< "$arg"
       timeout -k 10 600 python3 -u scripts/parity_probe.py "${pa[@]}" > ${O}_probe_${pa[0]}_${pa[1]}${pa[3]}.log 2>&1 || exit 1
