@@ -1819,8 +1819,13 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
             }
                 PSTAMP(L * 32 + 16)
             const int lr = lane & 15, lh = lane >> 4;
-            const int rres = rv0 + ((rs0 - rv0) & ~15);  // resident tiles end (whole tiles)
-            const int nst = (rv1 - rres + 15) >> 4;        // streamed tiles
+            // resident tiles cover [rv0, rs0) — the last one partial, its
+            // missing rows read clamped and masked — and the streamed tiles
+            // start at rs0: at base 139 resident + 64 streamed rows, one
+            // streamed tile a wave (round 5: 128 + 75, the fifth tile behind
+            // wave 0's resident ones)
+            const int rres = rs0, nres_t = rs0 - rv0;  // resident rows end, count
+            const int nst = (rv1 - rres + 15) >> 4;    // streamed tiles
             const f16 *te = (const f16 *)a.te;
             const half8 z8 = {};
             auto sload = [&](half8 (&f)[NK], int t) {  // streamed tile t's B fragments
@@ -1856,8 +1861,8 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                     if (valid && n != a.suppress_id) best[r] = k > best[r] ? k : best[r];
                 }
             };
-            for (int t = w; 16 * t < rres - rv0; t += 4) {  // resident tiles
-                const int j = 16 * t + lr;                   // row within the resident copy
+            for (int t = w; 16 * t < nres_t; t += 4) {  // resident tiles
+                const int j = 16 * t + lr < nres_t ? 16 * t + lr : nres_t - 1;  // row within the resident copy
                 const f16 *wr = vres + j * NS;
                 // every B fragment of the tile requested before the first
                 // MFMA (one LDS latency a tile, not one per MFMA step: the
