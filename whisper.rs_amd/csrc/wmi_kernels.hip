@@ -15,6 +15,7 @@
 // f32 multiply/add stay separately rounded (no FMA contraction) everywhere a
 // reference operation is restated; MFMA and the dot-product accumulations
 // are the only places where the summation order differs from the CPU.
+#include <utility>
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -918,15 +919,39 @@ typedef uint32_t a4vec __attribute__((ext_vector_type(4)));
 // as m - S: fl(m - S) = -fl(S - m), so its f16 bits are the table index
 // f16(|S - m|) with no mask (m is never -0: the caller adds +0).
 typedef float f2v __attribute__((ext_vector_type(2)));
+// PASS 3 (sum sweep, one clip): as PASS 1, and the table values p kept in
+// pst (registers: the tile's two P fragments); PASS 4: P16 = f16(p * inv)
+// from pst — no Q K^T and no table reads — then P16 V
 template <int KQ, int PASS, bool TAIL>
 __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, const f16 *Vb, int key0, int kb,
                                            const uint16_t *tab, const half8 (&qf)[4], float &mx, double &sum,
-                                           float m, float inv, floatx16 &o0, floatx16 &o1) {
+                                           float m, float inv, floatx16 &o0, floatx16 &o1, half8 (&pst)[2]) {
     constexpr int VLD = 32 * KQ + 8;
     const int lane = threadIdx.x & 63, lr = lane & 31, lh = lane >> 5;
     const int T = a.T;
     const uint32_t n_exp = (uint32_t)a.n_exp;
     const f2v scale2 = {a.scale, a.scale}, m2 = {m, m};
+    if constexpr (PASS == 4) {
+        half8 pa[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pa[s][i] = f16_rt((float)pst[s][i] * inv);  // (keys past T: p = 0)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            half8 vb[2];
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+                const f16 *vp = Vb + (dt * 32 + lr) * VLD + kb * 32 + 16 * s + 4 * lh;
+                const half4 v0 = *(const half4 *)vp, v1 = *(const half4 *)(vp + 8);
+                vb[dt][0] = v0[0]; vb[dt][1] = v0[1]; vb[dt][2] = v0[2]; vb[dt][3] = v0[3];
+                vb[dt][4] = v1[0]; vb[dt][5] = v1[1]; vb[dt][6] = v1[2]; vb[dt][7] = v1[3];
+            }
+            o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[s], vb[0], o0, 0, 0, 0);
+            o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[s], vb[1], o1, 0, 0, 0);
+        }
+        return;
+    }
     {  // this wave's 32-key part kb of the tile
         floatx16 sc;
 #pragma unroll
@@ -955,9 +980,14 @@ __device__ __forceinline__ void attn4_tile(const AttnArgs &a, const f16 *Kb, con
                     i = i < n_exp ? i : n_exp;  // v_min: index n_exp holds 0
                     if (TAIL) i = key < T ? i : n_exp;
                     const float e = h2f_bits(tab[i]);  // unguarded read (a guarded one branches per element)
-                    if constexpr (PASS == 1) sum += (double)e;
-                    else pa[(r + u) >> 3][(r + u) & 7] = f16_rt(e * inv);  // P16 = f16(p * (1 / sum))
+                    if constexpr (PASS == 1 || PASS == 3) sum += (double)e;
+                    if constexpr (PASS == 3) pa[(r + u) >> 3][(r + u) & 7] = (f16)e;  // (an f16 value: exact)
+                    if constexpr (PASS == 2) pa[(r + u) >> 3][(r + u) & 7] = f16_rt(e * inv);  // P16 = f16(p * (1 / sum))
                 }
+            }
+            if constexpr (PASS == 3) {
+                pst[0] = pa[0];
+                pst[1] = pa[1];
             }
             if constexpr (PASS == 2) {
 #pragma unroll
@@ -1007,6 +1037,7 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
     // read clamped: masked scores, finite values
     const int crow = tid >> 3, ccol = (tid & 7) * 8;
     const int vrow = tid / VCPR, vcol = (tid % VCPR) * 8;
+    half8 pdummy[2];
 #define ATT4_GLOAD(KT, KR, VR)                                                                  \
     {                                                                                           \
         const int kt_ = (KT) < ntiles ? (KT) : ntiles - 1;                                      \
@@ -1038,7 +1069,7 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
         a4vec kF[SCH], vF[VCH];  // tile kt + 2, requested before this tile's compute
         ATT4_GLOAD(kt + 2, kF, vF)
         attn4_tile<KQ, PASS, false>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * 64 * AT4_VLD, kt * AT4_KT, kb, tab, qf,
-                                mx, sum, m, inv, o0, o1);
+                                    mx, sum, m, inv, o0, o1, pdummy);
         ATT4_SSTORE(buf ^ 1, kB, vB)  // (after the last tile: unread)
         __syncthreads();
 #pragma unroll
@@ -1049,11 +1080,86 @@ __device__ __forceinline__ void attn4_sweep(const AttnArgs &a, const f16 *K, con
     if (nfull < ntiles) {  // the partial tile (stored by the last iteration)
         const int buf = nfull & 1;
         attn4_tile<KQ, PASS, true>(a, Ks + buf * AT4_KT * AT4_LD, Vs + buf * 64 * AT4_VLD, nfull * AT4_KT, kb,
-                               tab, qf, mx, sum, m, inv, o0, o1);
+                                   tab, qf, mx, sum, m, inv, o0, o1, pdummy);
         __syncthreads();  // (callers reuse the tile buffers: as after every loop tile)
     }
 #undef ATT4_GLOAD
 #undef ATT4_SSTORE
+}
+
+// The sum sweep keeping p in registers (PASS 3) and the P V sweep reading
+// them (PASS 4: only V tiles staged), for one clip's workgroups (NW <= 2:
+// the registers for a whole row's p fit beside the sweep's — MAXT tiles x 8
+// VGPRs), the tile loop unrolled so every tile's p has its own registers.
+// The arithmetic is PASS 1 / PASS 2's, value for value: a clip's output does
+// not depend on which form ran (test_enc_attn_nw_parity_and_batch_invariance)
+constexpr int AT4_MAXT_REG = 12;  // 128-key tiles held in registers (T <= 1536)
+template <int... I, typename F>
+__device__ __forceinline__ void static_for(std::integer_sequence<int, I...>, F &&f) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int NW, int KQ, int PASS>
+__device__ __forceinline__ void attn4_sweep_reg(const AttnArgs &a, const f16 *K, const f16 *Vt, f16 *Ks, f16 *Vs,
+                                                const uint16_t *tab, const half8 (&qf)[4], double &sum, float m,
+                                                float inv, floatx16 &o0, floatx16 &o1,
+                                                half8 (&ps)[AT4_MAXT_REG][2]) {
+    static_assert(PASS == 3 || PASS == 4, "stored-p passes");
+    constexpr int AT4_KT = 32 * KQ, AT4_VLD = AT4_KT + 8;
+    const int tid = threadIdx.x;
+    const int Tp = a.Tp;
+    const int ntiles = (a.T + AT4_KT - 1) / AT4_KT, nfull = a.T / AT4_KT;
+    constexpr int NT = 64 * KQ * NW;
+    constexpr int SCH = AT4_KT * 8 / NT;
+    constexpr int VCPR = AT4_KT / 8;
+    const int kb = (threadIdx.x >> 6) / NW;
+    const int crow = tid >> 3, ccol = (tid & 7) * 8;
+    const int vrow = tid / VCPR, vcol = (tid % VCPR) * 8;
+    float mx = 0.0f;
+    auto gload = [&](int kt, a4vec (&R)[SCH]) {  // PASS 3: K tile rows; PASS 4: V^T tile columns
+        const int kt_ = kt < ntiles ? kt : ntiles - 1;
+        const int key0 = kt_ * AT4_KT;
+#pragma unroll
+        for (int i = 0; i < SCH; ++i) {
+            if constexpr (PASS == 3) {
+                const int kr = key0 + crow + i * (NT / 8);
+                R[i] = *(const a4vec *)(K + (int64_t)(kr < Tp ? kr : Tp - 1) * 64 + ccol);
+            } else {
+                const int vc = key0 + vcol;
+                R[i] = *(const a4vec *)(Vt + (int64_t)(vrow + i * (NT / VCPR)) * Tp + (vc < Tp ? vc : Tp - 8));
+            }
+        }
+    };
+    auto sstore = [&](int buf, const a4vec (&R)[SCH]) {
+#pragma unroll
+        for (int i = 0; i < SCH; ++i) {
+            if constexpr (PASS == 3) *(a4vec *)(Ks + (buf * AT4_KT + crow + i * (NT / 8)) * AT4_LD + ccol) = R[i];
+            else *(a4vec *)(Vs + (buf * 64 + vrow + i * (NT / VCPR)) * AT4_VLD + vcol) = R[i];
+        }
+    };
+    a4vec rA[SCH], rB[SCH];
+    gload(0, rA);
+    sstore(0, rA);
+    gload(1, rB);
+    __syncthreads();
+    // tile KT as a template step (every tile's p in registers of its own:
+    // a runtime-indexed array would live in scratch memory)
+    auto step = [&](auto KTc) {
+        constexpr int kt = decltype(KTc)::value;
+        if (kt >= ntiles) return;  // workgroup-uniform
+        a4vec rF[SCH];
+        gload(kt + 2, rF);
+        const f16 *Kb = Ks + (kt & 1) * AT4_KT * AT4_LD;
+        const f16 *Vb = Vs + (kt & 1) * 64 * AT4_VLD;
+        if (kt < nfull)
+            attn4_tile<KQ, PASS, false>(a, Kb, Vb, kt * AT4_KT, kb, tab, qf, mx, sum, m, inv, o0, o1, ps[kt]);
+        else
+            attn4_tile<KQ, PASS, true>(a, Kb, Vb, kt * AT4_KT, kb, tab, qf, mx, sum, m, inv, o0, o1, ps[kt]);
+        sstore((kt & 1) ^ 1, rB);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < SCH; ++i) rB[i] = rF[i];
+    };
+    static_for(std::make_integer_sequence<int, AT4_MAXT_REG>{}, step);
 }
 
 // Waves w, w + NW, .. w + (KQ - 1) NW share query block w and split every
@@ -1104,7 +1210,17 @@ __global__ __launch_bounds__(64 * KQ * NW) void k_attn_enc4(AttnArgs a) {
 #pragma unroll
     for (int j = 0; j < KQ; ++j) mx = fmaxf(mx, xm[(qw + NW * j) * 64 + lane]);
     const float m = mx * a.scale + 0.0f;  // max of the raw scores, scaled once (never -0)
-    attn4_sweep<NW, KQ, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
+    // one clip (NW <= 2, four key parts): the sum sweep keeps p in registers
+    // and the P V sweep reads them instead of recomputing Q K^T and the table
+    constexpr bool REG = KQ == 4 && NW <= 2;
+    const bool reg = REG && a.T <= AT4_MAXT_REG * 32 * KQ;
+    half8 ps[REG ? AT4_MAXT_REG : 1][2];
+    if constexpr (REG) {
+        if (reg) attn4_sweep_reg<NW, KQ, 3>(a, K, Vt, Ks, Vs, tab, qf, sum, m, 0.0f, o0, o1, ps);
+        else attn4_sweep<NW, KQ, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
+    } else {
+        attn4_sweep<NW, KQ, 1>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, 0.0f, o0, o1);
+    }
     sum = sum + __shfl_xor(sum, 32);
     xd[w * 64 + lane] = sum;  // (xd and xm are disjoint: no barrier after the max reads)
     __syncthreads();
@@ -1118,7 +1234,12 @@ __global__ __launch_bounds__(64 * KQ * NW) void k_attn_enc4(AttnArgs a) {
     // (lane lr's inv belongs to query lr; the P16 operand of lane (lr, lh)
     // row r is query lr too: the score tile is K Q^T, keys in rows)
     __syncthreads();  // (the exchange slots are V buffers in sweep 2)
-    attn4_sweep<NW, KQ, 2>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, inv, o0, o1);
+    if constexpr (REG) {
+        if (reg) attn4_sweep_reg<NW, KQ, 4>(a, K, Vt, Ks, Vs, tab, qf, sum, m, inv, o0, o1, ps);
+        else attn4_sweep<NW, KQ, 2>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, inv, o0, o1);
+    } else {
+        attn4_sweep<NW, KQ, 2>(a, K, Vt, Ks, Vs, tab, qf, mx, sum, m, inv, o0, o1);
+    }
     // key parts 1 .. KQ - 1: partial O -> LDS (the K / V buffers are free
     // now), added to part 0's in part order
     float *xo = (float *)smraw;  // [KQ - 1][NW][32][64] over the table and tiles (free now)

@@ -580,6 +580,11 @@ struct GSet<KCH, NP, 1, Q5, PAIR> {
 template <int KCH, int NP, bool Q5 = false, bool ALDS = false>  // ALDS: A fragments read from LDS per step
 struct MSet {
     static constexpr int NKQ = KCH;  // (K / 32) / 4 MFMA steps per wave
+    // q5_1 chunks dequantised at each MFMA step, not in the poll: holding
+    // every chunk's blocks and its f16 weights until the poll ended spilled
+    // the 8-row instance at n = 768 (604 B a lane; 72 B now): small-q5_1 x 8
+    // clips 124.7 -> 94.0 ms decode (profiles/r06/q5_lazy_dequant_ab.txt)
+    static constexpr bool LAZY = Q5;
     WChunk<Q5> c[NP][NKQ];
     float bias[NP];
     __device__ __forceinline__ void load(const WMat &W, const float *b, int K, int rb, int r1, int slot, int) {
@@ -601,11 +606,16 @@ struct MSet {
         }
     }
     __device__ __forceinline__ void pre(int) {
+        if constexpr (LAZY) return;
         const int lh = (threadIdx.x & 63) >> 4;
 #pragma unroll
         for (int t = 0; t < NP; ++t)
 #pragma unroll
             for (int i = 0; i < NKQ; ++i) wc_pre(c[t][i], 8 * lh);
+    }
+    __device__ __forceinline__ half8 bfrag(int t, int i, int lh) const {
+        if constexpr (LAZY) return q5_half8(c[t][i].n, c[t][i].hd[0], c[t][i].hd[1], 8 * lh);
+        else return wc_h8(c[t][i], 0);
     }
     // kp: LDS [4][NP][16][8] floats
     template <int BT, typename Epi>
@@ -628,7 +638,7 @@ struct MSet {
             floatx4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int i = 0; i < NKQ; ++i)
-                d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ALDS ? afrag(i) : af[i], wc_h8(c[t][i], 0), d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ALDS ? afrag(i) : af[i], bfrag(t, i, lh), d, 0, 0, 0);
             if (lh < 2)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) kp[((w * NP + t) * 16 + lr) * 8 + 4 * lh + r] = d[r];
