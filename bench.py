@@ -50,7 +50,7 @@ KERNELS = {14: ("hbm", "dec_persist"), 1: ("mfma", "enc_mlp0"), 2: ("mfma", "enc
 # rocprofv3 PMC counters over the same template instance and workload
 # (scripts/pmc_pass.sh + scripts/pmc_summary.py; the profiler cannot run
 # inside this process), keyed by (model, kernel id, n_decode)
-PMC_TRAFFIC = {("base", 14, 128): "profiles/r05/final/pmc_persist_base.json"}
+PMC_TRAFFIC = {("base", 14, 128): "profiles/r06/final/pmc_persist_base.json"}
 # the other single-GPU configs of BASELINE.json / north_star, measured in the
 # same run as the headline (name -> model, clips, beam, steps, what it is)
 EXTRA_CONFIGS = (

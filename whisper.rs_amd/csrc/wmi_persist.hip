@@ -254,6 +254,8 @@ __device__ __forceinline__ void wc_load(WChunk<Q5> &c, const WMat &m, int64_t e)
 // sh = e % 32 (a lane's offset inside its block: (l16 & 3) * 8).  q5_1
 // chunks are dequantised once by wc_pre (called inside the phase's poll,
 // gpoll / poll_ln1 `pre`), to exactly the loader's f16 copy
+// (the one-row GEMVs dequantising at use instead, as the MFMA GEMVs do:
+// C3 decode 36.2-36.7 -> 38.9 ms, profiles/r06/q5_lazy_one_row_ab_REJECTED.txt)
 template <bool Q5>
 __device__ __forceinline__ void wc_pre(WChunk<Q5> &c, int sh) {
     if constexpr (Q5) {
