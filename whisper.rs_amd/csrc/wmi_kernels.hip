@@ -866,6 +866,9 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a0) {
     // mlp.2 77.0 -> 60.2 us; QKV and mlp.0 unchanged)
     if (t128 >= GEMM_G_MIN_TILES && tune_of(a.tune).gemm_g && a.K % 64 == 0 && (!a.conv || a.conv_cp % 64 == 0))
         return a.conv ? gemm_g_dispatch<true>(s, epi, a) : gemm_g_dispatch<false>(s, epi, a);
+    // (128 k a stage for the smaller tiles — half the k steps of these
+    // latency-bound one-clip GEMMs, the same MFMA order — measured slower:
+    // 1-clip encoder 0.685 -> 0.726 ms, profiles/r06/gemm_bk128_ab_REJECTED.txt)
     if (a.conv) {
         if (t128 >= 240) return gemm_dispatch_epi<128, 128, GBK, true>(s, epi, a);
         if (t12864 >= 240) return k64 ? gemm_dispatch_epi<128, 64, 64, true>(s, epi, a)
