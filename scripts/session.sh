@@ -14,6 +14,7 @@
 #   prof               rocprofv3 kernel-trace summary of the base bench: TAG_prof/
 #   pmc=MODEL:CLIPS    FETCH_SIZE / WRITE_SIZE passes of the persistent decoder (kernel 14): TAG_pmc_MODEL_CLIPS*
 #   encpmc=MODEL:CLIPS per-kernel MFMA utilisation of the encoder: TAG_encpmc_MODEL_CLIPS.txt
+#   gemmab=MODEL:CLIPS one-clip encoder GEMM paths A/B (scripts/gemm_p_ab.py): TAG_gemmab_MODEL_CLIPS.log
 #   probe=MODEL:CLIPS:NTOK[:beam]  step-logit parity probe (scripts/parity_probe.py): TAG_probe_MODEL_CLIPS.log
 #   ab=ENV1,ENV2,...   bench (base, 1 clip, 10 steps) alternating environments, e.g. ab=WMI_LIB=whisper.rs_amd/ab/X/libwhisper_mi355x.so,WMI_LIB=
 #                      (MODEL, CPG, BEAM in the environment select another config): TAG_ab.txt
@@ -79,6 +80,11 @@ import json; d=json.load(open('${O}_bench.json')); print('bench', d['value'], d[
           -d ${O}_encpmc_${m}_${c}_pmc -o run -- python3 $R/scripts/encode_probe.py $m $c 5 \
           > ${O}_encpmc_${m}_${c}_pmc.log 2>&1) || exit 1
       python3 scripts/enc_mfma_summary.py ${O}_encpmc_${m}_${c}_trace ${O}_encpmc_${m}_${c}_pmc ${O}_encpmc_${m}_${c}.txt ;;
+    gemmab)
+      # one-clip encoder GEMM paths (WMI_GEMM_P 0 / 1 / 2): bitwise check + interleaved encode medians
+      m=${arg%%:*}; c=${arg#*:}
+      timeout -k 10 300 python3 -u scripts/gemm_p_ab.py $m $c 3 20 > ${O}_gemmab_${m}_${c}.log 2>&1 || exit 1
+      tail -n 3 ${O}_gemmab_${m}_${c}.log ;;
     probe)
       IFS=: read -ra pa <<< "$arg"
       timeout -k 10 600 python3 -u scripts/parity_probe.py "${pa[@]}" > ${O}_probe_${pa[0]}_${pa[1]}${pa[3]}.log 2>&1 || exit 1

@@ -629,17 +629,19 @@ def test_multirow_instances_bitwise_independent_of_B(wmi, model_cache):
 
 
 def test_encoder_gemm_paths_bitwise(wmi, model_cache):
-    """The 8-clip encoder's GEMMs run on the LDS-DMA kernel (k_gemm_g) with
-    epilogues staged through LDS; WMI_GEMM_G=0 / WMI_GEMM_EPI=0 select the
-    register-staged kernel and the per-lane epilogue stores.  All four give
+    """The 8-clip encoder's GEMMs run on the LDS-DMA kernel (k_gemm_g) and
+    the one-clip ones on its LDS-DMA ring form (k_gemm_p), with epilogues
+    staged through LDS; WMI_GEMM_G=0 / WMI_GEMM_P=0 select the
+    register-staged kernel (k_gemm), WMI_GEMM_EPI=0 the per-lane epilogue
+    stores.  All give
     bitwise the same encoder output and cross K / V (one MFMA order; one
-    f32 -> f16 rounding sequence, f16_rt), at 8 clips (k_gemm_g) and one clip
-    (k_gemm's smaller tiles)."""
+    f32 -> f16 rounding sequence, f16_rt), at 8 clips and one clip."""
     path = synth.model_path("base", model_cache)
     clips = [synth.synth_pcm_f32(30.0, 1400 + i) for i in range(8)]
     for nc in (8, 1):
         ref = None
-        for env in ({}, {"WMI_GEMM_EPI": "0"}, {"WMI_GEMM_G": "0"}, {"WMI_GEMM_G": "0", "WMI_GEMM_EPI": "0"}):
+        for env in ({}, {"WMI_GEMM_EPI": "0"}, {"WMI_GEMM_G": "0"}, {"WMI_GEMM_G": "0", "WMI_GEMM_EPI": "0"},
+                    {"WMI_GEMM_P": "0"}, {"WMI_GEMM_P": "0", "WMI_GEMM_EPI": "0"}):
             ctx = _ctx_with_env(wmi, path, env, max_clips=nc)
             try:
                 ctx.pcm_to_mel_batch(clips[:nc])

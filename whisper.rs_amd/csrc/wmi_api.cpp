@@ -2208,6 +2208,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     knob("WMI_ENC_ATTN_NW", tn.enc_attn_nw, 0);
     knob("WMI_GEMM_G", tn.gemm_g, 0);
     knob("WMI_GEMM_EPI", tn.epi_staged, 0);
+    knob("WMI_GEMM_P", tn.gemm_p, 0);
     knob("WMI_MEL_G", tn.mel_g, 0);
     *out = ctx.release();
     return WMI_OK;
@@ -2773,8 +2774,8 @@ int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes) {
         case 9: src = ctx->dopart; have = R * (size_t)ctx->n_chunks_max * n * 4; break;
         case 10: {  // host: this context's tuning knobs (struct Tune, int32 fields in order)
             const Tune &t = ctx->tune;
-            const int32_t v[9] = {t.logits_cap, t.logits_g, t.gemv_nw, t.xattn_rows, t.graph_steps,
-                                  t.enc_attn_nw, t.gemm_g, t.mel_g, t.epi_staged};
+            const int32_t v[10] = {t.logits_cap, t.logits_g, t.gemv_nw, t.xattn_rows, t.graph_steps,
+                                   t.enc_attn_nw, t.gemm_g, t.mel_g, t.epi_staged, t.gemm_p};
             memcpy(out, v, std::min(sizeof v, bytes));
             return WMI_OK;
         }

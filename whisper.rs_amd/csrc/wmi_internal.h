@@ -83,6 +83,7 @@ struct Tune {
     // than MEL_FC_MAX non-zero weights takes anyway; tested bitwise equal
     int mel_g = 1;
     int epi_staged = 1;     // WMI_GEMM_EPI: GEMM epilogues through LDS, 16 / 8-byte stores (0: per-lane 2 / 4-byte stores)
+    int gemm_p = 1;         // WMI_GEMM_P: one-clip encoder GEMMs on k_gemm_p (LDS-DMA ring); 0: k_gemm
 };
 // (fixed since round 5; their alternatives measured slower and are removed:
 // chain logits grid cap at K <= 512, cooperative chain cross-attention up to

@@ -790,6 +790,161 @@ __global__ __launch_bounds__(256) void k_gemm_g(GemmArgs a) {
         }
 }
 
+// ---- one-clip GEMM (M ~ 1500: 96-384 workgroups, about one per CU): k_gemm's
+// BM x BN tiles and MFMA order, but the k stages (64 k) arrive through an
+// NST-deep ring of LDS-DMA buffers, NST - 1 stages in flight.  k_gemm holds
+// one stage in flight in registers, so with a single workgroup per CU each
+// stage cost one load latency (mlp.2 at K = 2048: 32 stages, 23.5 us).  The
+// wait is a counted vmcnt + a raw s_barrier in one asm statement:
+// __syncthreads() would drain the DMAs still in flight (vmcnt(0)).  The stage
+// issued at step kt (clamped to the last stage past the end) goes to the
+// buffer read at step kt - 1, which every wave has finished with once it has
+// passed step kt's barrier.  LDS image and swizzle as k_gemm_g's (128-byte
+// rows, chunk c of row r at c ^ ((r >> 1) & 7)); rows past M / N read the
+// last row, whose outputs are never stored.  Every output is bitwise k_gemm's.
+template <int BM, int BN, int NST, int EPI, bool CONV>
+__global__ __launch_bounds__(256) void k_gemm_p(GemmArgs a) {
+    constexpr int TM = BM / 64, TN = BN / 64;
+    constexpr int PA = BM / 32, PB = BN / 32, P = PA + PB;  // 1 KB DMA instructions per wave per stage
+    constexpr int SB = (BM + BN) * 128;                     // bytes per stage
+    extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
+    const int nwg = nbm * nbn;
+    int bid = blockIdx.x;
+    {  // XCD-aware bijective tile order (as k_gemm)
+        const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+    }
+    const int bn = bid % nbn, bm = bid / nbn;
+    const int m0 = bm * BM, n0 = bn * BN;
+    const int nk = a.K / 64;
+    const uint16_t *srcA[PA], *srcB[PB];
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+        const int row = (wave * PA + j) * 8 + (lane >> 3), lc = gg_chunk(row, lane & 7);
+        const int m = m0 + row < a.M ? m0 + row : a.M - 1;
+        if constexpr (CONV) {
+            const int b = m / a.conv_tout, t = m - b * a.conv_tout;
+            srcA[j] = a.A + ((int64_t)b * (a.conv_tin + 2) + (int64_t)t * a.conv_stride) * a.conv_cp + lc * 8;
+        } else {
+            srcA[j] = a.A + (int64_t)m * a.lda + lc * 8;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+        const int row = (wave * PB + j) * 8 + (lane >> 3), lc = gg_chunk(row, lane & 7);
+        const int n = n0 + row < a.N ? n0 + row : a.N - 1;
+        srcB[j] = a.B + (int64_t)n * a.K + lc * 8;
+    }
+    typedef __attribute__((address_space(3))) void lds_t;
+    // (implicit-GEMM conv: a row's 3 taps x Cp channels are contiguous, k = tap * Cp + c)
+    auto stage = [&](int buf, int kt) {
+        unsigned char *As = psm + buf * SB, *Bs = As + BM * 128;
+#pragma unroll
+        for (int j = 0; j < PA; ++j)
+            __builtin_amdgcn_global_load_lds((const void *)(srcA[j] + kt * 64), (lds_t *)(As + (wave * PA + j) * 1024), 16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < PB; ++j)
+            __builtin_amdgcn_global_load_lds((const void *)(srcB[j] + kt * 64), (lds_t *)(Bs + (wave * PB + j) * 1024), 16, 0, 0);
+    };
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+    for (int s = 0; s < NST - 1; ++s) stage(s, s < nk ? s : nk - 1);
+    for (int kt = 0; kt < nk; ++kt) {
+        // stage kt landed (this wave's DMAs; the barrier: every wave's)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((NST - 2) * P) : "memory");
+        {
+            const int kn = kt + NST - 1;
+            stage(kn % NST, kn < nk ? kn : nk - 1);
+        }
+        const unsigned char *As = psm + (kt % NST) * SB, *Bs = As + BM * 128;
+        // the whole stage's fragments first (one LDS latency a stage, not four)
+        half8 af[4][TM], bf[4][TN];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int c = 2 * ks + lh;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int r = wm * (BM / 2) + i * 32 + lr;
+                af[ks][i] = *(const half8 *)(As + r * 128 + gg_chunk(r, c) * 16);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int r = wn * (BN / 2) + j * 32 + lr;
+                bf[ks][j] = *(const half8 *)(Bs + r * 128 + gg_chunk(r, c) * 16);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink each read to its MFMA)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[ks][i], bf[ks][j], acc[i][j], 0, 0, 0);
+    }
+    // the clamped stages past the end are still landing: drain before the
+    // staged epilogue reuses the ring
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (epi_staged_ok<EPI, BN>(a)) {
+        gemm_epi_staged<EPI, BM, BN>(a, acc, (float *)psm, m0, n0);
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * (BN / 2) + j * 32 + lr;
+            const int mb = m0 + wm * (BM / 2) + i * 32 + 4 * lh;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                gemm_epi4<EPI>(a, mb + 8 * g, n, v);
+            }
+        }
+}
+
+template <int BM, int BN, int NST, bool CONV>
+static hipError_t gemm_p_dispatch(hipStream_t s, int epi, const GemmArgs &a) {
+    const int nwg = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+    constexpr size_t ring = (size_t)NST * (BM + BN) * 128, stg = epi_stage_bytes<BM, BN>();
+    constexpr size_t lds = ring > stg ? ring : stg;
+#define GEMMP_CASE(E)                                                                        \
+    case E: {                                                                               \
+        hipError_t e = allow_lds(k_gemm_p<BM, BN, NST, E, CONV>, lds);                     \
+        if (e != hipSuccess) return e;                                                      \
+        hipLaunchKernelGGL((k_gemm_p<BM, BN, NST, E, CONV>), dim3(nwg), dim3(256), lds, s, a); \
+        break;                                                                              \
+    }
+    if constexpr (CONV) {
+        switch (epi) {
+            GEMMP_CASE(EPI_CONV1)
+            GEMMP_CASE(EPI_CONV2PE)
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (epi) {
+            GEMMP_CASE(EPI_F32)
+            GEMMP_CASE(EPI_RESID)
+            GEMMP_CASE(EPI_GELU16)
+            GEMMP_CASE(EPI_QKV)
+            GEMMP_CASE(EPI_CROSSKV)
+            default: return hipErrorInvalidValue;
+        }
+    }
+#undef GEMMP_CASE
+    return hipGetLastError();
+}
+
 template <bool CONV>
 static hipError_t gemm_g_dispatch(hipStream_t s, int epi, const GemmArgs &a) {
     const int nwg = ((a.M + 127) / 128) * ((a.N + 127) / 128);
@@ -869,6 +1024,16 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a0) {
     // (128 k a stage for the smaller tiles — half the k steps of these
     // latency-bound one-clip GEMMs, the same MFMA order — measured slower:
     // 1-clip encoder 0.685 -> 0.726 ms, profiles/r06/gemm_bk128_ab_REJECTED.txt)
+    // the one-clip shapes: the same tiles with the k stages on an LDS-DMA ring
+    // (1-clip encode 0.637 -> 0.541 ms, bitwise equal; measured and not kept:
+    // 64 x 64 tiles throughout 0.547, rings of 4 / 6 stages at one workgroup a
+    // CU 0.587 vs 0.531, the one-clip cross K / V on the ring instead of
+    // k_gemm_g 0.533 vs 0.531: profiles/r06/gemm_p_ab.txt)
+    if (tune_of(a.tune).gemm_p && k64 && t128 < 240) {
+        if (t12864 >= 240)
+            return a.conv ? gemm_p_dispatch<128, 64, 3, true>(s, epi, a) : gemm_p_dispatch<128, 64, 3, false>(s, epi, a);
+        return a.conv ? gemm_p_dispatch<64, 64, 4, true>(s, epi, a) : gemm_p_dispatch<64, 64, 4, false>(s, epi, a);
+    }
     if (a.conv) {
         if (t128 >= 240) return gemm_dispatch_epi<128, 128, GBK, true>(s, epi, a);
         if (t12864 >= 240) return k64 ? gemm_dispatch_epi<128, 64, 64, true>(s, epi, a)
