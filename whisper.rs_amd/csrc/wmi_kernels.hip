@@ -1027,8 +1027,9 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a0) {
     // the one-clip shapes: the same tiles with the k stages on an LDS-DMA ring
     // (1-clip encode 0.637 -> 0.541 ms, bitwise equal; measured and not kept:
     // 64 x 64 tiles throughout 0.547, rings of 4 / 6 stages at one workgroup a
-    // CU 0.587 vs 0.531, the one-clip cross K / V on the ring instead of
-    // k_gemm_g 0.533 vs 0.531: profiles/r06/gemm_p_ab.txt)
+    // CU 0.587 vs 0.531, 6 / 8 stages for the <= 256-tile 64 x 64 grids 0.567 /
+    // 0.571 vs 0.559, the one-clip cross K / V on the ring instead of k_gemm_g
+    // 0.533 vs 0.531: profiles/r06/gemm_p_ab.txt)
     if (tune_of(a.tune).gemm_p && k64 && t128 < 240) {
         if (t12864 >= 240)
             return a.conv ? gemm_p_dispatch<128, 64, 3, true>(s, epi, a) : gemm_p_dispatch<128, 64, 3, false>(s, epi, a);
