@@ -1019,6 +1019,11 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a0) {
     // large M: the LDS-DMA kernel (bitwise the same outputs)
     // (8-clip encoder 3.10 -> 3.00 ms: conv2 84.6 -> 71.3, Wo 39.7 -> 34.8,
     // mlp.2 77.0 -> 60.2 us; QKV and mlp.0 unchanged)
+    // one clip (M <= 2048): every 64-k shape on k_gemm_p's LDS-DMA ring — the
+    // same tiles' MFMA order, the k stages 2-3 deep (below); the 128 x 128
+    // k_gemm_g keeps the 8-clip shapes
+    if (tune_of(a.tune).gemm_p && k64 && a.M <= 2048 && t128 >= 240)
+        return a.conv ? gemm_p_dispatch<128, 64, 3, true>(s, epi, a) : gemm_p_dispatch<128, 64, 3, false>(s, epi, a);
     if (t128 >= GEMM_G_MIN_TILES && tune_of(a.tune).gemm_g && a.K % 64 == 0 && (!a.conv || a.conv_cp % 64 == 0))
         return a.conv ? gemm_g_dispatch<true>(s, epi, a) : gemm_g_dispatch<false>(s, epi, a);
     // (128 k a stage for the smaller tiles — half the k steps of these
@@ -1028,8 +1033,10 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a0) {
     // (1-clip encode 0.637 -> 0.541 ms, bitwise equal; measured and not kept:
     // 64 x 64 tiles throughout 0.547, rings of 4 / 6 stages at one workgroup a
     // CU 0.587 vs 0.531, 6 / 8 stages for the <= 256-tile 64 x 64 grids 0.567 /
-    // 0.571 vs 0.559, the one-clip cross K / V on the ring instead of k_gemm_g
-    // 0.533 vs 0.531: profiles/r06/gemm_p_ab.txt)
+    // 0.571 vs 0.559; the one-clip shapes of >= 240 128 x 128 tiles on the
+    // ring instead of k_gemm_g: small 1.852 -> 1.813 ms, base 0.557 -> 0.548
+    // (its cross K / V; 0.533 vs 0.531 in an earlier session): kept, above;
+    // profiles/r06/gemm_p_ab.txt)
     if (tune_of(a.tune).gemm_p && k64 && t128 < 240) {
         if (t12864 >= 240)
             return a.conv ? gemm_p_dispatch<128, 64, 3, true>(s, epi, a) : gemm_p_dispatch<128, 64, 3, false>(s, epi, a);
