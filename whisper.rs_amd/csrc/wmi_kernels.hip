@@ -1036,6 +1036,7 @@ hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a0) {
     // 0.571 vs 0.559; the one-clip shapes of >= 240 128 x 128 tiles on the
     // ring instead of k_gemm_g: small 1.852 -> 1.813 ms, base 0.557 -> 0.548
     // (its cross K / V; 0.533 vs 0.531 in an earlier session): kept, above;
+    // the 8-clip shapes on the ring instead: 2.346 -> 2.360 ms, not kept;
     // profiles/r06/gemm_p_ab.txt)
     if (tune_of(a.tune).gemm_p && k64 && t128 < 240) {
         if (t12864 >= 240)
