@@ -246,7 +246,7 @@ int wmi_get_checksums(const wmi_context *ctx, float *out5);
  * [8][n_text_state] f32, 2 = logits [8][n_vocab] f32 (the persistent
  * decoder fills them only with WMI_PERSIST_LOGITS=1), 3 = the persistent
  * decoder's exchange block (8-byte {tag, value} granules), 4-9 = decoder
- * chain scratch, 10 = this context's tuning knobs (9 int32, host copy; the
+ * chain scratch, 10 = this context's tuning knobs (11 int32, host copy; the
  * WMI_* environment is read once per context at wmi_init_from_file),
  * 11 = decodes re-run on the kernel chain (int32, host), 12 = the encoder
  * residual stream, 13 = every position's logits [n_text_ctx][rows][n_vocab]
@@ -255,7 +255,9 @@ int wmi_get_checksums(const wmi_context *ctx, float *out5);
  * last beam search's parent slots / tokens [n_text_ctx][8] int32 (its last
  * clip), 16 = the rows of 13 (int32, host: max(8, max_clips)), 17 = the
  * persistent decoder's grid per row count (int32 [9], host; -1 = not sized
- * yet, 0 = kernel chain). */
+ * yet, 0 = kernel chain), 18 = the encoder GELU epilogues' threshold (f32,
+ * host: f16 inputs at or above it are computed, the rest read ggml's table;
+ * +inf with WMI_GELU_CALC=0). */
 int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes);
 
 /* ---- parity getters (copy device results into caller-owned buffers) --- */

@@ -23,12 +23,13 @@ iters = int(sys.argv[4]) if len(sys.argv) > 4 else 20
 path = synth.model_path(model)
 pcm = [synth.synth_pcm_f32(30.0, 1234 + i) for i in range(clips)]
 settings = tuple(os.environ.get("GEMM_P_SETTINGS", "0,1").split(","))
+VAR = os.environ.get("AB_VAR", "WMI_GEMM_P")  # the knob compared (WMI_GELU_CALC: the GELU epilogues)
 ctxs = {}
 for g in settings:
-    os.environ["WMI_GEMM_P"] = g
+    os.environ[VAR] = g
     ctxs[g] = wmi.WhisperContext.new(path, device=0, max_clips=clips)
     ctxs[g].pcm_to_mel_batch(pcm)
-del os.environ["WMI_GEMM_P"]
+del os.environ[VAR]
 ref = None
 for g in settings:
     ctx = ctxs[g]
@@ -38,7 +39,7 @@ for g in settings:
         ref = got
     else:
         same = all(np.array_equal(x, y) for a, b in zip(ref, got) for x, y in zip(a, b))
-        print(f"WMI_GEMM_P={g}: bitwise equal to WMI_GEMM_P={settings[0]}: {same}", flush=True)
+        print(f"{VAR}={g}: bitwise equal to {VAR}={settings[0]}: {same}", flush=True)
         if not same:
             sys.exit(1)
 times = {g: [] for g in settings}
@@ -52,9 +53,9 @@ for r in range(rounds):
             ctx.encode(1, 0)
             t.append(ctx.timings()["encode_ms"])
         times[g].append(float(np.median(t)))
-    print(f"round {r}: " + ", ".join(f"P={g} {times[g][-1]:.4f} ms" for g in settings), flush=True)
+    print(f"round {r}: " + ", ".join(f"{VAR}={g} {times[g][-1]:.4f} ms" for g in settings), flush=True)
 for g in settings:
-    print(f"{model} x{clips} WMI_GEMM_P={g}: encode median over rounds {np.median(times[g]):.4f} ms "
+    print(f"{model} x{clips} {VAR}={g}: encode median over rounds {np.median(times[g]):.4f} ms "
           f"(rounds {', '.join(f'{x:.4f}' for x in times[g])})", flush=True)
 for c in ctxs.values():
     c.close()

@@ -633,7 +633,9 @@ def test_encoder_gemm_paths_bitwise(wmi, model_cache):
     the one-clip ones on its LDS-DMA ring form (k_gemm_p), with epilogues
     staged through LDS; WMI_GEMM_G=0 / WMI_GEMM_P=0 select the
     register-staged kernel (k_gemm), WMI_GEMM_EPI=0 the per-lane epilogue
-    stores.  All give
+    stores, WMI_GELU_CALC=0 the GELU table for every input (by default the
+    epilogues compute the table's values above the context's scanned
+    threshold).  All give
     bitwise the same encoder output and cross K / V (one MFMA order; one
     f32 -> f16 rounding sequence, f16_rt), at 8 clips and one clip."""
     path = synth.model_path("base", model_cache)
@@ -641,9 +643,18 @@ def test_encoder_gemm_paths_bitwise(wmi, model_cache):
     for nc in (8, 1):
         ref = None
         for env in ({}, {"WMI_GEMM_EPI": "0"}, {"WMI_GEMM_G": "0"}, {"WMI_GEMM_G": "0", "WMI_GEMM_EPI": "0"},
-                    {"WMI_GEMM_P": "0"}, {"WMI_GEMM_P": "0", "WMI_GEMM_EPI": "0"}):
+                    {"WMI_GEMM_P": "0"}, {"WMI_GEMM_P": "0", "WMI_GEMM_EPI": "0"}, {"WMI_GELU_CALC": "0"},
+                    {"WMI_GELU_CALC": "0", "WMI_GEMM_EPI": "0"}):
             ctx = _ctx_with_env(wmi, path, env, max_clips=nc)
             try:
+                # the GELU epilogues' threshold: computed at or above it, the
+                # table below (+inf with WMI_GELU_CALC=0); the device's tanhf
+                # rounds to the table's f16 for every input (the scan: -inf)
+                gmin = float(np.frombuffer(ctx.debug_read(18, 4), np.float32)[0])
+                if env.get("WMI_GELU_CALC") == "0":
+                    assert gmin == np.inf
+                else:
+                    assert gmin < 0.0, gmin
                 ctx.pcm_to_mel_batch(clips[:nc])
                 ctx.encode(1, 0)
                 got = [(ctx.encoder_out(i), *ctx.cross_kv(i)) for i in range(nc)]

@@ -306,6 +306,7 @@ struct wmi_context {
     int n_fallbacks = 0;              // decodes re-run on the kernel chain after a persistent exchange timeout
     PersistLayer *d_players = nullptr;
     uint32_t *d_expfb = nullptr;       // exp fallback list of the persistent decoder [64] + count
+    float gelu_min = __builtin_huge_valf();  // encoder GELU epilogues compute f16 inputs >= this (k_gelu_scan)
     int n_expfb = 0;
     uint64_t *d_xg = nullptr;         // exchange block (persist_layout at n_audio_ctx)
     size_t xg_bytes = 0;
@@ -322,6 +323,9 @@ struct wmi_context {
     int32_t *d_dbar = nullptr, *d_dshape = nullptr;
     size_t gather_cap = 0;
 };
+
+// the encoder GELU epilogues' threshold under the context's WMI_GELU_CALC knob
+static float gelu_min_of(const wmi_context *ctx) { return ctx->tune.gelu_calc ? ctx->gelu_min : __builtin_huge_valf(); }
 
 namespace {
 
@@ -972,6 +976,28 @@ int upload_model(wmi_context *ctx, ParsedModel &pm) {
             HIPCHK(ctx, hipMemcpy(ctx->d_expfb, tab, 66 * 4, hipMemcpyHostToDevice));
         }
     }
+    // the encoder GELU epilogues' threshold: every f16 input above the
+    // largest one whose computed value differs from the table (the scan is
+    // exhaustive over the 63 488 finite inputs, so results stay the table's)
+    {
+        uint32_t *d_mo = nullptr, r[2] = {0, 0};
+        HIPCHK(ctx, hipMalloc(&d_mo, 8));
+        HIPCHK(ctx, hipMemset(d_mo, 0, 8));
+        HIPCHK(ctx, launch_gelu_scan(nullptr, ctx->gelu_tab, d_mo));
+        HIPCHK(ctx, hipMemcpy(r, d_mo, 8, hipMemcpyDeviceToHost));
+        HIPCHK(ctx, hipFree(d_mo));
+        const uint32_t mo = r[0];
+        if (r[1] != 63490u) {  // (not seen) an incomplete scan proves nothing: the table everywhere
+            ctx->gelu_min = __builtin_huge_valf();
+        } else if (!mo) {  // (measured: the device tanhf rounds to the table's f16 for every input)
+            ctx->gelu_min = -__builtin_huge_valf();
+        } else {
+            const uint32_t u = (mo & 0x80000000u) ? (mo & 0x7fffffffu) : ~mo;  // unord_f32
+            float xm;
+            memcpy(&xm, &u, 4);
+            ctx->gelu_min = nextafterf(xm, __builtin_huge_valf());
+        }
+    }
     if (ctx->wf32) ctx->use_persist = false;  // f32 matrices: the kernel chain with the f32 GEMVs
     return WMI_OK;
 }
@@ -1217,7 +1243,7 @@ int run_encode(wmi_context *ctx, int mel_offset) {
     g.A32 = ctx->xconv32; g.B32 = W32(ctx->conv1_w);
     g.M = B * T2; g.N = n; g.K = 3 * ctx->Cp1;
     g.conv = 1; g.conv_stride = 1; g.conv_tin = T2; g.conv_cp = ctx->Cp1; g.conv_tout = T2;
-    g.out16 = ctx->g1; g.ldo = n; g.gelu_tab = ctx->gelu_tab; g.T = T2;
+    g.out16 = ctx->g1; g.ldo = n; g.gelu_tab = ctx->gelu_tab; g.T = T2; g.gelu_min = gelu_min_of(ctx);
     g.tune = &ctx->tune;
 
     HIPCHK(ctx, launch_gemm(s, EPI_CONV1, g));
@@ -1226,7 +1252,7 @@ int run_encode(wmi_context *ctx, int mel_offset) {
     g.A = ctx->g1; g.B = ctx->conv2_w; g.bias = ctx->conv2_b; g.B32 = W32(ctx->conv2_w);
     g.M = B * T; g.N = n; g.K = 3 * n;
     g.conv = 1; g.conv_stride = 2; g.conv_tin = T2; g.conv_cp = n; g.conv_tout = T;
-    g.out32 = ctx->h; g.ldo = n; g.gelu_tab = ctx->gelu_tab; g.pe = ctx->e_pe; g.T = T;
+    g.out32 = ctx->h; g.ldo = n; g.gelu_tab = ctx->gelu_tab; g.pe = ctx->e_pe; g.T = T; g.gelu_min = gelu_min_of(ctx);
     g.tune = &ctx->tune;
 
     HIPCHK(ctx, launch_gemm(s, EPI_CONV2PE, g));
@@ -1257,7 +1283,7 @@ int run_encode(wmi_context *ctx, int mel_offset) {
         g = GemmArgs{};
         g.A = ctx->xln; g.lda = n; g.B = e.w0; g.bias = e.b0; g.M = M; g.N = 4 * n; g.K = n;
         g.A32 = ctx->xln32; g.B32 = W32(e.w0);
-        g.out16 = ctx->hid; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
+        g.out16 = ctx->hid; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab; g.gelu_min = gelu_min_of(ctx);
         g.tune = &ctx->tune;
 
         HIPCHK(ctx, launch_gemm(s, EPI_GELU16, g));
@@ -2209,6 +2235,7 @@ static int wmi_init_from_file_impl(const char *path, int device, int max_clips, 
     knob("WMI_GEMM_G", tn.gemm_g, 0);
     knob("WMI_GEMM_EPI", tn.epi_staged, 0);
     knob("WMI_GEMM_P", tn.gemm_p, 0);
+    knob("WMI_GELU_CALC", tn.gelu_calc, 0);
     knob("WMI_MEL_G", tn.mel_g, 0);
     *out = ctx.release();
     return WMI_OK;
@@ -2680,7 +2707,7 @@ int wmi_bench_kernel(wmi_context *ctx, int which, int iters, wmi_kernel_bench *o
             GemmArgs g{};
             const EncLayerDev &e = ctx->enc[0];
             g.A = ctx->xln; g.lda = n; g.B = e.w0; g.bias = e.b0; g.M = M; g.N = 4 * n; g.K = n;
-            g.out16 = ctx->hid; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab;
+            g.out16 = ctx->hid; g.ldo = 4 * n; g.gelu_tab = ctx->gelu_tab; g.gelu_min = gelu_min_of(ctx);
             g.tune = &ctx->tune;
 
             HIPCHK(ctx, launch_gemm(s, EPI_GELU16, g));
@@ -2774,8 +2801,8 @@ int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes) {
         case 9: src = ctx->dopart; have = R * (size_t)ctx->n_chunks_max * n * 4; break;
         case 10: {  // host: this context's tuning knobs (struct Tune, int32 fields in order)
             const Tune &t = ctx->tune;
-            const int32_t v[10] = {t.logits_cap, t.logits_g, t.gemv_nw, t.xattn_rows, t.graph_steps,
-                                   t.enc_attn_nw, t.gemm_g, t.mel_g, t.epi_staged, t.gemm_p};
+            const int32_t v[11] = {t.logits_cap, t.logits_g, t.gemv_nw, t.xattn_rows, t.graph_steps,
+                                   t.enc_attn_nw, t.gemm_g, t.mel_g, t.epi_staged, t.gemm_p, t.gelu_calc};
             memcpy(out, v, std::min(sizeof v, bytes));
             return WMI_OK;
         }
@@ -2798,6 +2825,11 @@ int wmi_debug_read(const wmi_context *ctx, int which, void *out, size_t bytes) {
             return WMI_OK;
         }
         case 12: src = ctx->h; have = (size_t)ctx->enc_clips * ctx->enc_T * ctx->hp.n_audio_state * 4; break;  // encoder residual stream
+        case 18: {  // host: the encoder GELU epilogues' threshold (float; +inf: table only)
+            const float v = gelu_min_of(ctx);
+            memcpy(out, &v, std::min(sizeof v, bytes));
+            return WMI_OK;
+        }
         case 11: {  // host: decodes re-run on the kernel chain after a persistent exchange timeout
             const int32_t v = ctx->n_fallbacks;
             memcpy(out, &v, std::min(sizeof v, bytes));

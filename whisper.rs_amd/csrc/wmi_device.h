@@ -181,6 +181,27 @@ __device__ __forceinline__ unsigned long long rows_max_u64(unsigned long long k)
     return kstep<32>(k);
 }
 __device__ __forceinline__ float gelu_lookup(const uint16_t *tab, float x) { return h2f_bits(tab[f2h_bits(x)]); }
+// ggml's table_gelu_f16 entry for f16 input f, computed: the host builds the
+// table with exactly this f32 expression (build_tables, wmi_api.cpp), one
+// rounding per operation.  The device's tanhf is within an ulp of the host's,
+// which moves the f16 result only where 1 + tanh cancels (x < -1.8: 235 of
+// the 63 488 finite inputs, scripts/gelu_probe.py), so the encoder GEMM
+// epilogues compute it for inputs >= gmin — the context's exhaustive device
+// scan (k_gelu_scan) puts gmin just above the largest input that differs —
+// and read the table below (+inf: the table everywhere).  The table's 128 KB
+// of random 2-byte gathers were what bounded the mlp.0 epilogue.
+__device__ __forceinline__ uint16_t gelu_calc_bits(float f) {
+    const float t = tanhf(0.79788456080286535587989211986876f * f * (1.0f + 0.044715f * f * f));
+    return f2h_bits(0.5f * f * (1.0f + t));
+}
+__device__ __forceinline__ uint16_t gelu_bits(const uint16_t *tab, float x, float gmin) {
+    const uint16_t h = f2h_bits(x);
+    const float f = h2f_bits(h);
+    uint16_t r;
+    if (f >= gmin) r = gelu_calc_bits(f);  // (NaN inputs fail the compare: table)
+    else r = tab[h];
+    return r;
+}
 
 // ggml's table_exp_f16 entry for a non-positive f16 argument, computed:
 // f16((float)exp((double)x)) — the host builds the table with exactly this

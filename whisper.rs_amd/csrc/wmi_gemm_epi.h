@@ -56,14 +56,15 @@ __device__ __forceinline__ void gemm_epi4(const GemmArgs &a, int m, int n, const
             float *p = a.out32 + (int64_t)mm * a.ldo + n;
             *p = (v[r] + bias) + *p;
         } else if (EPI == EPI_GELU16) {
-            a.out16[(int64_t)mm * a.ldo + n] = a.gelu_tab[f2h_bits(v[r] + bias)];
+            a.out16[(int64_t)mm * a.ldo + n] = gelu_bits(a.gelu_tab, v[r] + bias, a.gelu_min);
         } else if (EPI == EPI_CONV1) {
             const int b = mm / a.T, t = mm - b * a.T;
-            a.out16[((int64_t)b * (a.T + 2) + t + 1) * a.ldo + n] = a.gelu_tab[f2h_bits(v[r] + bias)];
+            a.out16[((int64_t)b * (a.T + 2) + t + 1) * a.ldo + n] = gelu_bits(a.gelu_tab, v[r] + bias, a.gelu_min);
         } else if (EPI == EPI_CONV2PE) {
             const int b = mm / a.T, t = mm - b * a.T;
             (void)b;
-            a.out32[(int64_t)mm * a.ldo + n] = a.pe[(int64_t)t * a.ldo + n] + gelu_lookup(a.gelu_tab, v[r] + bias);
+            a.out32[(int64_t)mm * a.ldo + n] =
+                a.pe[(int64_t)t * a.ldo + n] + h2f_bits(gelu_bits(a.gelu_tab, v[r] + bias, a.gelu_min));
         } else if (EPI == EPI_CROSSKV) {
             const int ns = a.n_state;
             const int l = n / (2 * ns), rr = n - l * 2 * ns;

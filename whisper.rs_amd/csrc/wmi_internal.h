@@ -83,6 +83,7 @@ struct Tune {
     // than MEL_FC_MAX non-zero weights takes anyway; tested bitwise equal
     int mel_g = 1;
     int epi_staged = 1;     // WMI_GEMM_EPI: GEMM epilogues through LDS, 16 / 8-byte stores (0: per-lane 2 / 4-byte stores)
+    int gelu_calc = 1;      // WMI_GELU_CALC: encoder GELU epilogues compute the table's values above the scanned threshold (0: table only)
     int gemm_p = 1;         // WMI_GEMM_P: one-clip encoder GEMMs on k_gemm_p (LDS-DMA ring); 0: k_gemm
 };
 // (fixed since round 5; their alternatives measured slower and are removed:
@@ -104,6 +105,7 @@ struct GemmArgs {
     uint16_t *out16;
     int ldo;
     const uint16_t *gelu_tab;
+    float gelu_min = __builtin_huge_valf();  // GELU epilogues compute inputs >= gelu_min (gelu_bits), +inf: table only
     const float *pe;    // EPI_CONV2PE: [T][N]
     int T;              // rows per clip (for b/t split)
     // EPI_QKV
@@ -120,6 +122,10 @@ struct GemmArgs {
     int epi_staged;     // set by launch_gemm from the context's knob (Tune::epi_staged)
 };
 hipError_t launch_gemm(hipStream_t s, int epi, const GemmArgs &a);
+// exhaustive scan of gelu_bits' computed path against the table: maxord[0] =
+// the largest ord_f32(f) over f16 inputs f whose computed value differs
+// (0 if none), maxord[1] = the inputs checked (the caller zeroes both)
+hipError_t launch_gelu_scan(hipStream_t s, const uint16_t *gelu_tab, uint32_t *maxord);
 hipError_t launch_gemm32(hipStream_t s, int epi, const GemmArgs &a);  // wmi_f32.hip
 
 // ---- encoder self-attention (ggml flash_attn_f16 semantics, exact softmax) --

@@ -513,10 +513,10 @@ __device__ __forceinline__ void gemm_epi_staged(const GemmArgs &a, const floatx1
             *p = make_float4(x[0] + o.x, x[1] + o.y, x[2] + o.z, x[3] + o.w);
         } else if constexpr (EPI == EPI_GELU16 || EPI == EPI_CONV1) {
             ushort4 g;
-            g.x = a.gelu_tab[f2h_bits(x[0])];
-            g.y = a.gelu_tab[f2h_bits(x[1])];
-            g.z = a.gelu_tab[f2h_bits(x[2])];
-            g.w = a.gelu_tab[f2h_bits(x[3])];
+            g.x = gelu_bits(a.gelu_tab, x[0], a.gelu_min);
+            g.y = gelu_bits(a.gelu_tab, x[1], a.gelu_min);
+            g.z = gelu_bits(a.gelu_tab, x[2], a.gelu_min);
+            g.w = gelu_bits(a.gelu_tab, x[3], a.gelu_min);
             int64_t o = (int64_t)m * a.ldo + n;
             if constexpr (EPI == EPI_CONV1) {
                 const int b = m / a.T, t = m - b * a.T;
@@ -527,8 +527,10 @@ __device__ __forceinline__ void gemm_epi_staged(const GemmArgs &a, const floatx1
             const int t = m - (m / a.T) * a.T;
             const float4 pe = *(const float4 *)(a.pe + (int64_t)t * a.ldo + n);
             *(float4 *)(a.out32 + (int64_t)m * a.ldo + n) =
-                make_float4(pe.x + gelu_lookup(a.gelu_tab, x[0]), pe.y + gelu_lookup(a.gelu_tab, x[1]),
-                            pe.z + gelu_lookup(a.gelu_tab, x[2]), pe.w + gelu_lookup(a.gelu_tab, x[3]));
+                make_float4(pe.x + h2f_bits(gelu_bits(a.gelu_tab, x[0], a.gelu_min)),
+                            pe.y + h2f_bits(gelu_bits(a.gelu_tab, x[1], a.gelu_min)),
+                            pe.z + h2f_bits(gelu_bits(a.gelu_tab, x[2], a.gelu_min)),
+                            pe.w + h2f_bits(gelu_bits(a.gelu_tab, x[3], a.gelu_min)));
         } else if constexpr (EPI == EPI_CROSSKV) {
             const int ns = a.n_state, l = n / (2 * ns), rr = n - l * 2 * ns;
             const int b = m / a.T, t = m - b * a.T;
@@ -788,6 +790,20 @@ __global__ __launch_bounds__(256) void k_gemm_g(GemmArgs a) {
                 gemm_epi4<EPI>(a, mb + 8 * g, n, v);
             }
         }
+}
+
+__global__ void k_gelu_scan(const uint16_t *tab, uint32_t *maxord) {
+    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h > 0xffff) return;
+    const float f = h2f_bits((uint16_t)h);
+    if (f != f) return;  // NaN inputs always take the table
+    if (gelu_calc_bits(f) != tab[h]) atomicMax(maxord, ord_f32(f));
+    atomicAdd(maxord + 1, 1u);  // inputs checked (the host expects all 63 490 non-NaN ones)
+}
+
+hipError_t launch_gelu_scan(hipStream_t s, const uint16_t *gelu_tab, uint32_t *maxord) {
+    hipLaunchKernelGGL(k_gelu_scan, dim3(65536 / 256), dim3(256), 0, s, gelu_tab, maxord);
+    return hipGetLastError();
 }
 
 // ---- one-clip GEMM (M ~ 1500: 96-384 workgroups, about one per CU): k_gemm's
