@@ -692,6 +692,29 @@ def test_split_grid_equals_full_grid(wmi, model_cache):
     np.testing.assert_array_equal(res[0][1], res[1][1])
 
 
+def test_gelu_calc_equals_table_decode(wmi, model_cache):
+    """The persistent decoder's phase H computes GELU where the context's scan
+    allows (gelu_bits) instead of gathering ggml's table: bitwise the ids and
+    every step's logits of the table-only context (WMI_GELU_CALC=0), on the
+    one-row instance and the 8-row split grid, encoder included."""
+    path = synth.model_path("base", model_cache)
+    for nc in (1, 8):
+        clips = [synth.synth_pcm_f32(30.0, 1500 + i) for i in range(nc)]
+        res = []
+        for env in ({}, {"WMI_GELU_CALC": "0"}):
+            ctx = _ctx_with_env(wmi, path, dict(env, WMI_LOGITS_ALL="1"), max_clips=nc)
+            try:
+                ctx.pcm_to_mel_batch(clips)
+                ctx.encode(1, 0)
+                toks = ctx.decode_greedy(40, suppress_eot=True)
+                res.append((toks, ctx.step_logits(len(_prompt(ctx)) + 40 - 1)))
+            finally:
+                ctx.close()
+        for i in range(nc):
+            np.testing.assert_array_equal(res[0][0][i], res[1][0][i])
+        np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
 @pytest.mark.slow
 def test_beam_shared_cross_equals_per_row(wmi, model_cache):
     """C5's beam rows read their clip's cross K / V through one task per (head,

@@ -1639,6 +1639,7 @@ PersistArgs persist_args(wmi_context *ctx, int b0, int B, int G, int feed_len, i
     PersistArgs a{};
     a.layers = ctx->d_players; a.te = ctx->te; a.pe = ctx->d_pe; a.dln_w = ctx->dln_w; a.dln_b = ctx->dln_b;
     a.gelu_tab = ctx->gelu_tab; a.exp_tab = ctx->exp_tab; a.n_exp = ctx->n_exp; a.exp_fb = ctx->d_expfb;
+    a.gelu_min = gelu_min_of(ctx);
     a.kcache = ctx->kcache; a.vcache = ctx->vcache; a.ck = ctx->ck; a.cv = ctx->cv;
     a.L = ctx->dec_layers; a.n = n; a.V = hp.n_vocab; a.B = B; a.T = T; a.tctx = hp.n_text_ctx;
     a.Bt = ctx->enc_clips; a.b0 = b0;

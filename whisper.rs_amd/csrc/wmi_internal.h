@@ -358,6 +358,7 @@ struct PersistArgs {
     const float *pe;             // positional embedding [n_text_ctx][n]
     const float *dln_w, *dln_b;  // final LayerNorm
     const uint16_t *gelu_tab;    // ggml GELU table [65536]
+    float gelu_min = __builtin_huge_valf();  // phase H computes GELU of f16 inputs >= gelu_min (gelu_bits), +inf: table
     const uint16_t *exp_tab;     // ggml exp table, non-positive half [n_exp]
     int n_exp;
     const uint32_t *exp_fb;      // [64] exp fallback list (launch_exp_fallbacks), 0xffffffff-padded
