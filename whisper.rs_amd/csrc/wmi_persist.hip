@@ -1769,10 +1769,18 @@ __global__ __launch_bounds__(PT, 1) void k_dec_persist(PersistArgs a) {
                         const float vn = from_next_row(v), ebn = from_next_row(eb);
                         if (!valid || (q & 1)) return;
                         const uint16_t h0 = f2h_bits(v + eb), h1 = f2h_bits(vn + ebn);
-                        // (computed where the context's scan allows: no dependent table
-                        // gather between the dot and the hand-off)
-                        const uint16_t g0 = gelu_bits(a.gelu_tab, h2f_bits(h0), a.gelu_min);
-                        const uint16_t g1 = gelu_bits(a.gelu_tab, h2f_bits(h1), a.gelu_min);
+                        // (n <= 512: computed where the context's scan allows — no
+                        // dependent table gather between the dot and the hand-off: base
+                        // decode 15.27 -> 15.10 ms; at n = 768 the tanhf cost more than
+                        // the gather, small 34.6 -> 34.8 ms: the table there)
+                        uint16_t g0, g1;
+                        if constexpr (NS <= 512) {
+                            g0 = gelu_bits(a.gelu_tab, h2f_bits(h0), a.gelu_min);
+                            g1 = gelu_bits(a.gelu_tab, h2f_bits(h1), a.gelu_min);
+                        } else {
+                            g0 = a.gelu_tab[h0];
+                            g1 = a.gelu_tab[h1];
+                        }
                         gput(xg + oH + b * (2 * NS) + row / 2, tag, (uint32_t)g0 | ((uint32_t)g1 << 16));
                     });
             }
